@@ -1,0 +1,245 @@
+#!/usr/bin/env python3
+"""Benchmark: device-resident WireGuard transport-data ChaCha20-Poly1305 seal+open.
+
+Metric (BASELINE.json): GiB/s + Mpkt/s device-resident ChaCha20-Poly1305
+seal/open at 1/2/4/8 MI355X.
+
+One step = one batch sealed (in place, header + tag framed) and then opened
+(tag verified, plaintext restored) -- BASELINE config 2 ("64 Ki packets x
+1500 B, one session key, seal then open") on every rank.  Multi-GPU is a
+plain index split with no data-path collective: every rank runs its own
+batch (weak scaling); RCCL is used only for the timing barrier and the
+max-over-ranks reduction.
+
+value = payload bytes through AEAD (seal + open, P bytes each) summed over
+ranks / max-over-ranks wall time of the timed steps, in GiB/s.
+
+Launch (N > 1):  python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+    --master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, MI355X_MICROARCH.md "Chip-level parameters"
+METRIC = "GiB/s + Mpkt/s device-resident ChaCha20-Poly1305 seal/open, 1/2/4/8 MI355X"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--workload", default="cfg2", choices=["cfg2", "cfg3", "cfg4", "cfg5"])
+    ap.add_argument("--lanes", type=int, default=0, help="lanes per packet (0 = auto)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--e2e", action="store_true", help="also time the pinned host->GPU->host path")
+    ap.add_argument("--verify", action="store_true", help="check statuses after the timed region")
+    return ap.parse_args()
+
+
+def cpu_baseline(w, seconds: float, threads: int):
+    """CPU restatement (oracle/, RFC 8439 port) timed on this host's cores.
+
+    The reference's own CPU path (Rust + graviola 0.2.0) cannot be built here
+    (no cargo, crate not vendored), so kind = "port".
+    """
+    from oracle import oracle  # checker / baseline only
+
+    n = min(w.n, 4096)
+    desc = w.desc[:n].copy()
+    base = int(desc["offset"][0])
+    desc["offset"] -= np.uint64(base)
+    span = int(desc["offset"][-1]) + int(desc["len"][-1]) + 32
+    buf = np.zeros(span, np.uint8)
+    oracle.synth_fill(buf, desc, w.inner_len[:n], w.data_seed)
+    od = desc.copy()
+    od["len"] += np.uint32(32)
+    ctr = w.counters[:n]
+    payload = int(desc["len"].astype(np.int64).sum())
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        oracle.seal_batch(w.keys, w.receivers, desc, ctr, buf, nthreads=threads)
+        st, _ = oracle.open_batch(w.keys, od, buf, nthreads=threads)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    assert (st == 0).all()
+    gib = 2 * payload * reps / el / 2**30
+    return {"value": round(gib, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "mpkt_s": round(2 * n * reps / el / 1e6, 4),
+            "sample": f"{n} packets of {w.name} (P={int(desc['len'][0])}) seal+open x{reps} in {el:.1f}s, "
+                      f"{threads} threads, C RFC 8439 restatement (oracle/rg_oracle.c)"}
+
+
+def load_traffic(workload: str):
+    p = os.path.join(REPO, "profiles", f"pmc_{workload}.json")
+    if os.path.exists(p):
+        with open(p) as f:
+            return json.load(f)
+    return None
+
+
+def main():
+    args = parse()
+    import torch
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from rustyguard_amd import workloads
+    from rustyguard_amd.aead import Engine
+    from rustyguard_amd.device import DeviceBatch
+
+    eng = Engine(local)
+    if args.lanes:
+        eng.set_lanes_per_packet(args.lanes)
+    if args.workload == "cfg5":
+        w = workloads.build("cfg5", rank, world)
+    else:
+        w = workloads.build(args.workload)
+    b = DeviceBatch(eng, w)
+    b.fill()
+    stream = torch.cuda.current_stream()
+    torch.cuda.synchronize()
+
+    def step():
+        b.seal(stream=stream)
+        b.open(stream=stream, counters_out=False)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        ev[k][0].record(stream)
+        b.seal(stream=stream)
+        ev[k][1].record(stream)
+        b.open(stream=stream, counters_out=False)
+        ev[k][2].record(stream)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        dist.barrier()
+    seal_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
+    open_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
+    if args.verify:
+        assert (b.status[: w.n] == 0).all().item(), "open failed after timed steps"
+
+    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if dist is not None:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    tmax = float(t.item())
+
+    payload = w.payload_bytes
+    total_payload = 2 * payload * args.steps * world  # seal + open
+    total_pkts = 2 * w.n * args.steps * world
+    value = total_payload / tmax / 2**30
+    seal_alg = 2 * payload + 32 * w.n        # read P, write P + header + tag
+    open_alg = 2 * payload + 33 * w.n        # read P + header + tag, write P + status
+    dominant = "seal" if seal_ms >= open_ms else "open"
+    dom_ms, dom_alg = (seal_ms, seal_alg) if dominant == "seal" else (open_ms, open_alg)
+    achieved = dom_alg / (dom_ms / 1e3) / 1e9
+    pmc = load_traffic(args.workload)
+    traffic = None
+    if pmc and pmc.get(dominant):
+        traffic = pmc[dominant].get("hbm_bytes_per_launch")
+
+    out = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(tmax / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic (SplitMix64 payload, fixed-seed keys; rustyguard_amd/workloads.py)",
+        "config": {"workload": f"{w.name}: {workloads.CONFIGS[w.name]}", "packets_per_gpu": w.n,
+                   "payload_bytes_per_packet": int(w.desc["len"][0]) if w.n else 0,
+                   "mean_payload_bytes": round(payload / max(w.n, 1), 2), "wire_bytes_per_gpu": w.wire_bytes,
+                   "sessions": int(w.meta.get("sessions", 1)), "parallelism": f"split{world} (no collective)",
+                   "lanes_per_packet": eng.lanes_per_packet(w.n)},
+        "mpkt_s": round(total_pkts / tmax / 1e6, 3),
+        "seal_ms": round(seal_ms, 5),
+        "open_ms": round(open_ms, 5),
+        "seal_gib_s": round(payload / (seal_ms / 1e3) / 2**30 * world, 3),
+        "open_gib_s": round(payload / (open_ms / 1e3) / 2**30 * world, 3),
+        "seal_mpkt_s": round(w.n / (seal_ms / 1e3) / 1e6 * world, 3),
+        "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "alg_bytes_per_launch": dom_alg,
+                     "note": "achieved = algorithmic bytes (seal 2P+32, open 2P+33 per packet) / mean launch time "
+                             "(HIP events on the launch stream); see DESIGN.md for the VALU roofline"},
+    }
+    if pmc:
+        out["roofline"]["pmc_source"] = pmc.get("source")
+    if args.e2e and rank == 0:
+        out["e2e"] = e2e_host(eng, w)
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        thr = args.cpu_threads or min(16, os.cpu_count() or 1)
+        out["cpu_baseline"] = cpu_baseline(w, args.cpu_seconds, thr)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def e2e_host(eng, w):
+    """Pinned host -> GPU -> pinned host (rg_*_batch_host), the packets-from-a-socket-buffer rate."""
+    from oracle import oracle  # only to produce the plaintext bytes on the host
+    from rustyguard_amd.aead import host_alloc
+
+    buf = host_alloc(w.buf_bytes)
+    buf[:] = 0
+    oracle.synth_fill(buf, w.desc, w.inner_len, w.data_seed)
+    od = w.open_desc()
+    eng.seal_host(w.keys, w.receivers, w.desc, w.counters, buf)  # warm
+    eng.open_host(w.keys, od, buf)
+    reps = 5
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        eng.seal_host(w.keys, w.receivers, w.desc, w.counters, buf)
+    t1 = time.perf_counter()
+    for _ in range(reps):
+        st, _ = eng.open_host(w.keys, od, buf)
+    t2 = time.perf_counter()
+    assert (st == 0).all()
+    p = w.payload_bytes
+    return {"seal_gib_s": round(p * reps / (t1 - t0) / 2**30, 3), "open_gib_s": round(p * reps / (t2 - t1) / 2**30, 3),
+            "seal_mpkt_s": round(w.n * reps / (t1 - t0) / 1e6, 3), "open_mpkt_s": round(w.n * reps / (t2 - t1) / 1e6, 3),
+            "note": "pinned hipHostMalloc frames, H2D+kernel+D2H over 2 streams, 32 MiB slices"}
+
+
+if __name__ == "__main__":
+    main()

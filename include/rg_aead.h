@@ -1,0 +1,196 @@
+/*
+ * rg_aead.h -- C ABI of the MI355X (gfx950) WireGuard transport-data AEAD
+ * engine.  Drop-in boundary for the reference's hot path:
+ *
+ *   trait CryptoPrimatives (rustyguard-crypto/src/prim.rs:74-111)
+ *     fn chacha20poly1305_enc(key, nonce, aad, payload, tag)      prim.rs:82-88
+ *     fn chacha20poly1305_dec(key, nonce, aad, payload, tag)      prim.rs:89-95
+ *   impl for Core (graviola 0.2.0 underneath)                     prim.rs:179-201
+ *   EncryptionKey::encrypt  (counter++, nonce, seal)              prim.rs:376-399
+ *   DecryptionKey::decrypt  (replay gate, open, mark_seen)        prim.rs:401-437
+ *   AntiReplay::{would_accept, mark_seen}                         rustyguard-utils/src/anti_replay.rs:25-64
+ *   PeerState::force_encrypt + EncryptedMetadata::frame_in_place  rustyguard-core/src/lib.rs:267-297, :450-470
+ *   Sessions::recv_message / decrypt_packet                       rustyguard-core/src/lib.rs:605-681
+ *
+ * The per-packet trait shape would pay a PCIe round trip per packet, so the
+ * primary entry points are BATCHED.  All calls are plain C: no exceptions or
+ * panics cross the ABI, every function returns RG_OK (0) or a negative
+ * rg_status; per-packet outcomes go to a caller-owned status array.
+ *
+ * Buffer contract (same for device and host variants)
+ * ---------------------------------------------------
+ *  buf            one byte arena holding wire frames; frame i starts at
+ *                 desc[i].offset, which must be 16-byte aligned (mirrors
+ *                 AlignedPacket, rustyguard-tun/src/lib.rs:21-24, and the
+ *                 alignment check of rustyguard-core/src/lib.rs:613-615).
+ *  frame layout   [DataHeader 16 B][payload P B][Tag 16 B]   (W = P + 32)
+ *                 DataHeader = {u32 type=4, u32 receiver, u64 counter}, LE
+ *                 (rustyguard-types/src/lib.rs:152-179).
+ *  seal           desc[i].len = P (payload bytes, P % 16 == 0: the
+ *                 assert of rustyguard-core/src/lib.rs:273-277).  The
+ *                 payload is encrypted in place, the header (if receivers
+ *                 != NULL) and the tag are written into the frame
+ *                 (frame_in_place, lib.rs:463-469).  nonce =
+ *                 00000000 || le64(counters[i]) (prim.rs:32-36), AAD empty.
+ *  open           desc[i].len = W (whole frame).  The counter is read from
+ *                 the header, the tag from the last 16 bytes; on success the
+ *                 payload is decrypted in place.  On any failure the frame is
+ *                 left byte-for-byte unchanged.
+ *  keys           key table, nkeys rows of 32 bytes; desc[i].key_idx picks
+ *                 the row (one row per session direction).
+ */
+#ifndef RG_AEAD_H
+#define RG_AEAD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RG_ABI_VERSION 1
+
+typedef struct rg_ctx rg_ctx;
+
+/* 16-byte packet descriptor; device copies must be 16-byte aligned. */
+typedef struct rg_pkt_desc {
+    uint64_t offset;  /* frame offset in buf, multiple of 16 */
+    uint32_t len;     /* seal: payload length P; open: frame length W */
+    uint32_t key_idx; /* key-table row; RG_KEY_SKIP = leave packet untouched */
+} rg_pkt_desc;
+
+#define RG_KEY_SKIP 0xFFFFFFFFu
+
+/* call status */
+typedef enum rg_status {
+    RG_OK = 0,
+    RG_EINVAL = -1,  /* bad argument (null pointer, n too large, ...) */
+    RG_EDEVICE = -2, /* HIP runtime error; rg_last_error() has the text */
+    RG_ENOMEM = -3,
+    RG_ENOTFOUND = -4,
+    RG_EFULL = -5,
+} rg_status;
+
+/* per-packet status (uint8_t), numbering shared with the CPU oracle.
+ * Maps onto rustyguard_core::Error (rustyguard-core/src/lib.rs:416-423). */
+enum rg_pkt_status {
+    RG_PKT_OK = 0,
+    RG_PKT_DECRYPT_ERR = 1, /* Error::DecryptionError: tag mismatch / < 16 B after header */
+    RG_PKT_INVALID = 2,     /* Error::InvalidMessage: W % 16 != 0, W < 16, bad seal desc */
+    RG_PKT_REJECTED = 3,    /* Error::Rejected: replayed/too old counter, no session,
+                               REJECT_AFTER_MESSAGES reached, or RG_KEY_SKIP */
+    RG_PKT_UNALIGNED = 4,   /* Error::Unaligned: frame not 16-byte aligned */
+    RG_PKT_NOT_DATA = 5,    /* type != MSG_DATA: route to the handshake path */
+};
+
+/* ---------------------------------------------------------------- context */
+
+int rg_abi_version(void);
+/* Create a context bound to HIP device `device` (one per process/GPU). */
+int rg_create(int device, rg_ctx **out);
+void rg_destroy(rg_ctx *ctx);
+/* Text of the last error on this thread ("" if none). */
+const char *rg_last_error(void);
+
+/* --------------------------------------- device-resident batch (async) */
+/* Every pointer is device memory; work is enqueued on `stream`
+ * (hipStream_t, NULL = legacy default stream) and the call returns without
+ * synchronising.  status/counters_out may be NULL for seal.  The kernels
+ * bounds-check every descriptor against buf_len and never touch memory
+ * outside [buf, buf + buf_len). */
+int rg_seal_batch_dev(rg_ctx *ctx, const uint8_t *keys, const uint32_t *receivers, uint32_t nkeys,
+                      const rg_pkt_desc *desc, const uint64_t *counters, size_t n, uint8_t *buf, size_t buf_len,
+                      uint8_t *status, void *stream);
+int rg_open_batch_dev(rg_ctx *ctx, const uint8_t *keys, uint32_t nkeys, const rg_pkt_desc *desc, size_t n,
+                      uint8_t *buf, size_t buf_len, uint8_t *status, uint64_t *counters_out, void *stream);
+
+/* Tuning knob: lanes cooperating on one packet (0 = automatic, else 1/2/4). */
+int rg_set_lanes_per_packet(rg_ctx *ctx, int lanes);
+int rg_get_lanes_per_packet(rg_ctx *ctx, size_t n);
+
+/* ----------------------------------------- host-memory batch (blocking) */
+/* Same contract with host pointers: frames are staged H2D, sealed/opened on
+ * the GPU and copied back D2H, pipelined over two streams.  Pinned memory
+ * (rg_host_alloc) gives the full PCIe rate. */
+int rg_seal_batch_host(rg_ctx *ctx, const uint8_t *keys, const uint32_t *receivers, uint32_t nkeys,
+                       const rg_pkt_desc *desc, const uint64_t *counters, size_t n, uint8_t *buf, size_t buf_len,
+                       uint8_t *status);
+int rg_open_batch_host(rg_ctx *ctx, const uint8_t *keys, uint32_t nkeys, const rg_pkt_desc *desc, size_t n,
+                       uint8_t *buf, size_t buf_len, uint8_t *status, uint64_t *counters_out);
+void *rg_host_alloc(size_t bytes);
+void rg_host_free(void *p);
+
+/* ------------------------- per-message drop-in for CryptoPrimatives */
+/* Exactly Core::chacha20poly1305_enc / _dec (prim.rs:179-201): any nonce,
+ * any AAD, any length, host pointers, blocking.  dec returns RG_OK, or
+ * RG_PKT_DECRYPT_ERR (positive 1) on a tag mismatch with payload untouched. */
+int rg_chacha20poly1305_enc(rg_ctx *ctx, const uint8_t key[32], const uint8_t nonce[12], const uint8_t *aad,
+                            size_t aad_len, uint8_t *payload, size_t len, uint8_t tag[16]);
+int rg_chacha20poly1305_dec(rg_ctx *ctx, const uint8_t key[32], const uint8_t nonce[12], const uint8_t *aad,
+                            size_t aad_len, uint8_t *payload, size_t len, const uint8_t tag[16]);
+
+/* ---------------------------------------------- host-side session layer */
+/* AntiReplay: RFC 6479 window, 2048-bit bitmap, WINDOW_SIZE = 1984
+ * (rustyguard-utils/src/anti_replay.rs:1-64), identical semantics. */
+typedef struct rg_antireplay {
+    uint64_t bitmap[32];
+    uint64_t last;
+} rg_antireplay;
+#define RG_REPLAY_WINDOW 1984u
+
+void rg_antireplay_init(rg_antireplay *r);
+int rg_antireplay_would_accept(const rg_antireplay *r, uint64_t n);
+void rg_antireplay_mark_seen(rg_antireplay *r, uint64_t n);
+
+/* Session table: the transport half of rustyguard_core::Sessions.  Each
+ * session owns an EncryptionKey {key, counter} and a DecryptionKey {key,
+ * AntiReplay} (prim.rs:376-437), the peer's receiver id for outgoing
+ * headers, and our local id that incoming headers name
+ * (rustyguard-core/src/lib.rs:230-235, :646-650). */
+typedef struct rg_sessions rg_sessions;
+
+/* REKEY_AFTER_MESSAGES / REJECT_AFTER_MESSAGES, rustyguard-core/src/lib.rs:63-65 */
+#define RG_REKEY_AFTER_MESSAGES (1ull << 60)
+#define RG_REJECT_AFTER_MESSAGES (0xFFFFFFFFFFFFFFFFull - (1ull << 13))
+
+int rg_sessions_create(rg_ctx *ctx, uint32_t capacity, rg_sessions **out);
+void rg_sessions_destroy(rg_sessions *s);
+/* Install a transport session (HandshakeState::split output, prim.rs:299-313);
+ * returns the slot index (>= 0) or a negative rg_status. */
+int rg_sessions_insert(rg_sessions *s, uint32_t local_id, uint32_t remote_id, const uint8_t send_key[32],
+                       const uint8_t recv_key[32]);
+int rg_sessions_remove(rg_sessions *s, uint32_t slot);
+int rg_sessions_lookup(const rg_sessions *s, uint32_t local_id); /* slot or RG_ENOTFOUND */
+/* EncryptionKey::counter() (prim.rs:396-398) / overwrite, e.g. for REKEY tests */
+uint64_t rg_sessions_send_counter(const rg_sessions *s, uint32_t slot);
+int rg_sessions_set_send_counter(rg_sessions *s, uint32_t slot, uint64_t counter);
+rg_antireplay *rg_sessions_replay(rg_sessions *s, uint32_t slot);
+
+/* Batched PeerState::encrypt_message + frame_in_place over host frames.
+ * Packets are processed in array order: each takes the next counter of its
+ * session (EncryptionKey::encrypt, prim.rs:386-394).  status[i]: OK, INVALID
+ * (P % 16 != 0 / bad desc), REJECTED (counter >= REJECT_AFTER_MESSAGES,
+ * lib.rs:204-206, 260-262).  rekey_out[i] (nullable) = 1 when the session
+ * counter reached REKEY_AFTER_MESSAGES (lib.rs:564-570). */
+int rg_send_batch(rg_sessions *s, const uint32_t *slots, const rg_pkt_desc *desc, size_t n, uint8_t *buf,
+                  size_t buf_len, uint8_t *status, uint8_t *rekey_out);
+/* Batched Sessions::recv_message for data frames: alignment/type/length
+ * checks, receiver-id -> session, replay pre-filter, GPU open, then the
+ * in-order anti-replay post-pass (A6 in SURVEY.md §8): packet j is accepted
+ * iff its tag verifies and would_accept(n_j) holds after packets 0..j-1.
+ * slots_out[i] = session slot (or 0xFFFFFFFF). */
+int rg_recv_batch(rg_sessions *s, const rg_pkt_desc *desc, size_t n, uint8_t *buf, size_t buf_len,
+                  uint8_t *status, uint32_t *slots_out);
+
+/* ------------------------------------------------ synthetic workloads */
+/* Device fill of payload bytes: inner bytes [0, inner_len[i]) of packet i
+ * are le64(mix64(seed + (i << 16) + word)), bytes [inner_len, P) are zero.
+ * desc/inner_len/buf are device pointers; desc[i].len = P. */
+int rg_synth_fill_dev(rg_ctx *ctx, const rg_pkt_desc *desc, const uint32_t *inner_len, size_t n, uint8_t *buf,
+                      size_t buf_len, uint64_t seed, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RG_AEAD_H */

@@ -1,0 +1,130 @@
+"""ctypes front-end of the CPU oracle (oracle/rg_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+``cpu_baseline`` leg of bench.py, always as the checker / the timed CPU
+baseline, never by the product package ``rustyguard_amd``.
+
+The C code restates RFC 8439 (the algorithm of graviola 0.2.0, which the
+reference calls at rustyguard-crypto/src/prim.rs:179-201) plus the WireGuard
+nonce/framing glue; see the header of rg_oracle.c for the file:line map.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "librg_oracle.so")
+_lib = None
+
+DESC_DTYPE = np.dtype([("offset", "<u8"), ("len", "<u4"), ("key_idx", "<u4")])
+
+OK, DECRYPT_ERR, INVALID, REJECTED, UNALIGNED, NOT_DATA = range(6)
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        u8p = ctypes.c_void_p
+        L.rg_oracle_chacha20_block.argtypes = [u8p, ctypes.c_uint32, u8p, u8p]
+        L.rg_oracle_poly1305.argtypes = [u8p, u8p, ctypes.c_size_t, u8p]
+        L.rg_oracle_aead_seal.argtypes = [u8p, u8p, u8p, ctypes.c_size_t, u8p, ctypes.c_size_t, u8p]
+        L.rg_oracle_aead_open.argtypes = [u8p, u8p, u8p, ctypes.c_size_t, u8p, ctypes.c_size_t, u8p]
+        L.rg_oracle_aead_open.restype = ctypes.c_int
+        L.rg_oracle_seal_batch.argtypes = [u8p, u8p, u8p, u8p, ctypes.c_size_t, u8p, u8p, ctypes.c_int]
+        L.rg_oracle_open_batch.argtypes = [u8p, u8p, ctypes.c_size_t, u8p, u8p, u8p, ctypes.c_int]
+        L.rg_oracle_mix64.argtypes = [ctypes.c_uint64]
+        L.rg_oracle_mix64.restype = ctypes.c_uint64
+        L.rg_oracle_synth_fill.argtypes = [u8p, u8p, u8p, ctypes.c_size_t, ctypes.c_uint64]
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    if a is None:
+        return None
+    if isinstance(a, (bytes, bytearray)):
+        a = np.frombuffer(bytes(a), dtype=np.uint8)
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _u8(b) -> np.ndarray:
+    return np.frombuffer(bytes(b), dtype=np.uint8).copy()
+
+
+def wg_nonce(counter: int) -> bytes:
+    """rustyguard-crypto/src/prim.rs:32-36."""
+    return b"\0" * 4 + int(counter).to_bytes(8, "little")
+
+
+def chacha20_block(key: bytes, counter: int, nonce: bytes) -> bytes:
+    out = np.zeros(64, np.uint8)
+    lib().rg_oracle_chacha20_block(_ptr(_u8(key)), counter, _ptr(_u8(nonce)), _ptr(out))
+    return out.tobytes()
+
+
+def poly1305(key: bytes, msg: bytes) -> bytes:
+    out = np.zeros(16, np.uint8)
+    m = _u8(msg) if msg else np.zeros(1, np.uint8)
+    lib().rg_oracle_poly1305(_ptr(_u8(key)), _ptr(m), len(msg), _ptr(out))
+    return out.tobytes()
+
+
+def aead_seal(key: bytes, nonce: bytes, aad: bytes, pt: bytes) -> tuple[bytes, bytes]:
+    """Core::chacha20poly1305_enc (prim.rs:179-188): returns (ciphertext, tag)."""
+    buf = _u8(pt) if pt else np.zeros(1, np.uint8)
+    a = _u8(aad) if aad else np.zeros(1, np.uint8)
+    tag = np.zeros(16, np.uint8)
+    lib().rg_oracle_aead_seal(_ptr(_u8(key)), _ptr(_u8(nonce)), _ptr(a), len(aad), _ptr(buf), len(pt), _ptr(tag))
+    return buf.tobytes()[: len(pt)], tag.tobytes()
+
+
+def aead_open(key: bytes, nonce: bytes, aad: bytes, ct: bytes, tag: bytes):
+    """Core::chacha20poly1305_dec (prim.rs:190-201): plaintext or None on DecryptionError."""
+    buf = _u8(ct) if ct else np.zeros(1, np.uint8)
+    a = _u8(aad) if aad else np.zeros(1, np.uint8)
+    rc = lib().rg_oracle_aead_open(_ptr(_u8(key)), _ptr(_u8(nonce)), _ptr(a), len(aad), _ptr(buf), len(ct),
+                                   _ptr(_u8(tag)))
+    return None if rc != 0 else buf.tobytes()[: len(ct)]
+
+
+def seal_batch(keys: np.ndarray, receivers, desc: np.ndarray, counters: np.ndarray, buf: np.ndarray,
+               nthreads: int = 1, status: np.ndarray | None = None) -> None:
+    """In-place batched seal over the include/rg_aead.h buffer contract."""
+    assert desc.dtype == DESC_DTYPE and buf.dtype == np.uint8
+    keys = np.ascontiguousarray(keys, dtype=np.uint8)
+    counters = np.ascontiguousarray(counters, dtype=np.uint64)
+    rec = None if receivers is None else np.ascontiguousarray(receivers, dtype=np.uint32)
+    lib().rg_oracle_seal_batch(_ptr(keys), _ptr(rec), _ptr(desc), _ptr(counters), len(desc), _ptr(buf),
+                               _ptr(status), nthreads)
+
+
+def open_batch(keys: np.ndarray, desc: np.ndarray, buf: np.ndarray, nthreads: int = 1):
+    """In-place batched open; returns (status u8[n], counters u64[n])."""
+    assert desc.dtype == DESC_DTYPE and buf.dtype == np.uint8
+    keys = np.ascontiguousarray(keys, dtype=np.uint8)
+    n = len(desc)
+    status = np.zeros(max(n, 1), np.uint8)
+    ctr = np.zeros(max(n, 1), np.uint64)
+    lib().rg_oracle_open_batch(_ptr(keys), _ptr(desc), n, _ptr(buf), _ptr(status), _ptr(ctr), nthreads)
+    return status[:n], ctr[:n]
+
+
+def mix64(x: int) -> int:
+    return int(lib().rg_oracle_mix64(x))
+
+
+def synth_fill(buf: np.ndarray, desc: np.ndarray, inner_len: np.ndarray, seed: int) -> None:
+    inner = np.ascontiguousarray(inner_len, dtype=np.uint32)
+    lib().rg_oracle_synth_fill(_ptr(buf), _ptr(desc), _ptr(inner), len(desc), seed)

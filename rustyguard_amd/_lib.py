@@ -1,0 +1,86 @@
+"""ctypes binding of librg_aead.so (include/rg_aead.h).
+
+There is deliberately no CPU fallback: if the HIP library is missing or fails
+to load, every entry point raises.  (The CPU oracle under oracle/ is test
+infrastructure and is never imported from this package.)
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+from . import build as _build
+
+_lib = None
+
+c_u8p = ctypes.c_void_p
+c_vp = ctypes.c_void_p
+c_size = ctypes.c_size_t
+c_u32 = ctypes.c_uint32
+c_u64 = ctypes.c_uint64
+c_int = ctypes.c_int
+
+# name -> (restype, argtypes); mirrors include/rg_aead.h one to one
+SIGNATURES = {
+    "rg_abi_version": (c_int, []),
+    "rg_last_error": (ctypes.c_char_p, []),
+    "rg_create": (c_int, [c_int, ctypes.POINTER(c_vp)]),
+    "rg_destroy": (None, [c_vp]),
+    "rg_seal_batch_dev": (c_int, [c_vp, c_u8p, c_vp, c_u32, c_vp, c_vp, c_size, c_u8p, c_size, c_u8p, c_vp]),
+    "rg_open_batch_dev": (c_int, [c_vp, c_u8p, c_u32, c_vp, c_size, c_u8p, c_size, c_u8p, c_vp, c_vp]),
+    "rg_set_lanes_per_packet": (c_int, [c_vp, c_int]),
+    "rg_get_lanes_per_packet": (c_int, [c_vp, c_size]),
+    "rg_seal_batch_host": (c_int, [c_vp, c_u8p, c_vp, c_u32, c_vp, c_vp, c_size, c_u8p, c_size, c_u8p]),
+    "rg_open_batch_host": (c_int, [c_vp, c_u8p, c_u32, c_vp, c_size, c_u8p, c_size, c_u8p, c_vp]),
+    "rg_host_alloc": (c_vp, [c_size]),
+    "rg_host_free": (None, [c_vp]),
+    "rg_chacha20poly1305_enc": (c_int, [c_vp, c_u8p, c_u8p, c_u8p, c_size, c_u8p, c_size, c_u8p]),
+    "rg_chacha20poly1305_dec": (c_int, [c_vp, c_u8p, c_u8p, c_u8p, c_size, c_u8p, c_size, c_u8p]),
+    "rg_antireplay_init": (None, [c_vp]),
+    "rg_antireplay_would_accept": (c_int, [c_vp, c_u64]),
+    "rg_antireplay_mark_seen": (None, [c_vp, c_u64]),
+    "rg_sessions_create": (c_int, [c_vp, c_u32, ctypes.POINTER(c_vp)]),
+    "rg_sessions_destroy": (None, [c_vp]),
+    "rg_sessions_insert": (c_int, [c_vp, c_u32, c_u32, c_u8p, c_u8p]),
+    "rg_sessions_remove": (c_int, [c_vp, c_u32]),
+    "rg_sessions_lookup": (c_int, [c_vp, c_u32]),
+    "rg_sessions_send_counter": (c_u64, [c_vp, c_u32]),
+    "rg_sessions_set_send_counter": (c_int, [c_vp, c_u32, c_u64]),
+    "rg_sessions_replay": (c_vp, [c_vp, c_u32]),
+    "rg_send_batch": (c_int, [c_vp, c_vp, c_vp, c_size, c_u8p, c_size, c_u8p, c_u8p]),
+    "rg_recv_batch": (c_int, [c_vp, c_vp, c_size, c_u8p, c_size, c_u8p, c_vp]),
+    "rg_synth_fill_dev": (c_int, [c_vp, c_vp, c_vp, c_size, c_u8p, c_size, c_u64, c_vp]),
+}
+
+
+class RgError(RuntimeError):
+    pass
+
+
+def lib_path() -> str:
+    return _build.LIB
+
+
+def lib(build_if_missing: bool = True):
+    """Load librg_aead.so; raise loudly if it cannot be loaded."""
+    global _lib
+    if _lib is None:
+        path = _build.LIB
+        if not os.path.exists(path):
+            if not build_if_missing:
+                raise RgError(f"librg_aead.so missing at {path}; run python -m rustyguard_amd.build")
+            _build.build()
+        L = ctypes.CDLL(path)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str) -> int:
+    if rc < 0:
+        err = lib().rg_last_error()
+        raise RgError(f"{what} failed ({rc}): {err.decode() if err else ''}")
+    return rc

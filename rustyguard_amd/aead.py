@@ -1,0 +1,302 @@
+"""Host-side mirror of the reference's transport AEAD interface over librg_aead.
+
+Reference interface -> this module
+  CryptoPrimatives::chacha20poly1305_enc/_dec (prim.rs:82-95, 179-201)
+                                         -> Engine.chacha20poly1305_enc/_dec
+  EncryptionKey {new, encrypt, counter}   (prim.rs:376-399) -> EncryptionKey
+  DecryptionKey {new, decrypt}            (prim.rs:401-437) -> DecryptionKey
+  AntiReplay {would_accept, mark_seen}    (anti_replay.rs:25-64) -> AntiReplay
+  CryptoError::{DecryptionError, Rejected} (rustyguard-crypto/src/lib.rs:43-48)
+                                         -> DecryptionError / Rejected exceptions
+  batched hot path                        -> Engine.seal_dev/open_dev (device
+                                             tensors), seal_host/open_host (numpy)
+  Sessions send/recv of data frames       -> Sessions.send_batch / recv_batch
+
+Every call goes through the HIP library; there is no CPU path here.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, lib
+from .workloads import DESC_DTYPE
+
+PKT_OK, PKT_DECRYPT_ERR, PKT_INVALID, PKT_REJECTED, PKT_UNALIGNED, PKT_NOT_DATA = range(6)
+KEY_SKIP = 0xFFFFFFFF
+REKEY_AFTER_MESSAGES = 1 << 60
+REJECT_AFTER_MESSAGES = (1 << 64) - 1 - (1 << 13)
+WINDOW_SIZE = 1984
+
+
+class CryptoError(Exception):
+    pass
+
+
+class DecryptionError(CryptoError):
+    """CryptoError::DecryptionError"""
+
+
+class Rejected(CryptoError):
+    """CryptoError::Rejected"""
+
+
+def _vp(x):
+    """Pointer of a numpy array / torch tensor / bytes-like (None passes through)."""
+    if x is None:
+        return None
+    if hasattr(x, "data_ptr"):
+        return ctypes.c_void_p(x.data_ptr())
+    if isinstance(x, np.ndarray):
+        return x.ctypes.data_as(ctypes.c_void_p)
+    if isinstance(x, bytearray):
+        return ctypes.cast((ctypes.c_char * len(x)).from_buffer(x), ctypes.c_void_p)
+    raise TypeError(type(x))
+
+
+def _stream_handle(stream):
+    if stream is None:
+        import torch
+
+        return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    if isinstance(stream, int):
+        return ctypes.c_void_p(stream)
+    return ctypes.c_void_p(stream.cuda_stream)
+
+
+def _ndesc(desc) -> int:
+    """Descriptor count of a device tensor holding rg_pkt_desc rows (16 bytes each)."""
+    nb = _nbytes(desc)
+    assert nb % 16 == 0, "descriptor tensor must hold whole 16-byte rg_pkt_desc rows"
+    return nb // 16
+
+
+def _nbytes(t) -> int:
+    if hasattr(t, "numel"):
+        return t.numel() * t.element_size()
+    return t.nbytes
+
+
+class Engine:
+    """One rg_ctx: a HIP device plus its staging buffers (one per process/GPU)."""
+
+    def __init__(self, device: int = 0):
+        self._L = lib()
+        h = ctypes.c_void_p()
+        check(self._L.rg_create(device, ctypes.byref(h)), "rg_create")
+        self._h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.rg_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    def set_lanes_per_packet(self, lanes: int):
+        check(self._L.rg_set_lanes_per_packet(self._h, lanes), "rg_set_lanes_per_packet")
+
+    def lanes_per_packet(self, n: int) -> int:
+        return check(self._L.rg_get_lanes_per_packet(self._h, n), "rg_get_lanes_per_packet")
+
+    # ---------------------------------------------------- device-resident
+    def seal_dev(self, keys, receivers, desc, counters, buf, status=None, stream=None):
+        """Enqueue a batched seal on `stream`; all tensors on this device."""
+        n = _ndesc(desc)
+        nkeys = _nbytes(keys) // 32
+        check(self._L.rg_seal_batch_dev(self._h, _vp(keys), _vp(receivers), nkeys, _vp(desc), _vp(counters), n,
+                                        _vp(buf), _nbytes(buf), _vp(status), _stream_handle(stream)),
+              "rg_seal_batch_dev")
+
+    def open_dev(self, keys, desc, buf, status, counters_out=None, stream=None):
+        n = _ndesc(desc)
+        nkeys = _nbytes(keys) // 32
+        check(self._L.rg_open_batch_dev(self._h, _vp(keys), nkeys, _vp(desc), n, _vp(buf), _nbytes(buf),
+                                        _vp(status), _vp(counters_out), _stream_handle(stream)),
+              "rg_open_batch_dev")
+
+    def synth_fill_dev(self, desc, inner_len, buf, seed: int, stream=None):
+        n = _ndesc(desc)
+        check(self._L.rg_synth_fill_dev(self._h, _vp(desc), _vp(inner_len), n, _vp(buf), _nbytes(buf), seed,
+                                        _stream_handle(stream)), "rg_synth_fill_dev")
+
+    # -------------------------------------------------------- host memory
+    def seal_host(self, keys: np.ndarray, receivers, desc: np.ndarray, counters: np.ndarray, buf: np.ndarray):
+        assert desc.dtype == DESC_DTYPE and buf.dtype == np.uint8 and buf.flags.c_contiguous
+        keys = np.ascontiguousarray(keys, np.uint8)
+        counters = np.ascontiguousarray(counters, np.uint64)
+        rec = None if receivers is None else np.ascontiguousarray(receivers, np.uint32)
+        status = np.zeros(max(len(desc), 1), np.uint8)
+        check(self._L.rg_seal_batch_host(self._h, _vp(keys), _vp(rec), keys.size // 32, _vp(desc), _vp(counters),
+                                         len(desc), _vp(buf), buf.nbytes, _vp(status)), "rg_seal_batch_host")
+        return status[: len(desc)]
+
+    def open_host(self, keys: np.ndarray, desc: np.ndarray, buf: np.ndarray):
+        assert desc.dtype == DESC_DTYPE and buf.dtype == np.uint8 and buf.flags.c_contiguous
+        keys = np.ascontiguousarray(keys, np.uint8)
+        n = len(desc)
+        status = np.zeros(max(n, 1), np.uint8)
+        ctr = np.zeros(max(n, 1), np.uint64)
+        check(self._L.rg_open_batch_host(self._h, _vp(keys), keys.size // 32, _vp(desc), n, _vp(buf), buf.nbytes,
+                                         _vp(status), _vp(ctr)), "rg_open_batch_host")
+        return status[:n], ctr[:n]
+
+    # --------------------------------------------- per-message drop-in
+    def chacha20poly1305_enc(self, key: bytes, nonce: bytes, aad: bytes, payload: bytearray) -> bytes:
+        """Core::chacha20poly1305_enc: encrypts `payload` in place, returns the tag."""
+        assert len(key) == 32 and len(nonce) == 12
+        tag = bytearray(16)
+        k, nz, a = bytearray(key), bytearray(nonce), bytearray(aad or b"\0")
+        check(self._L.rg_chacha20poly1305_enc(self._h, _vp(k), _vp(nz), _vp(a), len(aad), _vp(payload) if payload
+                                              else None, len(payload), _vp(tag)), "rg_chacha20poly1305_enc")
+        return bytes(tag)
+
+    def chacha20poly1305_dec(self, key: bytes, nonce: bytes, aad: bytes, payload: bytearray, tag: bytes) -> None:
+        """Core::chacha20poly1305_dec: decrypts in place or raises DecryptionError."""
+        assert len(key) == 32 and len(nonce) == 12 and len(tag) == 16
+        k, nz, a, t = bytearray(key), bytearray(nonce), bytearray(aad or b"\0"), bytearray(tag)
+        rc = check(self._L.rg_chacha20poly1305_dec(self._h, _vp(k), _vp(nz), _vp(a), len(aad), _vp(payload) if payload
+                                                   else None, len(payload), _vp(t)), "rg_chacha20poly1305_dec")
+        if rc == PKT_DECRYPT_ERR:
+            raise DecryptionError()
+
+
+def nonce(counter: int) -> bytes:
+    """prim.rs:32-36: 00000000 || le64(counter)."""
+    return b"\0" * 4 + int(counter).to_bytes(8, "little")
+
+
+# ---------------------------------------------------------------- AntiReplay
+class _ReplayStruct(ctypes.Structure):
+    _fields_ = [("bitmap", ctypes.c_uint64 * 32), ("last", ctypes.c_uint64)]
+
+
+class AntiReplay:
+    """rustyguard_utils::anti_replay::AntiReplay, backed by the C implementation."""
+
+    def __init__(self, _ptr=None):
+        if _ptr is None:
+            self._s = _ReplayStruct()
+            self._p = ctypes.cast(ctypes.byref(self._s), ctypes.c_void_p)
+            lib().rg_antireplay_init(self._p)
+        else:
+            self._p = ctypes.c_void_p(_ptr)
+
+    def would_accept(self, n: int) -> bool:
+        return bool(lib().rg_antireplay_would_accept(self._p, n))
+
+    def mark_seen(self, n: int) -> None:
+        lib().rg_antireplay_mark_seen(self._p, n)
+
+
+class EncryptionKey:
+    """prim.rs:376-399: seal with nonce(counter), counter += 1."""
+
+    def __init__(self, engine: Engine, key: bytes):
+        self.engine, self.key, self._counter = engine, bytes(key), 0
+
+    def encrypt(self, payload: bytearray) -> bytes:
+        n = self._counter
+        self._counter += 1
+        return self.engine.chacha20poly1305_enc(self.key, nonce(n), b"", payload)
+
+    def counter(self) -> int:
+        return self._counter
+
+
+class DecryptionKey:
+    """prim.rs:401-437: replay gate -> open -> mark_seen only on success."""
+
+    def __init__(self, engine: Engine, key: bytes):
+        self.engine, self.key, self.replay = engine, bytes(key), AntiReplay()
+
+    def decrypt(self, counter: int, payload_and_tag: bytearray) -> bytearray:
+        if not self.replay.would_accept(counter):
+            raise Rejected()
+        if len(payload_and_tag) < 16:
+            raise DecryptionError()
+        body = bytearray(payload_and_tag[:-16])
+        self.engine.chacha20poly1305_dec(self.key, nonce(counter), b"", body, bytes(payload_and_tag[-16:]))
+        payload_and_tag[:-16] = body
+        self.replay.mark_seen(counter)
+        return body
+
+
+# ------------------------------------------------------------------ Sessions
+class Sessions:
+    """Transport half of rustyguard_core::Sessions (batched, host frames)."""
+
+    def __init__(self, engine: Engine, capacity: int = 64):
+        self.engine = engine
+        h = ctypes.c_void_p()
+        check(lib().rg_sessions_create(engine.handle, capacity, ctypes.byref(h)), "rg_sessions_create")
+        self._h = h
+
+    def __del__(self):
+        try:
+            if self._h:
+                lib().rg_sessions_destroy(self._h)
+                self._h = None
+        except Exception:
+            pass
+
+    def insert(self, local_id: int, remote_id: int, send_key: bytes, recv_key: bytes) -> int:
+        sk, rk = bytearray(send_key), bytearray(recv_key)
+        return check(lib().rg_sessions_insert(self._h, local_id, remote_id, _vp(sk), _vp(rk)), "rg_sessions_insert")
+
+    def remove(self, slot: int):
+        check(lib().rg_sessions_remove(self._h, slot), "rg_sessions_remove")
+
+    def lookup(self, local_id: int) -> int | None:
+        rc = lib().rg_sessions_lookup(self._h, local_id)
+        return None if rc < 0 else rc
+
+    def send_counter(self, slot: int) -> int:
+        return int(lib().rg_sessions_send_counter(self._h, slot))
+
+    def set_send_counter(self, slot: int, counter: int):
+        check(lib().rg_sessions_set_send_counter(self._h, slot, counter), "rg_sessions_set_send_counter")
+
+    def replay(self, slot: int) -> AntiReplay:
+        return AntiReplay(_ptr=lib().rg_sessions_replay(self._h, slot))
+
+    def send_batch(self, slots, desc: np.ndarray, buf: np.ndarray):
+        slots = np.ascontiguousarray(slots, np.uint32)
+        n = len(desc)
+        status = np.zeros(max(n, 1), np.uint8)
+        rekey = np.zeros(max(n, 1), np.uint8)
+        check(lib().rg_send_batch(self._h, _vp(slots), _vp(desc), n, _vp(buf), buf.nbytes, _vp(status), _vp(rekey)),
+              "rg_send_batch")
+        return status[:n], rekey[:n]
+
+    def recv_batch(self, desc: np.ndarray, buf: np.ndarray):
+        n = len(desc)
+        status = np.zeros(max(n, 1), np.uint8)
+        slots = np.zeros(max(n, 1), np.uint32)
+        check(lib().rg_recv_batch(self._h, _vp(desc), n, _vp(buf), buf.nbytes, _vp(status), _vp(slots)),
+              "rg_recv_batch")
+        return status[:n], slots[:n]
+
+
+def host_alloc(nbytes: int) -> np.ndarray:
+    """Pinned host buffer (hipHostMalloc) viewed as uint8; freed with the array's owner."""
+    p = lib().rg_host_alloc(nbytes)
+    if not p:
+        raise _lib.RgError("rg_host_alloc failed")
+    buf = (ctypes.c_uint8 * nbytes).from_address(p)
+    arr = np.frombuffer(buf, dtype=np.uint8)
+    import weakref
+
+    weakref.finalize(buf, lib().rg_host_free, ctypes.c_void_p(p))
+    return arr

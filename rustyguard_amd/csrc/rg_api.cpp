@@ -1,0 +1,651 @@
+// rg_api.cpp -- the C ABI of include/rg_aead.h: device context, batched
+// device/host entry points, the per-message CryptoPrimatives drop-in, and the
+// host-side transport session layer (EncryptionKey / DecryptionKey /
+// AntiReplay, rustyguard-crypto/src/prim.rs:376-437,
+// rustyguard-utils/src/anti_replay.rs:1-64, rustyguard-core/src/lib.rs:249-681).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "rg_internal.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int set_err(int code, const char *what, hipError_t e = hipSuccess) {
+    char buf[256];
+    if (e != hipSuccess)
+        snprintf(buf, sizeof buf, "%s: %s", what, hipGetErrorString(e));
+    else
+        snprintf(buf, sizeof buf, "%s", what);
+    g_err = buf;
+    return code;
+}
+
+#define RG_HIP(call, what)                                                   \
+    do {                                                                     \
+        hipError_t e_ = (call);                                              \
+        if (e_ != hipSuccess) return set_err(RG_EDEVICE, what, e_);          \
+    } while (0)
+
+// grow-only device allocation
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    hipError_t reserve(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = std::max<size_t>(bytes, 4096);
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+struct HostBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    hipError_t reserve(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = std::max<size_t>(bytes, 4096);
+        hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+// one pipeline lane of the host path
+struct Slot {
+    hipStream_t stream = nullptr;
+    DevBuf d_buf, d_desc, d_ctr, d_status, d_ctr_out;
+    HostBuf h_desc, h_ctr, h_status, h_ctr_out;
+    // bookkeeping of the slice in flight
+    size_t i0 = 0, i1 = 0;
+    bool busy = false;
+};
+
+} // namespace
+
+struct rg_ctx {
+    int device = 0;
+    int lanes = 0;
+    std::mutex mu;
+    Slot slots[2];
+    DevBuf d_keys, d_recv;
+    DevBuf d_general;  // per-message drop-in arena
+    DevBuf d_jobs;
+};
+
+namespace {
+
+int check_ctx(rg_ctx *ctx) {
+    if (!ctx) return set_err(RG_EINVAL, "null context");
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return set_err(RG_EDEVICE, "hipSetDevice", e);
+    return RG_OK;
+}
+
+} // namespace
+
+extern "C" {
+
+int rg_abi_version(void) { return RG_ABI_VERSION; }
+
+const char *rg_last_error(void) { return g_err.c_str(); }
+
+int rg_create(int device, rg_ctx **out) {
+    if (!out) return set_err(RG_EINVAL, "null out");
+    *out = nullptr;
+    int ndev = 0;
+    RG_HIP(hipGetDeviceCount(&ndev), "hipGetDeviceCount");
+    if (device < 0 || device >= ndev) return set_err(RG_EINVAL, "no such HIP device");
+    RG_HIP(hipSetDevice(device), "hipSetDevice");
+    rg_ctx *c = new (std::nothrow) rg_ctx();
+    if (!c) return set_err(RG_ENOMEM, "alloc ctx");
+    c->device = device;
+    for (auto &s : c->slots) {
+        hipError_t e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
+        if (e != hipSuccess) {
+            rg_destroy(c);
+            return set_err(RG_EDEVICE, "hipStreamCreate", e);
+        }
+    }
+    *out = c;
+    return RG_OK;
+}
+
+void rg_destroy(rg_ctx *ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    for (auto &s : ctx->slots) {
+        if (s.stream) {
+            (void)hipStreamSynchronize(s.stream);
+            (void)hipStreamDestroy(s.stream);
+        }
+        s.d_buf.release(); s.d_desc.release(); s.d_ctr.release(); s.d_status.release(); s.d_ctr_out.release();
+        s.h_desc.release(); s.h_ctr.release(); s.h_status.release(); s.h_ctr_out.release();
+    }
+    ctx->d_keys.release();
+    ctx->d_recv.release();
+    ctx->d_general.release();
+    ctx->d_jobs.release();
+    delete ctx;
+}
+
+int rg_set_lanes_per_packet(rg_ctx *ctx, int lanes) {
+    if (!ctx) return set_err(RG_EINVAL, "null context");
+    if (lanes != 0 && lanes != 1 && lanes != 2 && lanes != 4) return set_err(RG_EINVAL, "lanes must be 0,1,2,4");
+    ctx->lanes = lanes;
+    return RG_OK;
+}
+
+int rg_get_lanes_per_packet(rg_ctx *ctx, size_t n) {
+    (void)n;
+    if (!ctx) return set_err(RG_EINVAL, "null context");
+    return 1;
+}
+
+// --------------------------------------------------------------- device API
+int rg_seal_batch_dev(rg_ctx *ctx, const uint8_t *keys, const uint32_t *receivers, uint32_t nkeys,
+                      const rg_pkt_desc *desc, const uint64_t *counters, size_t n, uint8_t *buf, size_t buf_len,
+                      uint8_t *status, void *stream) {
+    int rc = check_ctx(ctx);
+    if (rc) return rc;
+    if (n == 0) return RG_OK;
+    if (!keys || !desc || !counters || !buf || n > 0xFFFFFFFFull) return set_err(RG_EINVAL, "seal: bad args");
+    rg::SealArgs a;
+    a.keys = reinterpret_cast<const uint32_t *>(keys);
+    a.receivers = receivers;
+    a.desc = desc;
+    a.counters = counters;
+    a.buf = buf;
+    a.buf_len = buf_len;
+    a.status = status;
+    a.nkeys = nkeys;
+    a.n = (uint32_t)n;
+    RG_HIP(rg::launch_seal(a, rg_get_lanes_per_packet(ctx, n), (hipStream_t)stream), "seal launch");
+    return RG_OK;
+}
+
+int rg_open_batch_dev(rg_ctx *ctx, const uint8_t *keys, uint32_t nkeys, const rg_pkt_desc *desc, size_t n,
+                      uint8_t *buf, size_t buf_len, uint8_t *status, uint64_t *counters_out, void *stream) {
+    int rc = check_ctx(ctx);
+    if (rc) return rc;
+    if (n == 0) return RG_OK;
+    if (!keys || !desc || !buf || !status || n > 0xFFFFFFFFull) return set_err(RG_EINVAL, "open: bad args");
+    rg::OpenArgs a;
+    a.keys = reinterpret_cast<const uint32_t *>(keys);
+    a.desc = desc;
+    a.buf = buf;
+    a.buf_len = buf_len;
+    a.status = status;
+    a.counters_out = counters_out;
+    a.nkeys = nkeys;
+    a.n = (uint32_t)n;
+    RG_HIP(rg::launch_open(a, rg_get_lanes_per_packet(ctx, n), (hipStream_t)stream), "open launch");
+    return RG_OK;
+}
+
+int rg_synth_fill_dev(rg_ctx *ctx, const rg_pkt_desc *desc, const uint32_t *inner_len, size_t n, uint8_t *buf,
+                      size_t buf_len, uint64_t seed, void *stream) {
+    int rc = check_ctx(ctx);
+    if (rc) return rc;
+    if (n == 0) return RG_OK;
+    if (!desc || !inner_len || !buf || n > 0x7FFFFFFFull) return set_err(RG_EINVAL, "synth: bad args");
+    RG_HIP(rg::launch_synth_fill(desc, inner_len, (uint32_t)n, buf, buf_len, seed, (hipStream_t)stream),
+           "synth launch");
+    return RG_OK;
+}
+
+void *rg_host_alloc(size_t bytes) {
+    void *p = nullptr;
+    if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) return nullptr;
+    return p;
+}
+
+void rg_host_free(void *p) {
+    if (p) (void)hipHostFree(p);
+}
+
+} // extern "C"
+
+// ------------------------------------------------------------ host pipeline
+namespace {
+
+constexpr size_t kSliceBytes = 32ull << 20; // frames per pipeline slice
+constexpr size_t kSlicePkts = 1u << 16;
+constexpr uint64_t kOutOfRange = (UINT64_MAX / 2) & ~15ull;
+
+bool in_arena(const rg_pkt_desc &d, bool open, size_t buf_len) {
+    const uint64_t need = (uint64_t)d.len + (open ? 0 : 32);
+    return d.offset <= buf_len && need <= buf_len - d.offset && d.len <= rg::kMaxPayload + 32;
+}
+
+int upload_keys(rg_ctx *ctx, const uint8_t *keys, const uint32_t *receivers, uint32_t nkeys) {
+    RG_HIP(ctx->d_keys.reserve((size_t)nkeys * 32), "alloc keys");
+    RG_HIP(hipMemcpy(ctx->d_keys.p, keys, (size_t)nkeys * 32, hipMemcpyHostToDevice), "H2D keys");
+    if (receivers) {
+        RG_HIP(ctx->d_recv.reserve((size_t)nkeys * 4), "alloc receivers");
+        RG_HIP(hipMemcpy(ctx->d_recv.p, receivers, (size_t)nkeys * 4, hipMemcpyHostToDevice), "H2D receivers");
+    }
+    return RG_OK;
+}
+
+// Drain a finished slice: copy statuses / counters back to the caller.
+int finish_slot(Slot &s, uint8_t *status, uint64_t *counters_out) {
+    if (!s.busy) return RG_OK;
+    RG_HIP(hipStreamSynchronize(s.stream), "slice sync");
+    const size_t m = s.i1 - s.i0;
+    if (status) memcpy(status + s.i0, s.h_status.p, m);
+    if (counters_out) memcpy(counters_out + s.i0, s.h_ctr_out.p, m * 8);
+    s.busy = false;
+    return RG_OK;
+}
+
+// Shared driver of the two host entry points.
+int host_batch(rg_ctx *ctx, bool open, uint32_t nkeys, const rg_pkt_desc *desc, const uint64_t *counters, size_t n,
+               uint8_t *buf, size_t buf_len, uint8_t *status, uint64_t *counters_out, bool with_receivers) {
+    size_t i = 0;
+    int which = 0;
+    while (i < n) {
+        // slice [i, j): bounded by packet count and by the byte span of its frames
+        size_t j = i;
+        uint64_t lo = UINT64_MAX, hi = 0;
+        while (j < n && j - i < kSlicePkts) {
+            const rg_pkt_desc &d = desc[j];
+            if (in_arena(d, open, buf_len)) {
+                const uint64_t end = d.offset + (uint64_t)d.len + (open ? 0 : 32);
+                const uint64_t nlo = std::min<uint64_t>(lo, d.offset & ~15ull), nhi = std::max<uint64_t>(hi, end);
+                if (j > i && nhi - nlo > kSliceBytes) break;
+                lo = nlo;
+                hi = nhi;
+            }
+            ++j;
+        }
+        if (lo == UINT64_MAX) lo = hi = 0; // nothing in range: only statuses come back
+        Slot &s = ctx->slots[which];
+        int rc = finish_slot(s, status, counters_out);
+        if (rc) return rc;
+        const size_t m = j - i;
+        const size_t span = hi - lo;
+        RG_HIP(s.d_buf.reserve(span + 16), "alloc slice");
+        RG_HIP(s.d_desc.reserve(m * sizeof(rg_pkt_desc)), "alloc desc");
+        RG_HIP(s.d_status.reserve(m), "alloc status");
+        RG_HIP(s.h_desc.reserve(m * sizeof(rg_pkt_desc)), "alloc h_desc");
+        RG_HIP(s.h_status.reserve(m), "alloc h_status");
+        rg_pkt_desc *hd = static_cast<rg_pkt_desc *>(s.h_desc.p);
+        for (size_t k = 0; k < m; ++k) {
+            hd[k] = desc[i + k];
+            // frames outside the arena get an aligned out-of-range offset: the kernel flags them INVALID
+            hd[k].offset = in_arena(desc[i + k], open, buf_len) ? desc[i + k].offset - lo : kOutOfRange;
+        }
+        hipStream_t st = s.stream;
+        RG_HIP(hipMemcpyAsync(s.d_desc.p, hd, m * sizeof(rg_pkt_desc), hipMemcpyHostToDevice, st), "H2D desc");
+        if (span) RG_HIP(hipMemcpyAsync(s.d_buf.p, buf + lo, span, hipMemcpyHostToDevice, st), "H2D frames");
+        uint8_t *dbuf = static_cast<uint8_t *>(s.d_buf.p);
+        if (!open) {
+            RG_HIP(s.d_ctr.reserve(m * 8), "alloc ctr");
+            RG_HIP(s.h_ctr.reserve(m * 8), "alloc h_ctr");
+            memcpy(s.h_ctr.p, counters + i, m * 8);
+            RG_HIP(hipMemcpyAsync(s.d_ctr.p, s.h_ctr.p, m * 8, hipMemcpyHostToDevice, st), "H2D ctr");
+            rg::SealArgs a;
+            a.keys = static_cast<const uint32_t *>(ctx->d_keys.p);
+            a.receivers = with_receivers ? static_cast<const uint32_t *>(ctx->d_recv.p) : nullptr;
+            a.desc = static_cast<const rg_pkt_desc *>(s.d_desc.p);
+            a.counters = static_cast<const uint64_t *>(s.d_ctr.p);
+            a.buf = dbuf;
+            a.buf_len = span;
+            a.status = static_cast<uint8_t *>(s.d_status.p);
+            a.nkeys = nkeys;
+            a.n = (uint32_t)m;
+            RG_HIP(rg::launch_seal(a, rg_get_lanes_per_packet(ctx, m), st), "seal launch");
+        } else {
+            RG_HIP(s.d_ctr_out.reserve(m * 8), "alloc ctr_out");
+            RG_HIP(s.h_ctr_out.reserve(m * 8), "alloc h_ctr_out");
+            rg::OpenArgs a;
+            a.keys = static_cast<const uint32_t *>(ctx->d_keys.p);
+            a.desc = static_cast<const rg_pkt_desc *>(s.d_desc.p);
+            a.buf = dbuf;
+            a.buf_len = span;
+            a.status = static_cast<uint8_t *>(s.d_status.p);
+            a.counters_out = static_cast<uint64_t *>(s.d_ctr_out.p);
+            a.nkeys = nkeys;
+            a.n = (uint32_t)m;
+            RG_HIP(rg::launch_open(a, rg_get_lanes_per_packet(ctx, m), st), "open launch");
+            RG_HIP(hipMemcpyAsync(s.h_ctr_out.p, s.d_ctr_out.p, m * 8, hipMemcpyDeviceToHost, st), "D2H ctr");
+        }
+        if (span) RG_HIP(hipMemcpyAsync(buf + lo, s.d_buf.p, span, hipMemcpyDeviceToHost, st), "D2H frames");
+        RG_HIP(hipMemcpyAsync(s.h_status.p, s.d_status.p, m, hipMemcpyDeviceToHost, st), "D2H status");
+        s.i0 = i;
+        s.i1 = j;
+        s.busy = true;
+        i = j;
+        which ^= 1;
+    }
+    for (auto &s : ctx->slots) {
+        int rc = finish_slot(s, status, open ? counters_out : nullptr);
+        if (rc) return rc;
+    }
+    return RG_OK;
+}
+
+} // namespace
+
+extern "C" {
+
+int rg_seal_batch_host(rg_ctx *ctx, const uint8_t *keys, const uint32_t *receivers, uint32_t nkeys,
+                       const rg_pkt_desc *desc, const uint64_t *counters, size_t n, uint8_t *buf, size_t buf_len,
+                       uint8_t *status) {
+    int rc = check_ctx(ctx);
+    if (rc) return rc;
+    if (n == 0) return RG_OK;
+    if (!keys || !desc || !counters || !buf || nkeys == 0) return set_err(RG_EINVAL, "seal_host: bad args");
+    std::lock_guard<std::mutex> g(ctx->mu);
+    rc = upload_keys(ctx, keys, receivers, nkeys);
+    if (rc) return rc;
+    std::vector<uint8_t> tmp;
+    if (!status) {
+        tmp.resize(n);
+        status = tmp.data();
+    }
+    return host_batch(ctx, false, nkeys, desc, counters, n, buf, buf_len, status, nullptr, receivers != nullptr);
+}
+
+int rg_open_batch_host(rg_ctx *ctx, const uint8_t *keys, uint32_t nkeys, const rg_pkt_desc *desc, size_t n,
+                       uint8_t *buf, size_t buf_len, uint8_t *status, uint64_t *counters_out) {
+    int rc = check_ctx(ctx);
+    if (rc) return rc;
+    if (n == 0) return RG_OK;
+    if (!keys || !desc || !buf || !status || nkeys == 0) return set_err(RG_EINVAL, "open_host: bad args");
+    std::lock_guard<std::mutex> g(ctx->mu);
+    rc = upload_keys(ctx, keys, nullptr, nkeys);
+    if (rc) return rc;
+    std::vector<uint64_t> tmp;
+    if (!counters_out) {
+        tmp.resize(n);
+        counters_out = tmp.data();
+    }
+    return host_batch(ctx, true, nkeys, desc, nullptr, n, buf, buf_len, status, counters_out, false);
+}
+
+// ---------------------------------------------------- per-message drop-in
+static int general_one(rg_ctx *ctx, bool dec, const uint8_t key[32], const uint8_t nonce[12], const uint8_t *aad,
+                       size_t aad_len, uint8_t *payload, size_t len, uint8_t tag[16]) {
+    int rc = check_ctx(ctx);
+    if (rc) return rc;
+    if (!key || !nonce || !tag || (aad_len && !aad) || (len && !payload))
+        return set_err(RG_EINVAL, "aead: bad args");
+    if (len > (64ull << 32)) return set_err(RG_EINVAL, "aead: message too long for a 32-bit block counter");
+    std::lock_guard<std::mutex> g(ctx->mu);
+    const size_t aad_off = 0, pay_off = (aad_len + 15) & ~15ull, tag_off = pay_off + ((len + 15) & ~15ull);
+    const size_t arena = tag_off + 16;
+    RG_HIP(ctx->d_general.reserve(arena), "alloc arena");
+    RG_HIP(ctx->d_jobs.reserve(sizeof(rg::GeneralJob)), "alloc job");
+    uint8_t *d = static_cast<uint8_t *>(ctx->d_general.p);
+    rg::GeneralJob job;
+    memset(&job, 0, sizeof job);
+    memcpy(job.key, key, 32);
+    memcpy(job.nonce, nonce, 12);
+    job.decrypt = dec ? 1 : 0;
+    job.aad_off = aad_off;
+    job.aad_len = aad_len;
+    job.payload_off = pay_off;
+    job.payload_len = len;
+    job.tag_off = tag_off;
+    hipStream_t st = ctx->slots[0].stream;
+    if (aad_len) RG_HIP(hipMemcpyAsync(d + aad_off, aad, aad_len, hipMemcpyHostToDevice, st), "H2D aad");
+    if (len) RG_HIP(hipMemcpyAsync(d + pay_off, payload, len, hipMemcpyHostToDevice, st), "H2D payload");
+    if (dec) RG_HIP(hipMemcpyAsync(d + tag_off, tag, 16, hipMemcpyHostToDevice, st), "H2D tag");
+    RG_HIP(hipMemcpyAsync(ctx->d_jobs.p, &job, sizeof job, hipMemcpyHostToDevice, st), "H2D job");
+    RG_HIP(rg::launch_general(static_cast<rg::GeneralJob *>(ctx->d_jobs.p), 1, d, st), "general launch");
+    RG_HIP(hipMemcpyAsync(&job, ctx->d_jobs.p, sizeof job, hipMemcpyDeviceToHost, st), "D2H job");
+    RG_HIP(hipStreamSynchronize(st), "general sync");
+    if (dec && job.status != RG_PKT_OK) return RG_PKT_DECRYPT_ERR; // payload untouched
+    if (len) RG_HIP(hipMemcpy(payload, d + pay_off, len, hipMemcpyDeviceToHost), "D2H payload");
+    if (!dec) RG_HIP(hipMemcpy(tag, d + tag_off, 16, hipMemcpyDeviceToHost), "D2H tag");
+    return RG_OK;
+}
+
+int rg_chacha20poly1305_enc(rg_ctx *ctx, const uint8_t key[32], const uint8_t nonce[12], const uint8_t *aad,
+                            size_t aad_len, uint8_t *payload, size_t len, uint8_t tag[16]) {
+    return general_one(ctx, false, key, nonce, aad, aad_len, payload, len, tag);
+}
+
+int rg_chacha20poly1305_dec(rg_ctx *ctx, const uint8_t key[32], const uint8_t nonce[12], const uint8_t *aad,
+                            size_t aad_len, uint8_t *payload, size_t len, const uint8_t tag[16]) {
+    return general_one(ctx, true, key, nonce, aad, aad_len, payload, len, const_cast<uint8_t *>(tag));
+}
+
+// ------------------------------------------------------------- AntiReplay
+// rustyguard-utils/src/anti_replay.rs:1-64 with usize = u64:
+// BITMAP_LEN = 32 words, REDUNDANT_BIT_SHIFTS = 6, WINDOW_SIZE = 2048 - 64.
+void rg_antireplay_init(rg_antireplay *r) {
+    if (r) memset(r, 0, sizeof *r);
+}
+
+int rg_antireplay_would_accept(const rg_antireplay *r, uint64_t n) {
+    if (n > r->last) return 1;
+    const uint64_t d = r->last - n;
+    if (d >= RG_REPLAY_WINDOW) return 0;
+    const uint64_t index = n >> 6, shift = n & 63;
+    return ((r->bitmap[index & 31] >> shift) & 1) == 0;
+}
+
+void rg_antireplay_mark_seen(rg_antireplay *r, uint64_t n) {
+    const uint64_t index = n >> 6, shift = n & 63;
+    if (n > r->last) {
+        const uint64_t next_index = (r->last >> 6) + 1;
+        if (index > next_index && index - next_index > 32) {
+            memset(r->bitmap, 0, sizeof r->bitmap); // the window skipped entirely ahead
+        } else {
+            for (uint64_t i = next_index; i <= index; ++i) r->bitmap[i & 31] = 0;
+        }
+        r->last = n;
+    }
+    r->bitmap[index & 31] |= 1ull << shift;
+}
+
+} // extern "C"
+
+// ----------------------------------------------------------- session table
+namespace {
+struct Session {
+    bool used = false;
+    uint32_t local_id = 0, remote_id = 0;
+    uint64_t send_ctr = 0;
+    rg_antireplay replay{};
+};
+} // namespace
+
+struct rg_sessions {
+    rg_ctx *ctx = nullptr;
+    uint32_t cap = 0;
+    std::vector<Session> s;
+    std::vector<uint8_t> keys;       // rows [0,cap): send keys, [cap,2cap): recv keys
+    std::vector<uint32_t> receivers; // remote ids for send rows
+    std::unordered_map<uint32_t, uint32_t> by_local;
+};
+
+extern "C" {
+
+int rg_sessions_create(rg_ctx *ctx, uint32_t capacity, rg_sessions **out) {
+    if (!ctx || !out || capacity == 0 || capacity > (1u << 24)) return set_err(RG_EINVAL, "sessions: bad args");
+    rg_sessions *s = new (std::nothrow) rg_sessions();
+    if (!s) return set_err(RG_ENOMEM, "alloc sessions");
+    s->ctx = ctx;
+    s->cap = capacity;
+    s->s.resize(capacity);
+    s->keys.assign((size_t)capacity * 64, 0);
+    s->receivers.assign((size_t)capacity * 2, 0);
+    *out = s;
+    return RG_OK;
+}
+
+void rg_sessions_destroy(rg_sessions *s) {
+    if (!s) return;
+    std::fill(s->keys.begin(), s->keys.end(), 0); // zeroize, as prim.rs:227-231 / lib.rs:216-228
+    delete s;
+}
+
+int rg_sessions_insert(rg_sessions *s, uint32_t local_id, uint32_t remote_id, const uint8_t send_key[32],
+                       const uint8_t recv_key[32]) {
+    if (!s || !send_key || !recv_key) return set_err(RG_EINVAL, "insert: bad args");
+    if (s->by_local.count(local_id)) return set_err(RG_EINVAL, "insert: local id in use");
+    for (uint32_t i = 0; i < s->cap; ++i) {
+        Session &x = s->s[i];
+        if (x.used) continue;
+        x = Session();
+        x.used = true;
+        x.local_id = local_id;
+        x.remote_id = remote_id;
+        memcpy(&s->keys[(size_t)i * 32], send_key, 32);
+        memcpy(&s->keys[((size_t)s->cap + i) * 32], recv_key, 32);
+        s->receivers[i] = remote_id;
+        s->by_local[local_id] = i;
+        return (int)i;
+    }
+    return set_err(RG_EFULL, "insert: table full");
+}
+
+int rg_sessions_remove(rg_sessions *s, uint32_t slot) {
+    if (!s || slot >= s->cap || !s->s[slot].used) return set_err(RG_EINVAL, "remove: bad slot");
+    s->by_local.erase(s->s[slot].local_id);
+    s->s[slot] = Session();
+    memset(&s->keys[(size_t)slot * 32], 0, 32);
+    memset(&s->keys[((size_t)s->cap + slot) * 32], 0, 32);
+    return RG_OK;
+}
+
+int rg_sessions_lookup(const rg_sessions *s, uint32_t local_id) {
+    if (!s) return set_err(RG_EINVAL, "lookup: null");
+    auto it = s->by_local.find(local_id);
+    return it == s->by_local.end() ? RG_ENOTFOUND : (int)it->second;
+}
+
+uint64_t rg_sessions_send_counter(const rg_sessions *s, uint32_t slot) {
+    if (!s || slot >= s->cap) return 0;
+    return s->s[slot].send_ctr;
+}
+
+int rg_sessions_set_send_counter(rg_sessions *s, uint32_t slot, uint64_t counter) {
+    if (!s || slot >= s->cap || !s->s[slot].used) return set_err(RG_EINVAL, "set_counter: bad slot");
+    s->s[slot].send_ctr = counter;
+    return RG_OK;
+}
+
+rg_antireplay *rg_sessions_replay(rg_sessions *s, uint32_t slot) {
+    if (!s || slot >= s->cap) return nullptr;
+    return &s->s[slot].replay;
+}
+
+int rg_send_batch(rg_sessions *s, const uint32_t *slots, const rg_pkt_desc *desc, size_t n, uint8_t *buf,
+                  size_t buf_len, uint8_t *status, uint8_t *rekey_out) {
+    if (!s || !slots || !desc || !buf || !status) return set_err(RG_EINVAL, "send_batch: bad args");
+    if (n == 0) return RG_OK;
+    std::vector<rg_pkt_desc> d(desc, desc + n);
+    std::vector<uint64_t> ctr(n, 0);
+    std::vector<uint8_t> host_status(n, RG_PKT_OK);
+    for (size_t i = 0; i < n; ++i) {
+        if (rekey_out) rekey_out[i] = 0;
+        const uint32_t slot = slots[i];
+        if (slot >= s->cap || !s->s[slot].used) {
+            host_status[i] = RG_PKT_REJECTED; // no transport session: caller must handshake
+        } else if (d[i].len % 16 != 0) {
+            host_status[i] = RG_PKT_INVALID; // force_encrypt's padding assert, lib.rs:273-277
+        } else if (s->s[slot].send_ctr >= RG_REJECT_AFTER_MESSAGES) {
+            host_status[i] = RG_PKT_REJECTED; // should_reject, lib.rs:204-206
+        }
+        if (host_status[i] != RG_PKT_OK) {
+            d[i].key_idx = RG_KEY_SKIP;
+            continue;
+        }
+        Session &x = s->s[slot];
+        ctr[i] = x.send_ctr++; // EncryptionKey::encrypt, prim.rs:387-388
+        d[i].key_idx = slot;
+        if (rekey_out && x.send_ctr >= RG_REKEY_AFTER_MESSAGES) rekey_out[i] = 1; // lib.rs:564-570
+    }
+    int rc = rg_seal_batch_host(s->ctx, s->keys.data(), s->receivers.data(), s->cap, d.data(), ctr.data(), n, buf,
+                                buf_len, status);
+    if (rc) return rc;
+    for (size_t i = 0; i < n; ++i)
+        if (host_status[i] != RG_PKT_OK) status[i] = host_status[i];
+    return RG_OK;
+}
+
+int rg_recv_batch(rg_sessions *s, const rg_pkt_desc *desc, size_t n, uint8_t *buf, size_t buf_len,
+                  uint8_t *status, uint32_t *slots_out) {
+    if (!s || !desc || !buf || !status) return set_err(RG_EINVAL, "recv_batch: bad args");
+    if (n == 0) return RG_OK;
+    std::vector<rg_pkt_desc> d(desc, desc + n);
+    std::vector<uint8_t> host_status(n, 0xFF);
+    std::vector<uint32_t> slot_of(n, 0xFFFFFFFFu);
+    std::vector<uint64_t> ctr(n, 0);
+    for (size_t i = 0; i < n; ++i) {
+        const uint64_t off = d[i].offset;
+        const uint32_t w = d[i].len;
+        uint8_t st = 0xFF;
+        if (off > buf_len || buf_len - off < w) st = RG_PKT_INVALID;
+        else if (((uintptr_t)(buf + off) & 15) != 0) st = RG_PKT_UNALIGNED; // lib.rs:613-615
+        else if (w < 4) st = RG_PKT_INVALID;
+        else {
+            uint32_t type, recv;
+            memcpy(&type, buf + off, 4);
+            if (type != 4u) st = RG_PKT_NOT_DATA; // handshake/cookie: control plane
+            else if (w % 16 != 0 || w < 16) st = RG_PKT_INVALID; // message_mut_from
+            else {
+                memcpy(&recv, buf + off + 4, 4);
+                memcpy(&ctr[i], buf + off + 8, 8);
+                auto it = s->by_local.find(recv);
+                if (it == s->by_local.end()) st = RG_PKT_REJECTED; // lib.rs:646-650
+                else {
+                    slot_of[i] = it->second;
+                    // replay pre-filter with the pre-batch window: a counter rejected now is
+                    // rejected by any later window state too (the window only advances)
+                    if (!rg_antireplay_would_accept(&s->s[it->second].replay, ctr[i])) st = RG_PKT_REJECTED;
+                    else if (w < 32) st = RG_PKT_DECRYPT_ERR; // prim.rs:427-429
+                }
+            }
+        }
+        host_status[i] = st;
+        d[i].key_idx = st == 0xFF ? s->cap + slot_of[i] : RG_KEY_SKIP;
+    }
+    int rc = rg_open_batch_host(s->ctx, s->keys.data(), 2 * s->cap, d.data(), n, buf, buf_len, status, nullptr);
+    if (rc) return rc;
+    // in-order post-pass (RFC 6479 §3.4.3: only authenticated counters advance the window)
+    for (size_t i = 0; i < n; ++i) {
+        if (host_status[i] != 0xFF) {
+            status[i] = host_status[i];
+        } else if (status[i] == RG_PKT_OK) {
+            rg_antireplay *r = &s->s[slot_of[i]].replay;
+            if (rg_antireplay_would_accept(r, ctr[i])) rg_antireplay_mark_seen(r, ctr[i]);
+            else status[i] = RG_PKT_REJECTED; // duplicate inside this batch
+        }
+        if (slots_out) slots_out[i] = slot_of[i];
+    }
+    return RG_OK;
+}
+
+} // extern "C"

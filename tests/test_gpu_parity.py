@@ -1,0 +1,313 @@
+"""GPU parity: the HIP path (through the C ABI) against the pinned CPU oracle.
+
+Bit-exact comparisons everywhere (integer/byte work).  Small and medium
+batches are compared byte-for-byte with the oracle run live on the same
+inputs; the full BASELINE configurations are compared through SHA-256 of the
+sealed frames against tests/golden/config_digests.json (computed by the
+oracle, spot-checked with OpenSSL) plus the open round-trip property.
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+from conftest import load_golden
+from oracle import oracle
+from rustyguard_amd import aead, workloads
+from rustyguard_amd.workloads import DESC_DTYPE
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+def _dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def _random_batch(rng, n, nkeys=3, sizes=None, stride=None, counters=None):
+    if sizes is None:
+        sizes = rng.integers(0, 129, n) * 16  # P in [0, 2048], multiples of 16
+    sizes = np.asarray(sizes, np.int64)
+    desc = np.zeros(n, DESC_DTYPE)
+    W = sizes + 32
+    if stride:
+        desc["offset"] = np.arange(n, dtype=np.uint64) * stride
+        total = n * stride
+    else:
+        gaps = rng.integers(0, 3, n) * 16  # holes between frames
+        off = np.concatenate([[0], np.cumsum(W + gaps)[:-1]]).astype(np.uint64)
+        desc["offset"] = off
+        total = int(off[-1] + W[-1] + 64)
+    desc["len"] = sizes
+    desc["key_idx"] = rng.integers(0, nkeys, n)
+    keys = rng.integers(0, 256, (nkeys, 32), dtype=np.uint8)
+    rec = rng.integers(0, 2**32, nkeys, dtype=np.uint64).astype(np.uint32)
+    if counters is None:
+        counters = rng.integers(0, 2**62, n, dtype=np.uint64)
+    buf = rng.integers(0, 256, total, dtype=np.uint8)
+    return keys, rec, desc, np.asarray(counters, np.uint64), buf
+
+
+def _gpu_seal(engine, keys, rec, desc, counters, buf):
+    b = _dev(buf)
+    st = torch.zeros(len(desc), dtype=torch.uint8, device="cuda")
+    engine.seal_dev(_dev(keys), None if rec is None else _dev(rec.view(np.int32)),
+                    _dev(desc.view(np.uint8).reshape(-1, 16)), _dev(counters.view(np.int64)), b, st)
+    torch.cuda.synchronize()
+    return b.cpu().numpy(), st.cpu().numpy()
+
+
+def _gpu_open(engine, keys, desc_open, buf):
+    b = _dev(buf)
+    st = torch.zeros(len(desc_open), dtype=torch.uint8, device="cuda")
+    co = torch.zeros(len(desc_open), dtype=torch.int64, device="cuda")
+    engine.open_dev(_dev(keys), _dev(desc_open.view(np.uint8).reshape(-1, 16)), b, st, co)
+    torch.cuda.synchronize()
+    return b.cpu().numpy(), st.cpu().numpy(), co.cpu().numpy().view(np.uint64)
+
+
+def _lanes(engine):
+    return [1, 2, 4]
+
+
+# ------------------------------------------------------------ reference pins
+def test_reference_snapshots_per_message(engine):
+    """CryptoPrimatives drop-in reproduces the reference's insta snapshots."""
+    g = load_golden("reference_snapshots.json")
+    for v in g["transport_seals"]:
+        key = bytes.fromhex(v["key"])
+        buf = bytearray.fromhex(v["plaintext"])
+        tag = engine.chacha20poly1305_enc(key, aead.nonce(v["counter"]), b"", buf)
+        assert buf.hex() == v["ciphertext"] and tag.hex() == v["tag"]
+        engine.chacha20poly1305_dec(key, aead.nonce(v["counter"]), b"", buf, tag)
+        assert buf.hex() == v["plaintext"]
+
+
+@pytest.mark.parametrize("lanes", [1, 2, 4])
+def test_reference_framed_packet_batch(engine, lanes):
+    """rustyguard-core snapshot-3: the full 48-byte framed data packet."""
+    engine.set_lanes_per_packet(lanes)
+    v = load_golden("reference_snapshots.json")["framed_packets"][0]
+    keys = np.frombuffer(bytes.fromhex(v["key"]), np.uint8).reshape(1, 32)
+    pt = np.frombuffer(bytes.fromhex(v["plaintext"]), np.uint8)
+    desc = np.zeros(1, DESC_DTYPE)
+    desc["len"] = len(pt)
+    buf = np.zeros(len(pt) + 32, np.uint8)
+    buf[16:16 + len(pt)] = pt
+    out, st = _gpu_seal(engine, keys, np.array([v["receiver"]], np.uint32), desc,
+                        np.array([v["counter"]], np.uint64), buf)
+    assert st[0] == aead.PKT_OK
+    assert out.tobytes().hex() == v["frame"]
+    od = desc.copy()
+    od["len"] = len(buf)
+    back, st, ctr = _gpu_open(engine, keys, od, out)
+    assert st[0] == aead.PKT_OK and ctr[0] == v["counter"]
+    assert np.array_equal(back[16:32], pt)
+    forged = out.copy()
+    forged[v["tamper_byte"]] ^= 1
+    back, st, _ = _gpu_open(engine, keys, od, forged)
+    assert st[0] == aead.PKT_DECRYPT_ERR
+    assert np.array_equal(back, forged)  # untouched on failure
+    engine.set_lanes_per_packet(0)
+
+
+def test_per_message_openssl_vectors(engine):
+    g = load_golden("openssl_vectors.json")
+    for v in g["wg_transport"][::3] + g["general_aad"]:
+        key = bytes.fromhex(v["key"])
+        nz = bytes.fromhex(v["nonce"]) if "nonce" in v else aead.nonce(v["counter"])
+        aad = bytes.fromhex(v.get("aad", ""))
+        buf = bytearray.fromhex(v["plaintext"])
+        tag = engine.chacha20poly1305_enc(key, nz, aad, buf)
+        assert buf.hex() == v["ciphertext"] and tag.hex() == v["tag"]
+        engine.chacha20poly1305_dec(key, nz, aad, buf, tag)
+        assert buf.hex() == v["plaintext"]
+        if len(buf):
+            bad = bytearray(tag)
+            bad[0] ^= 0x80
+            ct = bytearray.fromhex(v["ciphertext"])
+            with pytest.raises(aead.DecryptionError):
+                engine.chacha20poly1305_dec(key, nz, aad, ct, bytes(bad))
+            assert ct.hex() == v["ciphertext"]
+
+
+@pytest.mark.parametrize("lanes", [1, 2, 4])
+def test_batch_openssl_transport_vectors(engine, lanes):
+    """Every 16-aligned OpenSSL transport vector, sealed in one batch."""
+    engine.set_lanes_per_packet(lanes)
+    vs = [v for v in load_golden("openssl_vectors.json")["wg_transport"] if (len(v["plaintext"]) // 2) % 16 == 0]
+    n = len(vs)
+    P = np.array([len(v["plaintext"]) // 2 for v in vs])
+    desc = np.zeros(n, DESC_DTYPE)
+    desc["offset"] = np.concatenate([[0], np.cumsum(P + 32)[:-1]])
+    desc["len"] = P
+    desc["key_idx"] = np.arange(n)
+    keys = np.stack([np.frombuffer(bytes.fromhex(v["key"]), np.uint8) for v in vs])
+    ctr = np.array([v["counter"] for v in vs], np.uint64)
+    buf = np.zeros(int((P + 32).sum()), np.uint8)
+    for d, v in zip(desc, vs):
+        buf[d["offset"] + 16: d["offset"] + 16 + d["len"]] = np.frombuffer(bytes.fromhex(v["plaintext"]), np.uint8)
+    out, st = _gpu_seal(engine, keys, None, desc, ctr, buf)
+    assert (st == aead.PKT_OK).all()
+    for d, v in zip(desc, vs):
+        o, p = int(d["offset"]), int(d["len"])
+        assert out[o + 16: o + 16 + p].tobytes().hex() == v["ciphertext"]
+        assert out[o + 16 + p: o + 32 + p].tobytes().hex() == v["tag"]
+    engine.set_lanes_per_packet(0)
+
+
+# ------------------------------------------------------- oracle differential
+@pytest.mark.parametrize("lanes", [1, 2, 4])
+@pytest.mark.parametrize("seed", [1, 2])
+def test_random_batches_vs_oracle(engine, lanes, seed):
+    engine.set_lanes_per_packet(lanes)
+    rng = np.random.default_rng(seed)
+    n = 3000
+    keys, rec, desc, ctr, buf = _random_batch(rng, n, nkeys=5)
+    ctr[:4] = [0, 0xFFFFFFFF, 0x100000000, 2**64 - 1]
+    want = buf.copy()
+    oracle.seal_batch(keys, rec, desc, ctr, want, nthreads=8)
+    got, st = _gpu_seal(engine, keys, rec, desc, ctr, buf)
+    assert (st == aead.PKT_OK).all()
+    assert np.array_equal(got, want)
+    # open the sealed frames back
+    od = desc.copy()
+    od["len"] += 32
+    back, st, co = _gpu_open(engine, keys, od, got)
+    assert (st == aead.PKT_OK).all()
+    assert np.array_equal(co, ctr)
+    for d in desc[:200]:
+        o, p = int(d["offset"]), int(d["len"])
+        assert np.array_equal(back[o + 16: o + 16 + p], buf[o + 16: o + 16 + p])
+    engine.set_lanes_per_packet(0)
+
+
+@pytest.mark.parametrize("lanes", [1, 2, 4])
+def test_open_failures_leave_frames_untouched(engine, lanes):
+    engine.set_lanes_per_packet(lanes)
+    rng = np.random.default_rng(9)
+    n = 512
+    keys, rec, desc, ctr, buf = _random_batch(rng, n, nkeys=2, sizes=rng.integers(1, 96, n) * 16)
+    oracle.seal_batch(keys, rec, desc, ctr, buf)
+    od = desc.copy()
+    od["len"] += 32
+    sealed = buf.copy()
+    # tamper every 3rd packet at a random byte of payload or tag
+    bad = np.arange(0, n, 3)
+    for i in bad:
+        o, w = int(od[i]["offset"]), int(od[i]["len"])
+        buf[o + int(rng.integers(16, w))] ^= 1 << int(rng.integers(0, 8))
+    tampered = buf.copy()
+    back, st, _ = _gpu_open(engine, keys, od, buf)
+    want_st, _ = oracle.open_batch(keys, od, tampered.copy())
+    assert np.array_equal(st, want_st)
+    assert (st[bad] == aead.PKT_DECRYPT_ERR).all()
+    for i in bad:
+        o, w = int(od[i]["offset"]), int(od[i]["len"])
+        assert np.array_equal(back[o:o + w], tampered[o:o + w])
+    good = np.setdiff1d(np.arange(n), bad)
+    assert (st[good] == aead.PKT_OK).all()
+    engine.set_lanes_per_packet(0)
+
+
+def test_open_malformed_statuses_match_oracle(engine):
+    rng = np.random.default_rng(5)
+    keys = rng.integers(0, 256, (2, 32), dtype=np.uint8)
+    buf = np.zeros(4096, np.uint8)
+    cases = [  # (offset, W, type, key_idx)
+        (0, 48, 4, 0),        # decrypt error (random tag)
+        (64, 47, 4, 0),       # W % 16 != 0 -> InvalidMessage
+        (128, 3, 4, 0),       # shorter than the type word
+        (192, 16, 4, 0),      # header only -> DecryptionError (no tag)
+        (256, 64, 1, 0),      # handshake init type -> not data
+        (520, 48, 4, 0),      # unaligned
+        (640, 32, 4, 0),      # empty payload + random tag -> DecryptionError
+        (704, 48, 4, 0xFFFFFFFF),  # skipped by the host
+        (4080, 48, 4, 0),     # runs past the arena
+    ]
+    desc = np.zeros(len(cases), DESC_DTYPE)
+    for i, (o, w, t, k) in enumerate(cases):
+        desc[i] = (o, w, k)
+        if o + 4 <= len(buf):
+            buf[o:o + 4] = np.frombuffer(np.uint32(t).tobytes(), np.uint8)
+            buf[o + 8:o + 16] = rng.integers(0, 256, 8, dtype=np.uint8)
+    want, wctr = oracle.open_batch(keys, desc[[0, 1, 2, 3, 4, 5, 6]], buf.copy())
+    back, st, co = _gpu_open(engine, keys, desc, buf)
+    assert list(st[:7]) == list(want)
+    assert st[7] == aead.PKT_REJECTED and st[8] == aead.PKT_INVALID
+    assert list(st) == [1, 2, 2, 1, 5, 4, 1, 3, 2]
+
+
+def test_seal_rejects_bad_descriptors(engine):
+    keys = np.zeros((1, 32), np.uint8)
+    desc = np.zeros(4, DESC_DTYPE)
+    desc[0] = (0, 17, 0)      # P % 16 != 0
+    desc[1] = (8, 16, 0)      # unaligned
+    desc[2] = (64, 16, 3)     # key out of range
+    desc[3] = (4000, 512, 0)  # past the end
+    buf = np.arange(4096, dtype=np.uint32).astype(np.uint8)
+    out, st = _gpu_seal(engine, keys, None, desc, np.zeros(4, np.uint64), buf)
+    assert list(st) == [aead.PKT_INVALID] * 4
+    assert np.array_equal(out, buf)
+
+
+def test_empty_payload_keepalive(engine):
+    """Keepalive seals an empty payload (rustyguard-core/src/time.rs:131): 32-byte frame."""
+    keys = np.frombuffer(bytes(range(32)), np.uint8).reshape(1, 32)
+    desc = np.zeros(1, DESC_DTYPE)
+    buf = np.zeros(32, np.uint8)
+    out, st = _gpu_seal(engine, keys, np.array([7], np.uint32), desc, np.array([5], np.uint64), buf)
+    want = buf.copy()
+    oracle.seal_batch(keys, np.array([7], np.uint32), desc, np.array([5], np.uint64), want)
+    assert np.array_equal(out, want)
+
+
+def test_host_path_matches_oracle(engine):
+    rng = np.random.default_rng(11)
+    n = 20000
+    keys, rec, desc, ctr, buf = _random_batch(rng, n, nkeys=7)
+    want = buf.copy()
+    oracle.seal_batch(keys, rec, desc, ctr, want, nthreads=8)
+    got = buf.copy()
+    st = engine.seal_host(keys, rec, desc, ctr, got)
+    assert (st == aead.PKT_OK).all() and np.array_equal(got, want)
+    od = desc.copy()
+    od["len"] += 32
+    st, co = engine.open_host(keys, od, got)
+    assert (st == aead.PKT_OK).all() and np.array_equal(co, ctr)
+    assert np.array_equal(got[16:16 + int(desc[0]["len"])], buf[16:16 + int(desc[0]["len"])])
+
+
+# ------------------------------------------------------- full configurations
+@pytest.mark.parametrize("name", ["cfg2", "cfg3", "cfg4"])
+def test_full_config_digest(engine, name):
+    from rustyguard_amd.device import DeviceBatch
+
+    dig = load_golden("config_digests.json")[name]
+    w = workloads.build(name)
+    assert w.n == dig["n"] and w.buf_bytes == dig["buf_bytes"]
+    b = DeviceBatch(engine, w)
+    b.fill()
+    torch.cuda.synchronize()
+    assert hashlib.sha256(b.host_buf().tobytes()).hexdigest() == dig["plain_sha256"]
+    for lanes in _lanes(engine):
+        engine.set_lanes_per_packet(lanes)
+        b.fill()
+        b.seal()
+        torch.cuda.synchronize()
+        assert (b.status[: w.n] == 0).all().item()
+        assert hashlib.sha256(b.host_buf().tobytes()).hexdigest() == dig["sealed_sha256"], lanes
+        b.open()
+        torch.cuda.synchronize()
+        assert (b.status[: w.n] == 0).all().item()
+        assert torch.equal(b.counters_out[: w.n], b.counters)
+        assert hashlib.sha256(b.host_buf().tobytes()).hexdigest() != dig["sealed_sha256"]
+        # plaintext restored except the framing (header + tag) written by seal
+        hb = b.host_buf()
+        plain = np.zeros_like(hb)
+        oracle.synth_fill(plain, w.desc, w.inner_len, w.data_seed)
+        for d in w.desc[:: max(1, w.n // 500)]:
+            o, p = int(d["offset"]), int(d["len"])
+            assert np.array_equal(hb[o + 16:o + 16 + p], plain[o + 16:o + 16 + p])
+    engine.set_lanes_per_packet(0)

@@ -1,0 +1,99 @@
+"""Pin the CPU oracle before it is trusted as the checker.
+
+Sources of truth:
+  * the reference's own insta snapshots (rustyguard-crypto handshake-{4..7},
+    rustyguard-core snapshot-3) -- bytes committed in tests/golden/;
+  * RFC 8439 known answers (the algorithm graviola 0.2.0 implements);
+  * OpenSSL EVP_chacha20_poly1305 multi-block vectors (generated here).
+"""
+import numpy as np
+import pytest
+
+from conftest import load_golden
+from oracle import openssl_ref, oracle
+
+
+def _seal(v):
+    return oracle.aead_seal(bytes.fromhex(v["key"]), oracle.wg_nonce(v["counter"]), b"", bytes.fromhex(v["plaintext"]))
+
+
+@pytest.mark.parametrize("v", load_golden("reference_snapshots.json")["transport_seals"], ids=lambda v: v["source"][:45])
+def test_reference_transport_snapshots(v):
+    # EncryptionKey::encrypt -> (ciphertext in place, tag) == insta snapshot
+    ct, tag = _seal(v)
+    assert ct.hex() == v["ciphertext"]
+    assert tag.hex() == v["tag"]
+    # DecryptionKey::decrypt round trip (rustyguard-crypto/src/lib.rs:548-549)
+    pt = oracle.aead_open(bytes.fromhex(v["key"]), oracle.wg_nonce(v["counter"]), b"", ct, tag)
+    assert pt == bytes.fromhex(v["plaintext"])
+
+
+def test_reference_framed_packet_and_tamper():
+    v = load_golden("reference_snapshots.json")["framed_packets"][0]
+    keys = np.frombuffer(bytes.fromhex(v["key"]), np.uint8).reshape(1, 32)
+    desc = np.zeros(1, oracle.DESC_DTYPE)
+    pt = bytes.fromhex(v["plaintext"])
+    desc["len"] = len(pt)
+    buf = np.zeros(len(pt) + 32, np.uint8)
+    buf[16:16 + len(pt)] = np.frombuffer(pt, np.uint8)
+    oracle.seal_batch(keys, np.array([v["receiver"]], np.uint32), desc, np.array([v["counter"]], np.uint64), buf)
+    assert buf.tobytes().hex() == v["frame"]
+    # open the framed packet (Sessions::recv_message -> Message::Read)
+    odesc = desc.copy()
+    odesc["len"] = len(buf)
+    b2 = buf.copy()
+    st, ctr = oracle.open_batch(keys, odesc, b2)
+    assert st[0] == oracle.OK and ctr[0] == v["counter"]
+    assert b2[16:16 + len(pt)].tobytes() == pt
+    # forged_packet_does_not_update_peer_endpoint: flip byte 47 -> DecryptionError, frame untouched
+    b3 = buf.copy()
+    b3[v["tamper_byte"]] ^= 1
+    before = b3.copy()
+    st, _ = oracle.open_batch(keys, odesc, b3)
+    assert st[0] == oracle.DECRYPT_ERR
+    assert np.array_equal(b3, before)
+
+
+def test_rfc8439_known_answers():
+    g = load_golden("rfc8439.json")
+    for b in g["chacha20_block"]:
+        out = oracle.chacha20_block(bytes.fromhex(b["key"]), b["counter"], bytes.fromhex(b["nonce"]))
+        assert out.hex() == b["block"] and out.hex().startswith(b["block_prefix"])
+    for p in g["poly1305"]:
+        assert oracle.poly1305(bytes.fromhex(p["key"]), bytes.fromhex(p["message"])).hex() == p["tag"]
+    for a in g["aead"]:
+        ct, tag = oracle.aead_seal(bytes.fromhex(a["key"]), bytes.fromhex(a["nonce"]), bytes.fromhex(a["aad"]),
+                                   bytes.fromhex(a["plaintext"]))
+        assert tag.hex() == a["tag"] and ct.hex() == a["ciphertext"]
+
+
+def test_openssl_vectors():
+    g = load_golden("openssl_vectors.json")
+    for v in g["wg_transport"]:
+        ct, tag = _seal(v)
+        assert (ct.hex(), tag.hex()) == (v["ciphertext"], v["tag"]), (len(v["plaintext"]) // 2, v["counter"])
+    for v in g["general_aad"]:
+        ct, tag = oracle.aead_seal(bytes.fromhex(v["key"]), bytes.fromhex(v["nonce"]), bytes.fromhex(v["aad"]),
+                                   bytes.fromhex(v["plaintext"]))
+        assert (ct.hex(), tag.hex()) == (v["ciphertext"], v["tag"])
+
+
+@pytest.mark.skipif(not openssl_ref.available(), reason="libcrypto not present")
+def test_oracle_vs_openssl_random():
+    rng = np.random.default_rng(1234)
+    for _ in range(200):
+        ln = int(rng.integers(0, 2100))
+        key = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
+        ctr = int(rng.integers(0, 2**63)) * 2 + int(rng.integers(0, 2))
+        pt = rng.integers(0, 256, ln, dtype=np.uint8).tobytes()
+        n = oracle.wg_nonce(ctr)
+        assert oracle.aead_seal(key, n, b"", pt) == openssl_ref.seal(key, n, b"", pt)
+
+
+def test_oracle_open_rejects_every_single_bit_flip_of_tag():
+    key, pt = bytes(range(32)), b"x" * 64
+    ct, tag = oracle.aead_seal(key, oracle.wg_nonce(7), b"", pt)
+    for bit in range(128):
+        t = bytearray(tag)
+        t[bit // 8] ^= 1 << (bit % 8)
+        assert oracle.aead_open(key, oracle.wg_nonce(7), b"", ct, bytes(t)) is None
