@@ -105,9 +105,23 @@ int rg_seal_batch_dev(rg_ctx *ctx, const uint8_t *keys, const uint32_t *receiver
 int rg_open_batch_dev(rg_ctx *ctx, const uint8_t *keys, uint32_t nkeys, const rg_pkt_desc *desc, size_t n,
                       uint8_t *buf, size_t buf_len, uint8_t *status, uint64_t *counters_out, void *stream);
 
-/* Tuning knob: lanes cooperating on one packet (0 = automatic, else 1/2/4). */
+/* Tuning knobs.  lanes: lanes cooperating on one packet (0 = automatic, else
+ * 1/2/4).  wg_per_cu: resident 256-thread workgroups per CU of the persistent
+ * grid (0 = automatic, -1 = plain one-shot grid). */
 int rg_set_lanes_per_packet(rg_ctx *ctx, int lanes);
 int rg_get_lanes_per_packet(rg_ctx *ctx, size_t n);
+int rg_set_wg_per_cu(rg_ctx *ctx, int wg_per_cu);
+/* Kernel choice: 0 = lane-pass kernels (K lanes per packet, direct loads),
+ * 1/2/4 = LDS-staged tiles (one packet per lane, coalesced LDS-DMA windows
+ * of that many 64-byte chunks). */
+int rg_set_staged(rg_ctx *ctx, int window_chunks);
+/* Diagnostics only (profiling the seal kernel, output is NOT a valid seal):
+ * 0 = normal, 1 = compute only (no payload loads/stores), 2 = memory only. */
+int rg_set_debug_mode(rg_ctx *ctx, int mode);
+/* mode 3 (staged kernels): per-wave s_memtime section totals are written to
+ * this device buffer, 8 x u64 per wave (setup, store, dma-issue, dma-wait,
+ * chunk, tail, valid, 0). */
+int rg_set_debug_buffer(rg_ctx *ctx, void *dev_ptr);
 
 /* ----------------------------------------- host-memory batch (blocking) */
 /* Same contract with host pointers: frames are staged H2D, sealed/opened on

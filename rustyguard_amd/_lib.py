@@ -30,6 +30,10 @@ SIGNATURES = {
     "rg_open_batch_dev": (c_int, [c_vp, c_u8p, c_u32, c_vp, c_size, c_u8p, c_size, c_u8p, c_vp, c_vp]),
     "rg_set_lanes_per_packet": (c_int, [c_vp, c_int]),
     "rg_get_lanes_per_packet": (c_int, [c_vp, c_size]),
+    "rg_set_wg_per_cu": (c_int, [c_vp, c_int]),
+    "rg_set_debug_mode": (c_int, [c_vp, c_int]),
+    "rg_set_staged": (c_int, [c_vp, c_int]),
+    "rg_set_debug_buffer": (c_int, [c_vp, c_vp]),
     "rg_seal_batch_host": (c_int, [c_vp, c_u8p, c_vp, c_u32, c_vp, c_vp, c_size, c_u8p, c_size, c_u8p]),
     "rg_open_batch_host": (c_int, [c_vp, c_u8p, c_u32, c_vp, c_size, c_u8p, c_size, c_u8p, c_vp]),
     "rg_host_alloc": (c_vp, [c_size]),

@@ -107,6 +107,22 @@ class Engine:
     def set_lanes_per_packet(self, lanes: int):
         check(self._L.rg_set_lanes_per_packet(self._h, lanes), "rg_set_lanes_per_packet")
 
+    def set_staged(self, window_chunks: int):
+        """0 = lane-pass kernels; 1/2/4 = LDS-staged tile kernel with that window."""
+        check(self._L.rg_set_staged(self._h, window_chunks), "rg_set_staged")
+
+    def set_debug_mode(self, mode: int):
+        """Diagnostics: 1 = compute-only seal, 2 = memory-only seal (outputs invalid)."""
+        check(self._L.rg_set_debug_mode(self._h, mode), "rg_set_debug_mode")
+
+    def set_debug_buffer(self, tensor):
+        """Diagnostics: device buffer receiving per-wave stamp totals (debug mode 3)."""
+        check(self._L.rg_set_debug_buffer(self._h, _vp(tensor) if tensor is not None else None),
+              "rg_set_debug_buffer")
+
+    def set_wg_per_cu(self, wg: int):
+        check(self._L.rg_set_wg_per_cu(self._h, wg), "rg_set_wg_per_cu")
+
     def lanes_per_packet(self, n: int) -> int:
         return check(self._L.rg_get_lanes_per_packet(self._h, n), "rg_get_lanes_per_packet")
 

@@ -91,7 +91,13 @@ struct Slot {
 
 struct rg_ctx {
     int device = 0;
-    int lanes = 0;
+    int lanes = 0;      // 0 = auto
+    int wg_per_cu = 0;  // 0 = auto, -1 = plain one-shot grid (no LDS reservation)
+    int cus = 0;
+    int debug_mode = 0;
+    int staged_g = 2; // 0 = lane-pass kernels, else LDS-staged windows of G chunks (default: 2)
+    uint64_t *dbg = nullptr; // diagnostics buffer (device), stamp builds only
+    int max_wg[2][3] = {{0, 0, 0}, {0, 0, 0}}; // [seal, open][K = 1, 2, 4]
     std::mutex mu;
     Slot slots[2];
     DevBuf d_keys, d_recv;
@@ -126,6 +132,14 @@ int rg_create(int device, rg_ctx **out) {
     rg_ctx *c = new (std::nothrow) rg_ctx();
     if (!c) return set_err(RG_ENOMEM, "alloc ctx");
     c->device = device;
+    {
+        hipError_t e = hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device);
+        if (e == hipSuccess) e = rg::prepare_kernels(c->max_wg);
+        if (e != hipSuccess) {
+            delete c;
+            return set_err(RG_EDEVICE, "kernel setup", e);
+        }
+    }
     for (auto &s : c->slots) {
         hipError_t e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
         if (e != hipSuccess) {
@@ -163,9 +177,96 @@ int rg_set_lanes_per_packet(rg_ctx *ctx, int lanes) {
 }
 
 int rg_get_lanes_per_packet(rg_ctx *ctx, size_t n) {
-    (void)n;
     if (!ctx) return set_err(RG_EINVAL, "null context");
-    return 1;
+    if (ctx->lanes) return ctx->lanes;
+    // fewest lanes per packet that still gives every SIMD >= 2 waves
+    // (n * K lanes >= CUs * 2 workgroups * 256 lanes)
+    const size_t want = (size_t)(ctx->cus > 0 ? ctx->cus : 256) * 512;
+    if (n >= want) return 1;
+    if (2 * n >= want) return 2;
+    return 4;
+}
+
+int rg_set_wg_per_cu(rg_ctx *ctx, int wg) {
+    if (!ctx) return set_err(RG_EINVAL, "null context");
+    if (wg < -1 || wg > 8) return set_err(RG_EINVAL, "wg_per_cu must be -1..8");
+    ctx->wg_per_cu = wg;
+    return RG_OK;
+}
+
+int rg_set_staged(rg_ctx *ctx, int g) {
+    if (!ctx) return set_err(RG_EINVAL, "null context");
+    if (g != 0 && g != 1 && g != 2 && g != 4) return set_err(RG_EINVAL, "staged window must be 0, 1, 2 or 4 chunks");
+    ctx->staged_g = g;
+    return RG_OK;
+}
+
+int rg_set_debug_buffer(rg_ctx *ctx, void *dev_ptr) {
+    if (!ctx) return set_err(RG_EINVAL, "null context");
+    ctx->dbg = static_cast<uint64_t *>(dev_ptr);
+    return RG_OK;
+}
+
+int rg_set_debug_mode(rg_ctx *ctx, int mode) {
+    if (!ctx) return set_err(RG_EINVAL, "null context");
+    if (mode < 0 || mode > 3) return set_err(RG_EINVAL, "debug mode must be 0..3");
+    ctx->debug_mode = mode;
+    return RG_OK;
+}
+
+static rg::Launch launch_cfg(rg_ctx *ctx, size_t n, bool open) {
+    rg::Launch L;
+    L.lanes = rg_get_lanes_per_packet(ctx, n);
+    L.cus = ctx->cus;
+    L.debug_mode = open ? 0 : ctx->debug_mode;
+    if (L.debug_mode == 3 && ctx->staged_g == 0) L.debug_mode = 0;
+    L.staged_g = ctx->staged_g;
+    const int k = L.lanes == 1 ? 0 : L.lanes == 2 ? 1 : 2;
+    const int cap = std::max(1, ctx->max_wg[open ? 1 : 0][k]);
+    if (ctx->wg_per_cu < 0) {
+        L.wg_per_cu = 0;
+    } else if (ctx->wg_per_cu > 0) {
+        L.wg_per_cu = std::min(ctx->wg_per_cu, cap);
+    } else {
+        // enough resident workgroups for one packet per lane group, capped by occupancy
+        const size_t need = ((size_t)n * L.lanes + 255) / 256;
+        const size_t per_cu = (need + L.cus - 1) / std::max(1, L.cus);
+        L.wg_per_cu = (int)std::max<size_t>(1, std::min<size_t>(per_cu, (size_t)cap));
+    }
+    return L;
+}
+
+// Staged kernel residency: one 4-wave workgroup per CU handles 4 tiles of 64
+// packets at a time; a second resident workgroup (2 waves per SIMD) pays off
+// once every CU has at least two workgroups' worth of tiles.
+static int staged_wg_per_cu(rg_ctx *ctx, size_t n) {
+    if (ctx->wg_per_cu > 0) return ctx->wg_per_cu;
+    const size_t tiles = (n + 63) / 64;
+    const size_t wgs = (tiles + 3) / 4;
+    return wgs >= (size_t)ctx->cus * 2 ? 2 : 1;
+}
+
+static hipError_t launch_seal_any(rg_ctx *ctx, const rg::SealArgs &a0, hipStream_t st) {
+    rg::SealArgs a = a0;
+    a.dbg = ctx->debug_mode == 3 ? ctx->dbg : nullptr;
+    rg::Launch L = launch_cfg(ctx, a.n, false);
+    if (L.staged_g > 0 && (L.debug_mode == 0 || L.debug_mode == 3)) {
+        L.wg_per_cu = staged_wg_per_cu(ctx, a.n);
+        return rg::launch_staged(&a, nullptr, L.staged_g, L, st);
+    }
+    return rg::launch_seal(a, L, st);
+}
+
+static hipError_t launch_open_any(rg_ctx *ctx, const rg::OpenArgs &a0, hipStream_t st) {
+    rg::OpenArgs a = a0;
+    a.dbg = ctx->debug_mode == 3 ? ctx->dbg : nullptr;
+    rg::Launch L = launch_cfg(ctx, a.n, true);
+    L.debug_mode = ctx->debug_mode == 3 ? 3 : 0;
+    if (L.staged_g > 0) {
+        L.wg_per_cu = staged_wg_per_cu(ctx, a.n);
+        return rg::launch_staged(nullptr, &a, L.staged_g, L, st);
+    }
+    return rg::launch_open(a, L, st);
 }
 
 // --------------------------------------------------------------- device API
@@ -175,8 +276,9 @@ int rg_seal_batch_dev(rg_ctx *ctx, const uint8_t *keys, const uint32_t *receiver
     int rc = check_ctx(ctx);
     if (rc) return rc;
     if (n == 0) return RG_OK;
-    if (!keys || !desc || !counters || !buf || n > 0xFFFFFFFFull) return set_err(RG_EINVAL, "seal: bad args");
-    rg::SealArgs a;
+    if (!keys || !desc || !counters || !buf || nkeys == 0 || n > 0xFFFFFFFFull)
+        return set_err(RG_EINVAL, "seal: bad args");
+    rg::SealArgs a{};
     a.keys = reinterpret_cast<const uint32_t *>(keys);
     a.receivers = receivers;
     a.desc = desc;
@@ -186,7 +288,7 @@ int rg_seal_batch_dev(rg_ctx *ctx, const uint8_t *keys, const uint32_t *receiver
     a.status = status;
     a.nkeys = nkeys;
     a.n = (uint32_t)n;
-    RG_HIP(rg::launch_seal(a, rg_get_lanes_per_packet(ctx, n), (hipStream_t)stream), "seal launch");
+    RG_HIP(launch_seal_any(ctx, a, (hipStream_t)stream), "seal launch");
     return RG_OK;
 }
 
@@ -195,8 +297,9 @@ int rg_open_batch_dev(rg_ctx *ctx, const uint8_t *keys, uint32_t nkeys, const rg
     int rc = check_ctx(ctx);
     if (rc) return rc;
     if (n == 0) return RG_OK;
-    if (!keys || !desc || !buf || !status || n > 0xFFFFFFFFull) return set_err(RG_EINVAL, "open: bad args");
-    rg::OpenArgs a;
+    if (!keys || !desc || !buf || !status || nkeys == 0 || n > 0xFFFFFFFFull)
+        return set_err(RG_EINVAL, "open: bad args");
+    rg::OpenArgs a{};
     a.keys = reinterpret_cast<const uint32_t *>(keys);
     a.desc = desc;
     a.buf = buf;
@@ -205,7 +308,7 @@ int rg_open_batch_dev(rg_ctx *ctx, const uint8_t *keys, uint32_t nkeys, const rg
     a.counters_out = counters_out;
     a.nkeys = nkeys;
     a.n = (uint32_t)n;
-    RG_HIP(rg::launch_open(a, rg_get_lanes_per_packet(ctx, n), (hipStream_t)stream), "open launch");
+    RG_HIP(launch_open_any(ctx, a, (hipStream_t)stream), "open launch");
     return RG_OK;
 }
 
@@ -311,7 +414,7 @@ int host_batch(rg_ctx *ctx, bool open, uint32_t nkeys, const rg_pkt_desc *desc, 
             RG_HIP(s.h_ctr.reserve(m * 8), "alloc h_ctr");
             memcpy(s.h_ctr.p, counters + i, m * 8);
             RG_HIP(hipMemcpyAsync(s.d_ctr.p, s.h_ctr.p, m * 8, hipMemcpyHostToDevice, st), "H2D ctr");
-            rg::SealArgs a;
+            rg::SealArgs a{};
             a.keys = static_cast<const uint32_t *>(ctx->d_keys.p);
             a.receivers = with_receivers ? static_cast<const uint32_t *>(ctx->d_recv.p) : nullptr;
             a.desc = static_cast<const rg_pkt_desc *>(s.d_desc.p);
@@ -321,11 +424,11 @@ int host_batch(rg_ctx *ctx, bool open, uint32_t nkeys, const rg_pkt_desc *desc, 
             a.status = static_cast<uint8_t *>(s.d_status.p);
             a.nkeys = nkeys;
             a.n = (uint32_t)m;
-            RG_HIP(rg::launch_seal(a, rg_get_lanes_per_packet(ctx, m), st), "seal launch");
+            RG_HIP(launch_seal_any(ctx, a, st), "seal launch");
         } else {
             RG_HIP(s.d_ctr_out.reserve(m * 8), "alloc ctr_out");
             RG_HIP(s.h_ctr_out.reserve(m * 8), "alloc h_ctr_out");
-            rg::OpenArgs a;
+            rg::OpenArgs a{};
             a.keys = static_cast<const uint32_t *>(ctx->d_keys.p);
             a.desc = static_cast<const rg_pkt_desc *>(s.d_desc.p);
             a.buf = dbuf;
@@ -334,7 +437,7 @@ int host_batch(rg_ctx *ctx, bool open, uint32_t nkeys, const rg_pkt_desc *desc, 
             a.counters_out = static_cast<uint64_t *>(s.d_ctr_out.p);
             a.nkeys = nkeys;
             a.n = (uint32_t)m;
-            RG_HIP(rg::launch_open(a, rg_get_lanes_per_packet(ctx, m), st), "open launch");
+            RG_HIP(launch_open_any(ctx, a, st), "open launch");
             RG_HIP(hipMemcpyAsync(s.h_ctr_out.p, s.d_ctr_out.p, m * 8, hipMemcpyDeviceToHost, st), "D2H ctr");
         }
         if (span) RG_HIP(hipMemcpyAsync(buf + lo, s.d_buf.p, span, hipMemcpyDeviceToHost, st), "D2H frames");

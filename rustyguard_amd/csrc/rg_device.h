@@ -60,6 +60,136 @@ __device__ __forceinline__ void chacha_block(const Key8 &key, uint32_t block, ui
     out[15] = x15 + n2;
 }
 
+// Per-packet ChaCha20 state with the block-counter-independent part of the
+// first column round hoisted: of QR(0,4,8,12) QR(1,5,9,13) QR(2,6,10,14)
+// QR(3,7,11,15) only the first reads word 12 (the block counter), so the other
+// three are computed once per packet instead of once per 64-byte block.
+struct Stream {
+    Key8 key;
+    uint32_t n0, n1, n2;
+    uint32_t x0p;                  // 0x61707865 + k0: first step of QR(0,4,8,12)
+    uint32_t c1[4], c2[4], c3[4];  // QR1..QR3 outputs (a, b, c, d) after the first column round
+};
+
+__device__ __forceinline__ Stream make_stream(const Key8 &key, uint32_t n0, uint32_t n1, uint32_t n2) {
+    Stream st;
+    st.key = key;
+    st.n0 = n0;
+    st.n1 = n1;
+    st.n2 = n2;
+    st.x0p = 0x61707865u + key.k[0];
+    uint32_t a = 0x3320646eu, b = key.k[1], c = key.k[5], d = n0;
+    RG_QR(a, b, c, d);
+    st.c1[0] = a; st.c1[1] = b; st.c1[2] = c; st.c1[3] = d;
+    a = 0x79622d32u; b = key.k[2]; c = key.k[6]; d = n1;
+    RG_QR(a, b, c, d);
+    st.c2[0] = a; st.c2[1] = b; st.c2[2] = c; st.c2[3] = d;
+    a = 0x6b206574u; b = key.k[3]; c = key.k[7]; d = n2;
+    RG_QR(a, b, c, d);
+    st.c3[0] = a; st.c3[1] = b; st.c3[2] = c; st.c3[3] = d;
+    return st;
+}
+
+// Keystream block `block` of a Stream (identical output to chacha_block).
+__device__ __forceinline__ void stream_block(const Stream &st, uint32_t block, uint32_t out[16]) {
+    // finish QR(0,4,8,12) of the first column round: a += b was hoisted (x0p)
+    uint32_t x0 = st.x0p, x4 = st.key.k[0], x8 = st.key.k[4], x12 = block;
+    x12 ^= x0; x12 = rotl(x12, 16);
+    x8 += x12; x4 ^= x8; x4 = rotl(x4, 12);
+    x0 += x4; x12 ^= x0; x12 = rotl(x12, 8);
+    x8 += x12; x4 ^= x8; x4 = rotl(x4, 7);
+    uint32_t x1 = st.c1[0], x5 = st.c1[1], x9 = st.c1[2], x13 = st.c1[3];
+    uint32_t x2 = st.c2[0], x6 = st.c2[1], x10 = st.c2[2], x14 = st.c2[3];
+    uint32_t x3 = st.c3[0], x7 = st.c3[1], x11 = st.c3[2], x15 = st.c3[3];
+    // first diagonal round
+    RG_QR(x0, x5, x10, x15);
+    RG_QR(x1, x6, x11, x12);
+    RG_QR(x2, x7, x8, x13);
+    RG_QR(x3, x4, x9, x14);
+#pragma unroll
+    for (int i = 1; i < 10; i++) {
+        RG_QR(x0, x4, x8, x12);
+        RG_QR(x1, x5, x9, x13);
+        RG_QR(x2, x6, x10, x14);
+        RG_QR(x3, x7, x11, x15);
+        RG_QR(x0, x5, x10, x15);
+        RG_QR(x1, x6, x11, x12);
+        RG_QR(x2, x7, x8, x13);
+        RG_QR(x3, x4, x9, x14);
+    }
+    out[0] = x0 + 0x61707865u;
+    out[1] = x1 + 0x3320646eu;
+    out[2] = x2 + 0x79622d32u;
+    out[3] = x3 + 0x6b206574u;
+    out[4] = x4 + st.key.k[0];
+    out[5] = x5 + st.key.k[1];
+    out[6] = x6 + st.key.k[2];
+    out[7] = x7 + st.key.k[3];
+    out[8] = x8 + st.key.k[4];
+    out[9] = x9 + st.key.k[5];
+    out[10] = x10 + st.key.k[6];
+    out[11] = x11 + st.key.k[7];
+    out[12] = x12 + block;
+    out[13] = x13 + st.n0;
+    out[14] = x14 + st.n1;
+    out[15] = x15 + st.n2;
+}
+
+// stream_block with a hook run after double-round i (i = 0..9), so that
+// independent work (the previous chunk's Poly1305) is placed between the
+// ARX rounds in program order: the compiler schedules close to source order,
+// and the interleave fills the dependency gaps of both chains.
+template <typename Hook>
+__device__ __forceinline__ void stream_block_hooked(const Stream &st, uint32_t block, uint32_t out[16], Hook &&hook) {
+    uint32_t x0 = st.x0p, x4 = st.key.k[0], x8 = st.key.k[4], x12 = block;
+    x12 ^= x0; x12 = rotl(x12, 16);
+    x8 += x12; x4 ^= x8; x4 = rotl(x4, 12);
+    x0 += x4; x12 ^= x0; x12 = rotl(x12, 8);
+    x8 += x12; x4 ^= x8; x4 = rotl(x4, 7);
+    uint32_t x1 = st.c1[0], x5 = st.c1[1], x9 = st.c1[2], x13 = st.c1[3];
+    uint32_t x2 = st.c2[0], x6 = st.c2[1], x10 = st.c2[2], x14 = st.c2[3];
+    uint32_t x3 = st.c3[0], x7 = st.c3[1], x11 = st.c3[2], x15 = st.c3[3];
+    RG_QR(x0, x5, x10, x15);
+    RG_QR(x1, x6, x11, x12);
+    RG_QR(x2, x7, x8, x13);
+    RG_QR(x3, x4, x9, x14);
+    hook(0);
+#define RG_PIN_STATE()                                                                                 \
+    asm volatile("" : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3), "+v"(x4), "+v"(x5), "+v"(x6), "+v"(x7), \
+                 "+v"(x8), "+v"(x9), "+v"(x10), "+v"(x11), "+v"(x12), "+v"(x13), "+v"(x14), "+v"(x15))
+    RG_PIN_STATE();
+#pragma unroll
+    for (int i = 1; i < 10; i++) {
+        RG_QR(x0, x4, x8, x12);
+        RG_QR(x1, x5, x9, x13);
+        RG_QR(x2, x6, x10, x14);
+        RG_QR(x3, x7, x11, x15);
+        RG_QR(x0, x5, x10, x15);
+        RG_QR(x1, x6, x11, x12);
+        RG_QR(x2, x7, x8, x13);
+        RG_QR(x3, x4, x9, x14);
+        hook(i);
+        if (i % 2 == 1) RG_PIN_STATE();
+    }
+#undef RG_PIN_STATE
+    out[0] = x0 + 0x61707865u;
+    out[1] = x1 + 0x3320646eu;
+    out[2] = x2 + 0x79622d32u;
+    out[3] = x3 + 0x6b206574u;
+    out[4] = x4 + st.key.k[0];
+    out[5] = x5 + st.key.k[1];
+    out[6] = x6 + st.key.k[2];
+    out[7] = x7 + st.key.k[3];
+    out[8] = x8 + st.key.k[4];
+    out[9] = x9 + st.key.k[5];
+    out[10] = x10 + st.key.k[6];
+    out[11] = x11 + st.key.k[7];
+    out[12] = x12 + block;
+    out[13] = x13 + st.n0;
+    out[14] = x14 + st.n1;
+    out[15] = x15 + st.n2;
+}
+
 // ---------------------------------------------------------------- Poly1305
 // Accumulator h = h0 + h1 2^32 + h2 2^64 + h3 2^96 + h4 2^128, h4 small (< 8).
 struct Acc {
@@ -89,43 +219,68 @@ __device__ __forceinline__ uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) {
     return (uint64_t)a * (uint64_t)b + c;
 }
 
+__device__ __forceinline__ uint32_t addc(uint32_t a, uint32_t b, uint32_t cin, uint32_t &cout) {
+    return __builtin_addc(a, b, cin, &cout); // v_add_co_u32 / v_addc_co_u32
+}
+
 // h += m + hibit * 2^128
 __device__ __forceinline__ void acc_add(Acc &h, uint32_t m0, uint32_t m1, uint32_t m2, uint32_t m3, uint32_t hibit) {
-    uint64_t t = (uint64_t)h.h0 + m0;
-    h.h0 = (uint32_t)t;
-    t = (uint64_t)h.h1 + m1 + (t >> 32);
-    h.h1 = (uint32_t)t;
-    t = (uint64_t)h.h2 + m2 + (t >> 32);
-    h.h2 = (uint32_t)t;
-    t = (uint64_t)h.h3 + m3 + (t >> 32);
-    h.h3 = (uint32_t)t;
-    h.h4 = h.h4 + hibit + (uint32_t)(t >> 32);
+    uint32_t k;
+    h.h0 = addc(h.h0, m0, 0, k);
+    h.h1 = addc(h.h1, m1, k, k);
+    h.h2 = addc(h.h2, m2, k, k);
+    h.h3 = addc(h.h3, m3, k, k);
+    h.h4 = h.h4 + hibit + k;
 }
 
 // h = h * r mod 2^130-5, partially reduced (h4 <= 4 on exit).
 // Bounds: h_i < 2^32, h4 < 8, r_j < 2^28, rr_j < 2^28.33 -> every column sum
-// < 2^62.4 fits a u64; d4 < 2^31.6 fits a u32.
+// < 2^62.4 fits a u64.  The four columns are independent v_mad_u64_u32
+// chains; their 64-bit sums are then carried into 32-bit words with one
+// add-with-carry chain (no 64-bit shifts, no register-pair moves).
 __device__ __forceinline__ void acc_mul(Acc &h, const Mul &r) {
-    uint64_t d0 = mad64(h.h0, r.r0, mad64(h.h1, r.rr3, mad64(h.h2, r.rr2, (uint64_t)h.h3 * r.rr1)));
-    uint64_t d1 = mad64(h.h0, r.r1, mad64(h.h1, r.r0, mad64(h.h2, r.rr3, mad64(h.h3, r.rr2, (uint64_t)h.h4 * r.rr1))));
-    uint64_t d2 = mad64(h.h0, r.r2, mad64(h.h1, r.r1, mad64(h.h2, r.r0, mad64(h.h3, r.rr3, (uint64_t)h.h4 * r.rr2))));
-    uint64_t d3 = mad64(h.h0, r.r3, mad64(h.h1, r.r2, mad64(h.h2, r.r1, mad64(h.h3, r.r0, (uint64_t)h.h4 * r.rr3))));
-    uint32_t d4 = h.h4 * r.r0;
-    d1 += d0 >> 32;
-    d2 += d1 >> 32;
-    d3 += d2 >> 32;
-    d4 += (uint32_t)(d3 >> 32);
+    const uint64_t d0 = mad64(h.h3, r.rr1, mad64(h.h2, r.rr2, mad64(h.h1, r.rr3, (uint64_t)h.h0 * r.r0)));
+    const uint64_t d1 = mad64(h.h4, r.rr1, mad64(h.h3, r.rr2, mad64(h.h2, r.rr3, mad64(h.h1, r.r0, (uint64_t)h.h0 * r.r1))));
+    const uint64_t d2 = mad64(h.h4, r.rr2, mad64(h.h3, r.rr3, mad64(h.h2, r.r0, mad64(h.h1, r.r1, (uint64_t)h.h0 * r.r2))));
+    const uint64_t d3 = mad64(h.h4, r.rr3, mad64(h.h3, r.r0, mad64(h.h2, r.r1, mad64(h.h1, r.r2, (uint64_t)h.h0 * r.r3))));
+    const uint32_t d4 = h.h4 * r.r0; // < 2^31
+    uint32_t k;
+    const uint32_t w0 = (uint32_t)d0;
+    const uint32_t w1 = addc((uint32_t)d1, (uint32_t)(d0 >> 32), 0, k);
+    const uint32_t w2 = addc((uint32_t)d2, (uint32_t)(d1 >> 32), k, k);
+    const uint32_t w3 = addc((uint32_t)d3, (uint32_t)(d2 >> 32), k, k);
+    const uint32_t w4 = d4 + (uint32_t)(d3 >> 32) + k; // < 2^31.6
     // 2^130 == 5: fold bits >= 130 back in
-    uint32_t c = (d4 >> 2) + (d4 & ~3u);
-    uint64_t t = (uint64_t)(uint32_t)d0 + c;
-    h.h0 = (uint32_t)t;
-    t = (uint64_t)(uint32_t)d1 + (t >> 32);
-    h.h1 = (uint32_t)t;
-    t = (uint64_t)(uint32_t)d2 + (t >> 32);
-    h.h2 = (uint32_t)t;
-    t = (uint64_t)(uint32_t)d3 + (t >> 32);
-    h.h3 = (uint32_t)t;
-    h.h4 = (d4 & 3u) + (uint32_t)(t >> 32);
+    const uint32_t c = (w4 >> 2) + (w4 & ~3u);
+    h.h0 = addc(w0, c, 0, k);
+    h.h1 = addc(w1, 0, k, k);
+    h.h2 = addc(w2, 0, k, k);
+    h.h3 = addc(w3, 0, k, k);
+    h.h4 = (w4 & 3u) + k;
+}
+
+// h = valid ? (h + m + 2^128) * r : h, branch-free (v_cndmask) so that the
+// block can sit in the same basic block as independent keystream work.
+__device__ __forceinline__ void acc_block_pred(Acc &h, const uint4 &m, const Mul &r, bool valid) {
+    Acc t = h;
+    acc_add(t, m.x, m.y, m.z, m.w, 1);
+    acc_mul(t, r);
+    h.h0 = valid ? t.h0 : h.h0;
+    h.h1 = valid ? t.h1 : h.h1;
+    h.h2 = valid ? t.h2 : h.h2;
+    h.h3 = valid ? t.h3 : h.h3;
+    h.h4 = valid ? t.h4 : h.h4;
+}
+
+// empty asm that makes h opaque here: later Poly work cannot move above this
+// point and earlier work cannot sink below it (zero instructions)
+__device__ __forceinline__ void pin_acc(Acc &h) {
+    asm volatile("" : "+v"(h.h0), "+v"(h.h1), "+v"(h.h2), "+v"(h.h3), "+v"(h.h4));
+}
+
+__device__ __forceinline__ void acc_block(Acc &h, const uint4 &m, const Mul &r) {
+    acc_add(h, m.x, m.y, m.z, m.w, 1);
+    acc_mul(h, r);
 }
 
 // tag = (h mod p) + s mod 2^128, written as 4 little-endian words.
@@ -166,6 +321,64 @@ __device__ __forceinline__ void acc_finish(const Acc &hin, uint32_t s0, uint32_t
     tag[2] = (uint32_t)t;
     t = (uint64_t)w3 + s3 + (t >> 32);
     tag[3] = (uint32_t)t;
+}
+
+// ------------------------------------------------- general multiplier
+// Powers r^k are not clamped, so the rr = 5r/4 fold above does not apply.
+// A general multiplier G is kept in radix 2^26 (five limbs, with 5*g_j
+// precomputed, the textbook 2^130 == 5 fold); the accumulator is converted
+// 2^32 -> 2^26 -> multiply -> 2^32 around the product.
+struct Gen {
+    uint32_t g0, g1, g2, g3, g4, s1, s2, s3, s4;
+};
+
+__device__ __forceinline__ void to26(const Acc &h, uint32_t l[5]) {
+    const uint32_t M = 0x3ffffffu;
+    l[0] = h.h0 & M;
+    l[1] = ((h.h0 >> 26) | (h.h1 << 6)) & M;
+    l[2] = ((h.h1 >> 20) | (h.h2 << 12)) & M;
+    l[3] = ((h.h2 >> 14) | (h.h3 << 18)) & M;
+    l[4] = (h.h3 >> 8) | (h.h4 << 24); // h4 < 8 -> l4 < 2^27
+}
+
+__device__ __forceinline__ Gen make_gen(const Acc &g) {
+    uint32_t l[5];
+    to26(g, l);
+    Gen G;
+    G.g0 = l[0]; G.g1 = l[1]; G.g2 = l[2]; G.g3 = l[3]; G.g4 = l[4];
+    G.s1 = l[1] * 5; G.s2 = l[2] * 5; G.s3 = l[3] * 5; G.s4 = l[4] * 5;
+    return G;
+}
+
+// h = h * G mod 2^130-5, partially reduced (h4 <= 4 on exit).
+// Bounds: a_i < 2^27, g_j < 2^27, s_j < 2^29.4 -> columns < 2^59.
+__device__ __forceinline__ void acc_mul_gen(Acc &h, const Gen &G) {
+    uint32_t a[5];
+    to26(h, a);
+    uint64_t d0 = mad64(a[0], G.g0, mad64(a[1], G.s4, mad64(a[2], G.s3, mad64(a[3], G.s2, (uint64_t)a[4] * G.s1))));
+    uint64_t d1 = mad64(a[0], G.g1, mad64(a[1], G.g0, mad64(a[2], G.s4, mad64(a[3], G.s3, (uint64_t)a[4] * G.s2))));
+    uint64_t d2 = mad64(a[0], G.g2, mad64(a[1], G.g1, mad64(a[2], G.g0, mad64(a[3], G.s4, (uint64_t)a[4] * G.s3))));
+    uint64_t d3 = mad64(a[0], G.g3, mad64(a[1], G.g2, mad64(a[2], G.g1, mad64(a[3], G.g0, (uint64_t)a[4] * G.s4))));
+    uint64_t d4 = mad64(a[0], G.g4, mad64(a[1], G.g3, mad64(a[2], G.g2, mad64(a[3], G.g1, (uint64_t)a[4] * G.g0))));
+    const uint64_t M = 0x3ffffffu;
+    d1 += d0 >> 26;
+    d2 += d1 >> 26;
+    d3 += d2 >> 26;
+    d4 += d3 >> 26;
+    // fold bits >= 130: (d4 >> 26) * 5 into limb 0
+    uint64_t t0 = (d0 & M) + (d4 >> 26) * 5;
+    uint32_t l0 = (uint32_t)(t0 & M);
+    uint64_t l1 = (d1 & M) + (t0 >> 26);
+    // back to radix 2^32 (limbs may exceed 26 bits slightly; 64-bit packing absorbs it)
+    uint64_t t = (uint64_t)l0 + (l1 << 26);
+    h.h0 = (uint32_t)t;
+    t = (t >> 32) + ((d2 & M) << 20);
+    h.h1 = (uint32_t)t;
+    t = (t >> 32) + ((d3 & M) << 14);
+    h.h2 = (uint32_t)t;
+    t = (t >> 32) + ((d4 & M) << 8);
+    h.h3 = (uint32_t)t;
+    h.h4 = (uint32_t)(t >> 32); // < 4
 }
 
 __device__ __forceinline__ uint64_t mix64(uint64_t x) {

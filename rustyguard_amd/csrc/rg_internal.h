@@ -19,6 +19,7 @@ struct SealArgs {
     uint8_t *buf;
     uint64_t buf_len;
     uint8_t *status; // [n] or nullptr
+    uint64_t *dbg;   // diagnostics (stamp builds only), normally nullptr
     uint32_t nkeys;
     uint32_t n;
 };
@@ -30,6 +31,7 @@ struct OpenArgs {
     uint64_t buf_len;
     uint8_t *status;        // [n]
     uint64_t *counters_out; // [n] or nullptr
+    uint64_t *dbg;          // diagnostics (stamp builds only), normally nullptr
     uint32_t nkeys;
     uint32_t n;
 };
@@ -48,8 +50,25 @@ struct GeneralJob {
     uint32_t pad_;
 };
 
-hipError_t launch_seal(const SealArgs &a, int lanes_per_packet, hipStream_t s);
-hipError_t launch_open(const OpenArgs &a, int lanes_per_packet, hipStream_t s);
+// Launch geometry chosen by the host (rg_api.cpp): lanes per packet, CUs,
+// resident 256-thread workgroups per CU (0 = plain one-shot grid).
+struct Launch {
+    int lanes;
+    int cus;
+    int wg_per_cu;
+    int debug_mode; // diagnostics: 0 normal, 1/2 seal compute/memory only, 3 staged stamps
+    int staged_g;   // > 0: use the LDS-staged tile kernel with windows of this many chunks
+};
+constexpr uint32_t kLdsPerCu = 160u * 1024u;
+
+hipError_t launch_seal(const SealArgs &a, const Launch &L, hipStream_t s);
+hipError_t launch_open(const OpenArgs &a, const Launch &L, hipStream_t s);
+// LDS-staged tile kernel (one packet per lane, coalesced LDS-DMA windows of G chunks);
+// exactly one of sa / oa is non-null
+hipError_t launch_staged(const SealArgs *sa, const OpenArgs *oa, int G, const Launch &L, hipStream_t s);
+// sets the dynamic-LDS attribute and returns max resident workgroups per CU
+// for [seal, open][K = 1, 2, 4]
+hipError_t prepare_kernels(int max_wg[2][3]);
 hipError_t launch_general(GeneralJob *jobs, uint32_t njobs, uint8_t *arena, hipStream_t s);
 hipError_t launch_synth_fill(const rg_pkt_desc *desc, const uint32_t *inner_len, uint32_t n, uint8_t *buf,
                              uint64_t buf_len, uint64_t seed, hipStream_t s);

@@ -26,71 +26,231 @@ __device__ __forceinline__ uint4 xor4(uint4 m, const uint32_t *ks) {
     return make_uint4(m.x ^ ks[0], m.y ^ ks[1], m.z ^ ks[2], m.w ^ ks[3]);
 }
 
+// ------------------------------------------------------------ K lanes
+// K lanes cooperate on one packet (K = 1, 2, 4; groups never straddle a
+// wave).  Payload chunk c (64 B, keystream block c+1) belongs to lane
+// (c + shift) % K, where shift = roundup(C, K) - C pads the FRONT with empty
+// chunks so that lane K-1 always owns the last chunk.  Every lane computes
+// block 0 itself (r, s) -- it costs no wall time while C % K == 0.
+//
+// Poly1305 per lane in multiply-then-add form, acc = acc * r^d + m_b, where d
+// is the block distance to the lane's previous block: 1 inside a chunk and
+// 4K-3 across the K-1 chunks owned by the other lanes.  With B data blocks and
+// bl blocks in the last chunk, h_B = sum_j acc_j r^{e_j}, e_{K-1} = 1,
+// e_j = 4(K-2-j) + bl + 1; combined by a Horner pass over the lanes:
+//   S = acc_0; S = S r^4 + acc_j (j < K-1); S = S r^bl + acc_{K-1};
+//   h_B = S r;  tag = ((h_B + lenblock) r mod p) + s.
+template <int K> struct Powers {
+    Gen gap;   // r^(4K-3)
+    Gen four;  // r^4
+    Gen last;  // r^bl
+};
+
+template <int K> __device__ __forceinline__ Powers<K> make_powers(const Mul &r, uint32_t bl) {
+    Powers<K> pw;
+    if constexpr (K > 1) {
+        const Acc r1 = {r.r0, r.r1, r.r2, r.r3, 0};
+        Acc r2 = r1;
+        acc_mul(r2, r);
+        Acc r3 = r2;
+        acc_mul(r3, r);
+        Acc r4 = r2;
+        acc_mul_gen(r4, make_gen(r2));
+        pw.four = make_gen(r4);
+        Acc rg;
+        if constexpr (K == 2) {
+            rg = r4;
+            acc_mul(rg, r); // r^5
+        } else {
+            Acc r8 = r4;
+            acc_mul_gen(r8, pw.four);
+            Acc r12 = r8;
+            acc_mul_gen(r12, pw.four);
+            rg = r12;
+            acc_mul(rg, r); // r^13
+        }
+        pw.gap = make_gen(rg);
+        const Acc rb = bl == 1 ? r1 : bl == 2 ? r2 : bl == 3 ? r3 : r4;
+        pw.last = make_gen(rb);
+    }
+    return pw;
+}
+
+__device__ __forceinline__ Acc shfl_up_acc(const Acc &a, int width) {
+    Acc o;
+    o.h0 = __shfl_up(a.h0, 1, width);
+    o.h1 = __shfl_up(a.h1, 1, width);
+    o.h2 = __shfl_up(a.h2, 1, width);
+    o.h3 = __shfl_up(a.h3, 1, width);
+    o.h4 = __shfl_up(a.h4, 1, width);
+    return o;
+}
+
+// Combine the K per-lane accumulators into h_B on lane K-1 (other lanes: garbage).
+template <int K> __device__ __forceinline__ Acc combine_lanes(Acc acc, uint32_t j, const Powers<K> &pw) {
+    if constexpr (K > 1) {
+        Acc S = acc;
+#pragma unroll
+        for (uint32_t s = 1; s < K; ++s) {
+            Acc prev = shfl_up_acc(S, K);
+            acc_mul_gen(prev, s == K - 1 ? pw.last : pw.four);
+            acc_add(prev, acc.h0, acc.h1, acc.h2, acc.h3, acc.h4);
+            if (j == s) S = prev;
+        }
+        return S;
+    } else {
+        (void)j;
+        (void)pw;
+        return acc;
+    }
+}
+
+// Poly1305 step for one ciphertext block in multiply-then-add form.
+template <int K> __device__ __forceinline__ void poly_step(Acc &acc, const Mul &r, const Powers<K> &pw, bool first,
+                                                           const uint4 &ct) {
+    if constexpr (K > 1) {
+        if (first) acc_mul_gen(acc, pw.gap);
+        else acc_mul(acc, r);
+    } else {
+        (void)first;
+        (void)pw;
+        acc_mul(acc, r);
+    }
+    acc_add(acc, ct.x, ct.y, ct.z, ct.w, 1);
+}
+
+// One lane's share of a packet: keystream XOR in place + Poly1305 over the
+// ciphertext (seal: after XOR, open: before XOR).  Full 64-byte chunks run
+// branch-free (4 loads issued before the keystream block, 4 stores after);
+// the final partial chunk (bl < 4 blocks, always lane K-1's) runs after.
+// MODE (diagnostics only, selected with rg_set_debug_mode): 0 = normal;
+// 1 = compute only (payload loads/stores replaced by register data);
+// 2 = memory only (no keystream / Poly1305, loads XORed with the block index).
+template <int K, bool OPEN, int MODE = 0>
+__device__ __forceinline__ Acc lane_pass(uint4 *pl, const Stream &st, const Mul &r, const Powers<K> &pw, uint32_t nb,
+                                         uint32_t j) {
+    const uint32_t C = (nb + 3) >> 2;
+    const uint32_t T = (C + K - 1) / K; // rounds
+    const uint32_t shift = T * K - C;   // empty chunks padded at the front
+    const uint32_t bl = nb - 4 * (C - 1); // blocks in the last chunk (C > 0)
+    const bool has_partial = C > 0 && bl < 4 && j == K - 1;
+    const uint32_t t0 = j < shift ? 1 : 0;
+    const uint32_t tend = has_partial ? T - 1 : T;
+    Acc acc = {0, 0, 0, 0, 0};
+    uint32_t ks[16];
+    // Software pipeline: chunk t+1 is loaded at the top of round t, so its HBM
+    // latency hides under round t's keystream block (values live across the
+    // back-edge cannot be sunk to their use by the compiler).  The last round
+    // re-loads its own chunk instead of running off the end (no branch).
+    uint4 n0 = make_uint4(0, 0, 0, 0), n1 = n0, n2 = n0, n3 = n0;
+    if (t0 < tend && MODE != 1) {
+        const uint4 *src = pl + 4 * (t0 * K + j - shift);
+        n0 = src[0]; n1 = src[1]; n2 = src[2]; n3 = src[3];
+    }
+    for (uint32_t t = t0; t < tend; ++t) {
+        const uint32_t c = t * K + j - shift;
+        uint4 *src = pl + 4 * c;
+        const uint4 m0 = n0, m1 = n1, m2 = n2, m3 = n3;
+        if constexpr (MODE != 1) {
+            const uint4 *nxt = t + 1 < tend ? src + 4 * K : src;
+            n0 = nxt[0]; n1 = nxt[1]; n2 = nxt[2]; n3 = nxt[3];
+        } else {
+            n0.x += c; n1.y ^= c; n2.z += t; n3.w ^= t; // fake data, loop-carried
+        }
+        if constexpr (MODE == 2) {
+            const uint4 k = make_uint4(c, t, c ^ t, c + t);
+            src[0] = make_uint4(m0.x ^ k.x, m0.y ^ k.y, m0.z ^ k.z, m0.w ^ k.w);
+            src[1] = make_uint4(m1.x ^ k.x, m1.y ^ k.y, m1.z ^ k.z, m1.w ^ k.w);
+            src[2] = make_uint4(m2.x ^ k.x, m2.y ^ k.y, m2.z ^ k.z, m2.w ^ k.w);
+            src[3] = make_uint4(m3.x ^ k.x, m3.y ^ k.y, m3.z ^ k.z, m3.w ^ k.w);
+            acc.h0 ^= m0.x ^ m1.y ^ m2.z ^ m3.w;
+            continue;
+        }
+        stream_block(st, c + 1, ks);
+        const uint4 x0 = xor4(m0, ks + 0), x1 = xor4(m1, ks + 4), x2 = xor4(m2, ks + 8), x3 = xor4(m3, ks + 12);
+        if constexpr (MODE != 1) {
+            src[0] = x0;
+            src[1] = x1;
+            src[2] = x2;
+            src[3] = x3;
+        }
+        poly_step<K>(acc, r, pw, true, OPEN ? m0 : x0);
+        poly_step<K>(acc, r, pw, false, OPEN ? m1 : x1);
+        poly_step<K>(acc, r, pw, false, OPEN ? m2 : x2);
+        poly_step<K>(acc, r, pw, false, OPEN ? m3 : x3);
+    }
+    if (has_partial) {
+        const uint32_t c = C - 1;
+        uint4 *src = pl + 4 * c;
+        uint4 m[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+            if (q < (int)bl) m[q] = src[q];
+        stream_block(st, c + 1, ks);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            if (q < (int)bl) {
+                const uint4 x = xor4(m[q], ks + 4 * q);
+                src[q] = x;
+                poly_step<K>(acc, r, pw, q == 0, OPEN ? m[q] : x);
+            }
+        }
+    }
+    return acc;
+}
+
+// tag words from h_B (valid on lane K-1)
+__device__ __forceinline__ void finish_tag(Acc hB, const Mul &r, uint32_t P, uint32_t s0, uint32_t s1, uint32_t s2,
+                                           uint32_t s3, uint32_t tag[4]) {
+    acc_mul(hB, r);           // h_B = S r
+    acc_add(hB, 0, 0, P, 0, 1); // length block: le64(aad_len = 0) || le64(P)  (RFC 8439 §2.8)
+    acc_mul(hB, r);
+    acc_finish(hB, s0, s1, s2, s3, tag);
+}
+
 // ------------------------------------------------------------------ seal
 // Frame: [hdr 16][payload P][tag 16]; desc.len = P.
-__global__ __launch_bounds__(256) void seal_lane_kernel(SealArgs a) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= a.n) return;
+template <int K, int MODE> __device__ __forceinline__ void seal_packet(const SealArgs &a, uint32_t i, uint32_t j) {
     const rg_pkt_desc d = a.desc[i];
     const uint32_t P = d.len;
     const bool valid = d.key_idx < a.nkeys && (P & 15u) == 0 && (d.offset & 15u) == 0 && P <= kMaxPayload &&
                        d.offset <= a.buf_len && P + 32 <= a.buf_len - d.offset;
     if (!valid) {
-        if (a.status) a.status[i] = d.key_idx == RG_KEY_SKIP ? RG_PKT_REJECTED : RG_PKT_INVALID;
+        if (a.status && j == 0) a.status[i] = d.key_idx == RG_KEY_SKIP ? RG_PKT_REJECTED : RG_PKT_INVALID;
         return;
     }
     const Key8 key = load_key(a.keys, d.key_idx);
     const uint64_t ctr = a.counters[i];
     const uint32_t n1 = (uint32_t)ctr, n2 = (uint32_t)(ctr >> 32); // nonce = 0 || le64(ctr)
+    const Stream stm = make_stream(key, 0u, n1, n2);
     uint32_t ks[16];
-    chacha_block(key, 0, 0u, n1, n2, ks); // RFC 8439 §2.6 one-time key
+    stream_block(stm, 0, ks); // RFC 8439 §2.6 one-time key
     const Mul r = make_mul(ks[0], ks[1], ks[2], ks[3]);
     const uint32_t s0 = ks[4], s1 = ks[5], s2 = ks[6], s3 = ks[7];
-    Acc h = {0, 0, 0, 0, 0};
-
+    const uint32_t nb = P >> 4;
+    const uint32_t bl = nb == 0 ? 4 : nb - 4 * ((nb - 1) >> 2);
+    const Powers<K> pw = make_powers<K>(r, bl);
     uint8_t *frame = a.buf + d.offset;
-    uint4 *pl = reinterpret_cast<uint4 *>(frame + 16);
-    const uint32_t nb = P >> 4; // 16-byte blocks
-    for (uint32_t c = 0; 4 * c < nb; ++c) {
-        const uint32_t b0 = 4 * c;
-        const uint32_t cnt = nb - b0 < 4 ? nb - b0 : 4;
-        uint4 m[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-            if (q < (int)cnt) m[q] = pl[b0 + q];
-        chacha_block(key, c + 1, 0u, n1, n2, ks);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            if (q < (int)cnt) {
-                const uint4 ct = xor4(m[q], ks + 4 * q);
-                pl[b0 + q] = ct;
-                acc_add(h, ct.x, ct.y, ct.z, ct.w, 1);
-                acc_mul(h, r);
-            }
-        }
+    Acc acc = lane_pass<K, false, MODE>(reinterpret_cast<uint4 *>(frame + 16), stm, r, pw, nb, j);
+    Acc hB = combine_lanes<K>(acc, j, pw);
+    if (j == K - 1) {
+        uint32_t tag[4];
+        finish_tag(hB, r, P, s0, s1, s2, s3, tag);
+        if (a.receivers) // DataHeader {4, receiver, counter} (rustyguard-core/src/lib.rs:286-290)
+            *reinterpret_cast<uint4 *>(frame) = make_uint4(4u, a.receivers[d.key_idx], n1, n2);
+        *reinterpret_cast<uint4 *>(frame + 16 + P) = make_uint4(tag[0], tag[1], tag[2], tag[3]);
+        if (a.status) a.status[i] = RG_PKT_OK;
     }
-    // length block: le64(aad_len = 0) || le64(P)   (RFC 8439 §2.8)
-    acc_add(h, 0, 0, P, 0, 1);
-    acc_mul(h, r);
-    uint32_t tag[4];
-    acc_finish(h, s0, s1, s2, s3, tag);
-    if (a.receivers) {
-        // DataHeader {4, receiver, counter} (rustyguard-core/src/lib.rs:286-290)
-        *reinterpret_cast<uint4 *>(frame) = make_uint4(4u, a.receivers[d.key_idx], n1, n2);
-    }
-    *reinterpret_cast<uint4 *>(frame + 16 + P) = make_uint4(tag[0], tag[1], tag[2], tag[3]);
-    if (a.status) a.status[i] = RG_PKT_OK;
 }
 
 // ------------------------------------------------------------------ open
 // desc.len = W (frame).  Checks mirror rustyguard-core/src/lib.rs:613-629,
 // rustyguard-types/src/lib.rs:181-196 and rustyguard-crypto/src/prim.rs:427-429.
-__global__ __launch_bounds__(256) void open_lane_kernel(OpenArgs a) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= a.n) return;
+// Single pass: MAC the ciphertext and write plaintext; a failed tag re-applies
+// the keystream so the frame is left unchanged (constant-time tag compare).
+template <int K> __device__ __forceinline__ void open_packet(const OpenArgs &a, uint32_t i, uint32_t j) {
     const rg_pkt_desc d = a.desc[i];
     const uint32_t W = d.len;
-    if (a.counters_out) a.counters_out[i] = 0;
     uint8_t st;
     if (d.key_idx == RG_KEY_SKIP) st = RG_PKT_REJECTED;
     else if ((d.offset & 15u) != 0) st = RG_PKT_UNALIGNED;
@@ -98,72 +258,447 @@ __global__ __launch_bounds__(256) void open_lane_kernel(OpenArgs a) {
              W < 4)
         st = RG_PKT_INVALID;
     else st = 0xFF;
-    if (st != 0xFF) {
-        a.status[i] = st;
-        return;
-    }
     uint8_t *frame = a.buf + d.offset;
-    const uint32_t type = *reinterpret_cast<const uint32_t *>(frame);
-    if (type != 4u) {
-        a.status[i] = RG_PKT_NOT_DATA;
-        return;
+    uint64_t ctr = 0;
+    if (st == 0xFF) {
+        const uint4 hdr = *reinterpret_cast<const uint4 *>(frame);
+        if (hdr.x != 4u) st = RG_PKT_NOT_DATA;
+        else if ((W & 15u) != 0 || W < 16) st = RG_PKT_INVALID;
+        else {
+            ctr = ((uint64_t)hdr.w << 32) | hdr.z;
+            if (W < 32) st = RG_PKT_DECRYPT_ERR;
+        }
     }
-    if ((W & 15u) != 0 || W < 16) {
-        a.status[i] = RG_PKT_INVALID;
-        return;
-    }
-    const uint64_t ctr = *reinterpret_cast<const uint64_t *>(frame + 8);
-    if (a.counters_out) a.counters_out[i] = ctr;
-    if (W < 32) {
-        a.status[i] = RG_PKT_DECRYPT_ERR;
+    if (st != 0xFF) {
+        if (j == 0) {
+            a.status[i] = st;
+            if (a.counters_out) a.counters_out[i] = ctr;
+        }
         return;
     }
     const uint32_t P = W - 32;
     const Key8 key = load_key(a.keys, d.key_idx);
     const uint32_t n1 = (uint32_t)ctr, n2 = (uint32_t)(ctr >> 32);
+    const Stream stm = make_stream(key, 0u, n1, n2);
     uint32_t ks[16];
-    chacha_block(key, 0, 0u, n1, n2, ks);
+    stream_block(stm, 0, ks);
     const Mul r = make_mul(ks[0], ks[1], ks[2], ks[3]);
     const uint32_t s0 = ks[4], s1 = ks[5], s2 = ks[6], s3 = ks[7];
-    Acc h = {0, 0, 0, 0, 0};
-    uint4 *pl = reinterpret_cast<uint4 *>(frame + 16);
     const uint32_t nb = P >> 4;
-    // single pass: MAC the ciphertext and write plaintext; a failed tag
-    // re-applies the keystream below so the frame is left unchanged.
-    for (uint32_t c = 0; 4 * c < nb; ++c) {
-        const uint32_t b0 = 4 * c;
-        const uint32_t cnt = nb - b0 < 4 ? nb - b0 : 4;
-        uint4 m[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-            if (q < (int)cnt) m[q] = pl[b0 + q];
-        chacha_block(key, c + 1, 0u, n1, n2, ks);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            if (q < (int)cnt) {
-                acc_add(h, m[q].x, m[q].y, m[q].z, m[q].w, 1);
-                acc_mul(h, r);
-                pl[b0 + q] = xor4(m[q], ks + 4 * q);
-            }
-        }
+    const uint32_t bl = nb == 0 ? 4 : nb - 4 * ((nb - 1) >> 2);
+    const Powers<K> pw = make_powers<K>(r, bl);
+    uint4 *pl = reinterpret_cast<uint4 *>(frame + 16);
+    Acc acc = lane_pass<K, true>(pl, stm, r, pw, nb, j);
+    Acc hB = combine_lanes<K>(acc, j, pw);
+    uint32_t ok = 0;
+    if (j == K - 1) {
+        uint32_t tag[4];
+        finish_tag(hB, r, P, s0, s1, s2, s3, tag);
+        const uint4 want = *reinterpret_cast<const uint4 *>(frame + 16 + P);
+        const uint32_t diff = (tag[0] ^ want.x) | (tag[1] ^ want.y) | (tag[2] ^ want.z) | (tag[3] ^ want.w);
+        ok = diff == 0;
     }
-    acc_add(h, 0, 0, P, 0, 1);
-    acc_mul(h, r);
-    uint32_t tag[4];
-    acc_finish(h, s0, s1, s2, s3, tag);
-    const uint4 want = *reinterpret_cast<const uint4 *>(frame + 16 + P);
-    // constant-time compare (no early exit on the first differing word)
-    const uint32_t diff = (tag[0] ^ want.x) | (tag[1] ^ want.y) | (tag[2] ^ want.z) | (tag[3] ^ want.w);
-    if (diff != 0) {
-        for (uint32_t c = 0; 4 * c < nb; ++c) {
-            const uint32_t b0 = 4 * c;
-            const uint32_t cnt = nb - b0 < 4 ? nb - b0 : 4;
-            chacha_block(key, c + 1, 0u, n1, n2, ks);
+    if constexpr (K > 1) ok = __shfl(ok, K - 1, K);
+    if (!ok) {
+        // restore this lane's chunks: plaintext ^ keystream = ciphertext
+        const uint32_t C = (nb + 3) >> 2, Cpad = (C + K - 1) / K * K, shift = Cpad - C;
+        for (uint32_t v = j; v < Cpad; v += K) {
+            if (v < shift) continue;
+            const uint32_t c = v - shift, b0 = 4 * c, cnt = nb - b0 < 4 ? nb - b0 : 4;
+            stream_block(stm, c + 1, ks);
             for (uint32_t q = 0; q < cnt; ++q) pl[b0 + q] = xor4(pl[b0 + q], ks + 4 * q);
         }
-        a.status[i] = RG_PKT_DECRYPT_ERR;
-    } else {
-        a.status[i] = RG_PKT_OK;
+    }
+    if (j == K - 1) {
+        a.status[i] = ok ? RG_PKT_OK : RG_PKT_DECRYPT_ERR;
+        if (a.counters_out) a.counters_out[i] = ctr;
+    }
+}
+
+// ------------------------------------------------------------- kernels
+// Persistent grid: the host launches at most (CUs x workgroups-per-CU)
+// workgroups and reserves dynamic LDS so that exactly that many fit on each
+// CU -- residency, and therefore the per-SIMD wave count, is the same on every
+// CU (the dispatcher cannot stack three workgroups on one CU and one on
+// another).  Lane groups then walk the packets grid-stride; a whole group
+// (K lanes) always takes the same packet, so groups never diverge on i.
+template <int K, int MODE = 0> __global__ __launch_bounds__(256) void seal_kernel(SealArgs a) {
+    const uint32_t per_block = 256 / K;
+    const uint32_t stride = gridDim.x * per_block;
+    const uint32_t j = threadIdx.x % K;
+    for (uint32_t i = blockIdx.x * per_block + threadIdx.x / K; i < a.n; i += stride) seal_packet<K, MODE>(a, i, j);
+}
+
+template <int K> __global__ __launch_bounds__(256) void open_kernel(OpenArgs a) {
+    const uint32_t per_block = 256 / K;
+    const uint32_t stride = gridDim.x * per_block;
+    const uint32_t j = threadIdx.x % K;
+    for (uint32_t i = blockIdx.x * per_block + threadIdx.x / K; i < a.n; i += stride) open_packet<K>(a, i, j);
+}
+
+// ------------------------------------------------------ LDS-staged tiles
+// One wave owns a tile of 64 packets, one packet per lane (serial Horner with
+// the clamped r: the cheapest Poly1305 chain).  Payload moves HBM <-> LDS in
+// windows of G chunks per packet with coalesced wave-wide transfers:
+//
+//   * LDS-DMA (buffer_load_dwordx4 ... lds): instruction i reads the windows
+//     of 64/PPW packets, PPW = 4G lanes per packet each fetching one 16-byte
+//     piece, i.e. whole contiguous 64G-byte runs.  The LDS image is
+//     lane-linear, slot(p, pos) = p*PPW + pos, and the XOR swizzle goes on the
+//     SOURCE side (piece k = pos ^ f(p)) so that the per-packet ds_read_b128
+//     of one piece by 64 lanes is bank-conflict free.
+//   * compute: lane p reads its chunk's 4 pieces, XORs the keystream, writes
+//     the result back to the same slots and MACs the ciphertext;
+//   * write-back: lane l reads slot 64i+l (linear) and buffer_store's it to the
+//     same address the DMA read it from.
+//
+// Pieces past a packet's payload get an out-of-range buffer offset: the
+// descriptor's range check turns such a load into zeros and drops such a
+// store, so every wave issues exactly PPW DMA + PPW store instructions per
+// window and the vmcnt waits below are exact.  Windows are double-buffered:
+// the DMA of window w+1 overlaps the keystream work on window w.
+constexpr uint32_t kOOB = 0xFFFFFFF0u;
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ v4i make_rsrc(const uint8_t *base, uint32_t num_records) {
+    const uint64_t a = (uint64_t)base;
+    v4i r;
+    r.x = __builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+    r.y = __builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32)); // stride 0
+    r.z = __builtin_amdgcn_readfirstlane((int)num_records);
+    r.w = 0x00020000; // raw buffer, 32-bit data format (gfx9 family)
+    return r;
+}
+
+// one LDS-DMA wave-instruction: 16 bytes per lane to lds_byte + 16 * lane
+__device__ __forceinline__ void dma16(const v4i &rsrc, uint32_t voff, uint32_t lds_byte) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\t"
+                 "s_mov_b32 m0, %3\n\t"
+                 "s_nop 0\n\t"
+                 "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+                 "s_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(voff), "s"(rsrc), "s"(lds_byte)
+                 : "memory");
+}
+
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void store16(const v4i &rsrc, uint32_t voff, const uint4 &v) {
+    v4u d;
+    d.x = v.x;
+    d.y = v.y;
+    d.z = v.z;
+    d.w = v.w;
+    asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen\n\t"
+                 "s_nop 1"
+                 :
+                 : "v"(d), "v"(voff), "s"(rsrc)
+                 : "memory");
+}
+
+template <int N> __device__ __forceinline__ void wait_vm() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int G> struct StagedCfg {
+    static constexpr uint32_t PPW = 4 * G;            // 16-byte pieces per packet per window
+    static constexpr uint32_t PKT_PER_INST = 64 / PPW; // packets covered by one DMA instruction
+    static constexpr uint32_t BUF = 64 * PPW * 16;     // bytes per window buffer per wave
+    static constexpr uint32_t WAVE_LDS = 2 * BUF;      // double-buffered
+};
+
+// swizzle: makes slot(p, k ^ f(p)) distinct mod 16 over each ds_read_b128 lane group
+template <int G> __device__ __forceinline__ uint32_t swz(uint32_t p) {
+    constexpr uint32_t PPW = StagedCfg<G>::PPW;
+    return (p / (16 / PPW)) % PPW;
+}
+
+// diagnostic-build stamp (STAMP kernels only): shader-clock cycles, SGPR result
+__device__ __forceinline__ uint64_t stamp() {
+    uint64_t t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+}
+
+template <int G, bool OPEN, bool STAMP = false>
+__global__ __launch_bounds__(256) void staged_kernel(SealArgs sa, OpenArgs oa) {
+    uint64_t t_setup = 0, t_store = 0, t_issue = 0, t_wait = 0, t_chunk = 0, t_tail = 0, t_mark = 0;
+    if constexpr (STAMP) t_mark = stamp();
+    using Cfg = StagedCfg<G>;
+    constexpr uint32_t PPW = Cfg::PPW;
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds_raw[];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t n = OPEN ? oa.n : sa.n;
+    const uint32_t ntiles = (n + 63) / 64;
+    const uint32_t nwaves = gridDim.x * 4;
+    uint8_t *const buf = OPEN ? oa.buf : sa.buf;
+    const uint64_t buf_len = OPEN ? oa.buf_len : sa.buf_len;
+    const uint32_t lds_wave = (uint32_t)(uintptr_t)(lds_raw) + wave * Cfg::WAVE_LDS;
+    uint4 *const lds4 = reinterpret_cast<uint4 *>(lds_raw + wave * Cfg::WAVE_LDS);
+
+    for (uint32_t tile = blockIdx.x * 4 + wave; tile < ntiles; tile += nwaves) {
+        if constexpr (STAMP) {
+            const uint64_t t = stamp();
+            t_tail += t - t_mark;
+            t_mark = t;
+        }
+        const uint32_t i = tile * 64 + lane;
+        // ---- per-lane packet setup (one packet per lane)
+        bool live = i < n;
+        rg_pkt_desc d = {0, 0, 0};
+        if (live) d = OPEN ? oa.desc[i] : sa.desc[i];
+        uint8_t st = 0xFF;
+        uint32_t P = 0;
+        uint64_t ctr = 0;
+        if (live) {
+            if constexpr (!OPEN) {
+                P = d.len;
+                const bool ok = d.key_idx < sa.nkeys && (P & 15u) == 0 && (d.offset & 15u) == 0 &&
+                                P <= kMaxPayload && d.offset <= buf_len && P + 32 <= buf_len - d.offset;
+                if (!ok) st = d.key_idx == RG_KEY_SKIP ? RG_PKT_REJECTED : RG_PKT_INVALID;
+                else ctr = sa.counters[i];
+            } else {
+                const uint32_t W = d.len;
+                if (d.key_idx == RG_KEY_SKIP) st = RG_PKT_REJECTED;
+                else if ((d.offset & 15u) != 0) st = RG_PKT_UNALIGNED;
+                else if (d.key_idx >= oa.nkeys || W > kMaxPayload + 32 || d.offset > buf_len ||
+                         W > buf_len - d.offset || W < 4)
+                    st = RG_PKT_INVALID;
+                if (st == 0xFF) {
+                    const uint4 hdr = *reinterpret_cast<const uint4 *>(buf + d.offset);
+                    if (hdr.x != 4u) st = RG_PKT_NOT_DATA;
+                    else if ((W & 15u) != 0 || W < 16) st = RG_PKT_INVALID;
+                    else {
+                        ctr = ((uint64_t)hdr.w << 32) | hdr.z;
+                        if (W < 32) st = RG_PKT_DECRYPT_ERR;
+                    }
+                }
+                if (st == 0xFF) P = W - 32;
+            }
+        }
+        const bool work = live && st == 0xFF;
+        const uint32_t nb = work ? P >> 4 : 0; // 16-byte blocks of this lane's packet
+        const uint32_t C = (nb + 3) >> 2;      // 64-byte chunks
+        // ---- tile addressing: buffer descriptor based at the lowest frame of the tile
+        uint64_t lo = work ? d.offset : ~0ull;
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) {
+            const uint64_t o = __shfl_xor(lo, m);
+            lo = o < lo ? o : lo;
+        }
+        lo = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(lo >> 32)) << 32) |
+             __builtin_amdgcn_readfirstlane((uint32_t)lo);
+        if (lo == ~0ull) lo = 0;
+        const uint64_t span_cap = buf_len - lo;
+        const uint32_t nrec = span_cap > kOOB ? kOOB : (uint32_t)span_cap;
+        const v4i rsrc = make_rsrc(buf + lo, nrec);
+        // payload base of this lane's packet relative to the descriptor (kOOB if unusable)
+        uint32_t my_base = kOOB;
+        if (work && d.offset - lo + 16 + (uint64_t)P <= nrec) my_base = (uint32_t)(d.offset - lo) + 16;
+        const uint32_t myC = my_base == kOOB ? 0 : C;
+        // windows for the whole wave (uniform)
+        uint32_t Wl = (myC + G - 1) / G;
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) {
+            const uint32_t o = __shfl_xor(Wl, m);
+            Wl = o > Wl ? o : Wl;
+        }
+        const uint32_t W = __builtin_amdgcn_readfirstlane(Wl);
+        // DMA/store address table: instruction q serves packet pq = q*PKT_PER_INST + lane/PPW,
+        // piece k = (lane % PPW) ^ swz(pq)
+        uint32_t tb[PPW], tlim[PPW];
+#pragma unroll
+        for (uint32_t q = 0; q < PPW; ++q) {
+            const uint32_t pq = q * Cfg::PKT_PER_INST + lane / PPW;
+            const uint32_t k = (lane % PPW) ^ swz<G>(pq);
+            const uint32_t b = __shfl(my_base, pq);
+            const uint32_t blocks = __shfl(myC == 0 ? 0u : nb, pq);
+            tb[q] = b == kOOB ? kOOB : b + 16 * k;
+            tlim[q] = blocks > k ? blocks - k : 0; // piece valid in window w iff w*PPW < tlim
+        }
+        // ---- keys, one-time key
+        const uint32_t n1 = (uint32_t)ctr, n2 = (uint32_t)(ctr >> 32);
+        const Key8 key = load_key(OPEN ? oa.keys : sa.keys, work ? d.key_idx : 0u);
+        const Stream stm = make_stream(key, 0u, n1, n2);
+        uint32_t ks[16];
+        stream_block(stm, 0, ks);
+        const Mul r = make_mul(ks[0], ks[1], ks[2], ks[3]);
+        const uint32_t s0 = ks[4], s1 = ks[5], s2 = ks[6], s3 = ks[7];
+        Acc acc = {0, 0, 0, 0, 0};
+
+        // ---- chunk loop, software-pipelined: the keystream block of chunk c+1
+        // is generated in the same basic block as the Poly1305 of chunk c, so
+        // the two independent dependency chains interleave.
+        auto voff_of = [&](uint32_t q, uint32_t w) -> uint32_t {
+            return (tb[q] != kOOB && w * PPW < tlim[q]) ? tb[q] + w * PPW * 16 : kOOB;
+        };
+        auto issue_dma = [&](uint32_t w) {
+            const uint32_t lbase = lds_wave + (w & 1) * Cfg::BUF;
+#pragma unroll
+            for (uint32_t q = 0; q < PPW; ++q) dma16(rsrc, voff_of(q, w), __builtin_amdgcn_readfirstlane(lbase + q * 1024));
+        };
+        auto store_window = [&](uint32_t w) {
+            const uint4 *win = lds4 + (w & 1) * (Cfg::BUF / 16);
+            // all LDS reads first (one lgkmcnt wait), then the coalesced stores
+            uint4 v[PPW];
+#pragma unroll
+            for (uint32_t q = 0; q < PPW; ++q) v[q] = win[q * 64 + lane];
+#pragma unroll
+            for (uint32_t q = 0; q < PPW; ++q) store16(rsrc, voff_of(q, w), v[q]);
+        };
+        if constexpr (STAMP) {
+            const uint64_t t = stamp();
+            t_setup += t - t_mark;
+            t_mark = t;
+        }
+        const uint32_t Cmax = W * G; // wave-uniform chunk count (multiple of G)
+        const uint32_t f = swz<G>(lane);
+        uint32_t ksc[16];
+        stream_block(stm, 1, ksc);
+        for (uint32_t c = 0; c < Cmax; ++c) {
+            const uint32_t w = c / G, cl = c % G;
+            if (cl == 0) { // window boundary (wave-uniform)
+                if constexpr (STAMP) {
+                    const uint64_t t = stamp();
+                    t_chunk += t - t_mark;
+                    t_mark = t;
+                }
+                if (w > 0) store_window(w - 1);
+                if constexpr (STAMP) {
+                    const uint64_t t = stamp();
+                    t_store += t - t_mark;
+                    t_mark = t;
+                }
+                const bool more = w + 1 < W;
+                if (w == 0) {
+                    issue_dma(0);
+                    if (more) issue_dma(1);
+                } else if (more) {
+                    issue_dma(w + 1);
+                }
+                if constexpr (STAMP) {
+                    const uint64_t t = stamp();
+                    t_issue += t - t_mark;
+                    t_mark = t;
+                }
+                if (w == 0) {
+                    if (more) wait_vm<PPW>();
+                    else wait_vm<0>();
+                } else {
+                    // wait for DMA(w); younger: stores(w-1) and DMA(w+1)
+                    if (more) wait_vm<2 * PPW>();
+                    else wait_vm<PPW>();
+                }
+                if constexpr (STAMP) {
+                    const uint64_t t = stamp();
+                    t_wait += t - t_mark;
+                    t_mark = t;
+                }
+            }
+            uint4 *win = lds4 + (w & 1) * (Cfg::BUF / 16);
+            // blocks of this chunk that belong to the lane's payload (0..4)
+            const uint32_t cnt = c < myC ? (nb - 4 * c < 4 ? nb - 4 * c : 4) : 0;
+            const uint32_t sl0 = lane * PPW + ((4 * cl + 0) ^ f);
+            const uint32_t sl1 = lane * PPW + ((4 * cl + 1) ^ f);
+            const uint32_t sl2 = lane * PPW + ((4 * cl + 2) ^ f);
+            const uint32_t sl3 = lane * PPW + ((4 * cl + 3) ^ f);
+            const uint4 m0 = win[sl0], m1 = win[sl1], m2 = win[sl2], m3 = win[sl3];
+            // The LDS reads land while the first ChaCha rounds of the next block
+            // run: XOR + write-back sit in the hook after double round 0, the
+            // four Poly1305 blocks after double rounds 1, 3, 5 and 7.
+            uint4 x0, x1, x2, x3;
+            uint32_t ksn[16];
+            stream_block_hooked(stm, c + 2, ksn, [&](int dr) {
+                if (dr == 0) {
+                    x0 = xor4(m0, ksc + 0);
+                    x1 = xor4(m1, ksc + 4);
+                    x2 = xor4(m2, ksc + 8);
+                    x3 = xor4(m3, ksc + 12);
+                    // unconditional: pieces outside the payload are never stored
+                    // (their buffer offsets are out of range)
+                    win[sl0] = x0;
+                    win[sl1] = x1;
+                    win[sl2] = x2;
+                    win[sl3] = x3;
+                }
+                if (dr == 1) acc_block_pred(acc, OPEN ? m0 : x0, r, cnt > 0);
+                if (dr == 3) acc_block_pred(acc, OPEN ? m1 : x1, r, cnt > 1);
+                if (dr == 5) acc_block_pred(acc, OPEN ? m2 : x2, r, cnt > 2);
+                if (dr == 7) acc_block_pred(acc, OPEN ? m3 : x3, r, cnt > 3);
+                if (dr % 2 == 1) pin_acc(acc);
+            });
+#pragma unroll
+            for (int t = 0; t < 16; ++t) ksc[t] = ksn[t];
+        }
+        if constexpr (STAMP) {
+            const uint64_t t = stamp();
+            t_chunk += t - t_mark;
+            t_mark = t;
+        }
+        if (W > 0) store_window(W - 1);
+        wait_vm<0>(); // drain this tile's stores before the per-packet tail touches the frames
+        if (!live) continue;
+        uint8_t *frame = buf + d.offset;
+        if (st != 0xFF) {
+            if constexpr (!OPEN) {
+                if (sa.status) sa.status[i] = st;
+            } else {
+                oa.status[i] = st;
+                if (oa.counters_out) oa.counters_out[i] = ctr;
+            }
+            continue;
+        }
+        if (my_base == kOOB) { // tile span too large for a 32-bit buffer offset (not produced by rg_* callers)
+            if constexpr (!OPEN) {
+                if (sa.status) sa.status[i] = RG_PKT_INVALID;
+            } else {
+                oa.status[i] = RG_PKT_INVALID;
+            }
+            continue;
+        }
+        // h = acc * r  (multiply-then-add form closes with one more r), length block, finish
+        acc_add(acc, 0, 0, P, 0, 1);
+        acc_mul(acc, r);
+        uint32_t tag[4];
+        acc_finish(acc, s0, s1, s2, s3, tag);
+        if constexpr (!OPEN) {
+            if (sa.receivers) *reinterpret_cast<uint4 *>(frame) = make_uint4(4u, sa.receivers[d.key_idx], n1, n2);
+            *reinterpret_cast<uint4 *>(frame + 16 + P) = make_uint4(tag[0], tag[1], tag[2], tag[3]);
+            if (sa.status) sa.status[i] = RG_PKT_OK;
+        } else {
+            const uint4 want = *reinterpret_cast<const uint4 *>(frame + 16 + P);
+            const uint32_t diff = (tag[0] ^ want.x) | (tag[1] ^ want.y) | (tag[2] ^ want.z) | (tag[3] ^ want.w);
+            if (diff != 0) {
+                // forged/corrupt: re-apply the keystream so the frame is left unchanged
+                uint4 *pl = reinterpret_cast<uint4 *>(frame + 16);
+                for (uint32_t c = 0; 4 * c < nb; ++c) {
+                    const uint32_t cnt = nb - 4 * c < 4 ? nb - 4 * c : 4;
+                    stream_block(stm, c + 1, ks);
+                    for (uint32_t q = 0; q < cnt; ++q) pl[4 * c + q] = xor4(pl[4 * c + q], ks + 4 * q);
+                }
+            }
+            oa.status[i] = diff == 0 ? RG_PKT_OK : RG_PKT_DECRYPT_ERR;
+            if (oa.counters_out) oa.counters_out[i] = ctr;
+        }
+    }
+    if constexpr (STAMP) {
+        const uint64_t t = stamp();
+        t_tail += t - t_mark;
+        uint64_t *dbg = OPEN ? oa.dbg : sa.dbg;
+        if (dbg && lane == 0) {
+            uint64_t *o = dbg + 8 * (blockIdx.x * 4 + wave);
+            o[0] = t_setup;
+            o[1] = t_store;
+            o[2] = t_issue;
+            o[3] = t_wait;
+            o[4] = t_chunk;
+            o[5] = t_tail;
+            o[6] = 1;
+        }
     }
 }
 
@@ -250,20 +785,98 @@ __global__ __launch_bounds__(256) void synth_fill_kernel(const rg_pkt_desc *desc
 }
 
 // ---------------------------------------------------------------- launch
-hipError_t launch_seal(const SealArgs &a, int lanes_per_packet, hipStream_t s) {
-    (void)lanes_per_packet;
+static void grid_for(uint32_t n, int K, const Launch &L, uint32_t &blocks, uint32_t &lds) {
+    const uint64_t want = ((uint64_t)n * K + 255) / 256;
+    const uint64_t cap = (uint64_t)L.cus * (uint64_t)L.wg_per_cu;
+    blocks = (uint32_t)(want < cap || cap == 0 ? want : cap);
+    // reserve LDS so that exactly wg_per_cu workgroups are resident per CU
+    lds = L.wg_per_cu > 0 ? (kLdsPerCu / L.wg_per_cu) & ~255u : 0;
+}
+
+template <typename A, void (*F1)(A), void (*F2)(A), void (*F4)(A)>
+static hipError_t launch_k(const A &a, const Launch &L, hipStream_t s) {
     if (a.n == 0) return hipSuccess;
-    const uint32_t blocks = (a.n + 255) / 256;
-    hipLaunchKernelGGL(seal_lane_kernel, dim3(blocks), dim3(256), 0, s, a);
+    uint32_t blocks, lds;
+    grid_for(a.n, L.lanes, L, blocks, lds);
+    switch (L.lanes) {
+    case 1: hipLaunchKernelGGL(F1, dim3(blocks), dim3(256), lds, s, a); break;
+    case 2: hipLaunchKernelGGL(F2, dim3(blocks), dim3(256), lds, s, a); break;
+    case 4: hipLaunchKernelGGL(F4, dim3(blocks), dim3(256), lds, s, a); break;
+    default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 
-hipError_t launch_open(const OpenArgs &a, int lanes_per_packet, hipStream_t s) {
-    (void)lanes_per_packet;
-    if (a.n == 0) return hipSuccess;
-    const uint32_t blocks = (a.n + 255) / 256;
-    hipLaunchKernelGGL(open_lane_kernel, dim3(blocks), dim3(256), 0, s, a);
+hipError_t launch_seal(const SealArgs &a, const Launch &L, hipStream_t s) {
+    if (L.debug_mode == 1) return launch_k<SealArgs, seal_kernel<1, 1>, seal_kernel<2, 1>, seal_kernel<4, 1>>(a, L, s);
+    if (L.debug_mode == 2) return launch_k<SealArgs, seal_kernel<1, 2>, seal_kernel<2, 2>, seal_kernel<4, 2>>(a, L, s);
+    return launch_k<SealArgs, seal_kernel<1>, seal_kernel<2>, seal_kernel<4>>(a, L, s);
+}
+
+hipError_t launch_open(const OpenArgs &a, const Launch &L, hipStream_t s) {
+    return launch_k<OpenArgs, open_kernel<1>, open_kernel<2>, open_kernel<4>>(a, L, s);
+}
+
+template <int G> static uint32_t staged_lds_per_wg() { return 4 * StagedCfg<G>::WAVE_LDS; }
+
+hipError_t launch_staged(const SealArgs *sa, const OpenArgs *oa, int G, const Launch &L, hipStream_t s) {
+    const uint32_t n = sa ? sa->n : oa->n;
+    if (n == 0) return hipSuccess;
+    SealArgs a = sa ? *sa : SealArgs{};
+    OpenArgs b = oa ? *oa : OpenArgs{};
+    const uint64_t tiles = (n + 63) / 64;
+    const uint64_t want = (tiles + 3) / 4;
+    const int wpc = L.wg_per_cu > 0 ? L.wg_per_cu : 1;
+    const uint64_t cap = (uint64_t)L.cus * wpc;
+    const uint32_t blocks = (uint32_t)(want < cap || cap == 0 ? want : cap);
+    uint32_t need = G == 1 ? staged_lds_per_wg<1>() : G == 2 ? staged_lds_per_wg<2>() : staged_lds_per_wg<4>();
+    uint32_t lds = (kLdsPerCu / wpc) & ~255u;
+    if (lds < need) lds = need;
+    if (lds > kLdsPerCu) return hipErrorInvalidValue;
+#define RG_STAGED(GG)                                                                                  \
+    if (L.debug_mode == 3) {                                                                           \
+        if (sa) hipLaunchKernelGGL((staged_kernel<GG, false, true>), dim3(blocks), dim3(256), lds, s, a, b); \
+        else hipLaunchKernelGGL((staged_kernel<GG, true, true>), dim3(blocks), dim3(256), lds, s, a, b);     \
+    } else if (sa) hipLaunchKernelGGL((staged_kernel<GG, false>), dim3(blocks), dim3(256), lds, s, a, b); \
+    else hipLaunchKernelGGL((staged_kernel<GG, true>), dim3(blocks), dim3(256), lds, s, a, b);
+    switch (G) {
+    case 1: RG_STAGED(1) break;
+    case 2: RG_STAGED(2) break;
+    case 4: RG_STAGED(4) break;
+    default: return hipErrorInvalidValue;
+    }
+#undef RG_STAGED
     return hipGetLastError();
+}
+
+hipError_t prepare_kernels(int lanes_max_wg[2][3]) {
+    {
+        void *fs[12] = {(void *)staged_kernel<1, false>, (void *)staged_kernel<2, false>, (void *)staged_kernel<4, false>,
+                        (void *)staged_kernel<1, true>,  (void *)staged_kernel<2, true>,  (void *)staged_kernel<4, true>,
+                        (void *)staged_kernel<1, false, true>, (void *)staged_kernel<2, false, true>,
+                        (void *)staged_kernel<4, false, true>, (void *)staged_kernel<1, true, true>,
+                        (void *)staged_kernel<2, true, true>,  (void *)staged_kernel<4, true, true>};
+        for (void *f : fs) {
+            hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsPerCu);
+            if (e != hipSuccess) return e;
+        }
+    }
+    // allow up to the whole 160 KiB LDS as dynamic shared memory, and report
+    // how many 256-thread workgroups of each kernel fit on a CU (VGPR bound)
+    void *seal[3] = {(void *)seal_kernel<1>, (void *)seal_kernel<2>, (void *)seal_kernel<4>};
+    void *open[3] = {(void *)open_kernel<1>, (void *)open_kernel<2>, (void *)open_kernel<4>};
+    for (int k = 0; k < 3; ++k) {
+        for (int w = 0; w < 2; ++w) {
+            const void *f = w == 0 ? seal[k] : open[k];
+            hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsPerCu);
+            if (e != hipSuccess) return e;
+            int nb = 0;
+            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, 256, 0);
+            if (e != hipSuccess) return e;
+            lanes_max_wg[w][k] = nb;
+        }
+    }
+    return hipSuccess;
 }
 
 hipError_t launch_general(GeneralJob *jobs, uint32_t njobs, uint8_t *arena, hipStream_t s) {

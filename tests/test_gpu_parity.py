@@ -67,8 +67,28 @@ def _gpu_open(engine, keys, desc_open, buf):
     return b.cpu().numpy(), st.cpu().numpy(), co.cpu().numpy().view(np.uint64)
 
 
-def _lanes(engine):
-    return [1, 2, 4]
+# kernel configurations every parity test runs under: lane-pass kernels with
+# K lanes per packet, and the LDS-staged tile kernel with G-chunk windows
+MODES = [("lane", 1), ("lane", 2), ("lane", 4), ("staged", 1), ("staged", 2), ("staged", 4)]
+
+
+def _configure(engine, mode):
+    kind, v = mode
+    if kind == "lane":
+        engine.set_staged(0)
+        engine.set_lanes_per_packet(v)
+    else:
+        engine.set_lanes_per_packet(0)
+        engine.set_staged(v)
+
+
+def _reset(engine):
+    engine.set_staged(0)
+    engine.set_lanes_per_packet(0)
+
+
+def _mode_id(m):
+    return f"{m[0]}{m[1]}"
 
 
 # ------------------------------------------------------------ reference pins
@@ -84,10 +104,10 @@ def test_reference_snapshots_per_message(engine):
         assert buf.hex() == v["plaintext"]
 
 
-@pytest.mark.parametrize("lanes", [1, 2, 4])
-def test_reference_framed_packet_batch(engine, lanes):
+@pytest.mark.parametrize("mode", MODES, ids=_mode_id)
+def test_reference_framed_packet_batch(engine, mode):
     """rustyguard-core snapshot-3: the full 48-byte framed data packet."""
-    engine.set_lanes_per_packet(lanes)
+    _configure(engine, mode)
     v = load_golden("reference_snapshots.json")["framed_packets"][0]
     keys = np.frombuffer(bytes.fromhex(v["key"]), np.uint8).reshape(1, 32)
     pt = np.frombuffer(bytes.fromhex(v["plaintext"]), np.uint8)
@@ -109,7 +129,7 @@ def test_reference_framed_packet_batch(engine, lanes):
     back, st, _ = _gpu_open(engine, keys, od, forged)
     assert st[0] == aead.PKT_DECRYPT_ERR
     assert np.array_equal(back, forged)  # untouched on failure
-    engine.set_lanes_per_packet(0)
+    _reset(engine)
 
 
 def test_per_message_openssl_vectors(engine):
@@ -132,10 +152,10 @@ def test_per_message_openssl_vectors(engine):
             assert ct.hex() == v["ciphertext"]
 
 
-@pytest.mark.parametrize("lanes", [1, 2, 4])
-def test_batch_openssl_transport_vectors(engine, lanes):
+@pytest.mark.parametrize("mode", MODES, ids=_mode_id)
+def test_batch_openssl_transport_vectors(engine, mode):
     """Every 16-aligned OpenSSL transport vector, sealed in one batch."""
-    engine.set_lanes_per_packet(lanes)
+    _configure(engine, mode)
     vs = [v for v in load_golden("openssl_vectors.json")["wg_transport"] if (len(v["plaintext"]) // 2) % 16 == 0]
     n = len(vs)
     P = np.array([len(v["plaintext"]) // 2 for v in vs])
@@ -154,14 +174,14 @@ def test_batch_openssl_transport_vectors(engine, lanes):
         o, p = int(d["offset"]), int(d["len"])
         assert out[o + 16: o + 16 + p].tobytes().hex() == v["ciphertext"]
         assert out[o + 16 + p: o + 32 + p].tobytes().hex() == v["tag"]
-    engine.set_lanes_per_packet(0)
+    _reset(engine)
 
 
 # ------------------------------------------------------- oracle differential
-@pytest.mark.parametrize("lanes", [1, 2, 4])
+@pytest.mark.parametrize("mode", MODES, ids=_mode_id)
 @pytest.mark.parametrize("seed", [1, 2])
-def test_random_batches_vs_oracle(engine, lanes, seed):
-    engine.set_lanes_per_packet(lanes)
+def test_random_batches_vs_oracle(engine, mode, seed):
+    _configure(engine, mode)
     rng = np.random.default_rng(seed)
     n = 3000
     keys, rec, desc, ctr, buf = _random_batch(rng, n, nkeys=5)
@@ -180,12 +200,12 @@ def test_random_batches_vs_oracle(engine, lanes, seed):
     for d in desc[:200]:
         o, p = int(d["offset"]), int(d["len"])
         assert np.array_equal(back[o + 16: o + 16 + p], buf[o + 16: o + 16 + p])
-    engine.set_lanes_per_packet(0)
+    _reset(engine)
 
 
-@pytest.mark.parametrize("lanes", [1, 2, 4])
-def test_open_failures_leave_frames_untouched(engine, lanes):
-    engine.set_lanes_per_packet(lanes)
+@pytest.mark.parametrize("mode", MODES, ids=_mode_id)
+def test_open_failures_leave_frames_untouched(engine, mode):
+    _configure(engine, mode)
     rng = np.random.default_rng(9)
     n = 512
     keys, rec, desc, ctr, buf = _random_batch(rng, n, nkeys=2, sizes=rng.integers(1, 96, n) * 16)
@@ -208,10 +228,12 @@ def test_open_failures_leave_frames_untouched(engine, lanes):
         assert np.array_equal(back[o:o + w], tampered[o:o + w])
     good = np.setdiff1d(np.arange(n), bad)
     assert (st[good] == aead.PKT_OK).all()
-    engine.set_lanes_per_packet(0)
+    _reset(engine)
 
 
-def test_open_malformed_statuses_match_oracle(engine):
+@pytest.mark.parametrize("mode", MODES, ids=_mode_id)
+def test_open_malformed_statuses_match_oracle(engine, mode):
+    _configure(engine, mode)
     rng = np.random.default_rng(5)
     keys = rng.integers(0, 256, (2, 32), dtype=np.uint8)
     buf = np.zeros(4096, np.uint8)
@@ -237,9 +259,12 @@ def test_open_malformed_statuses_match_oracle(engine):
     assert list(st[:7]) == list(want)
     assert st[7] == aead.PKT_REJECTED and st[8] == aead.PKT_INVALID
     assert list(st) == [1, 2, 2, 1, 5, 4, 1, 3, 2]
+    _reset(engine)
 
 
-def test_seal_rejects_bad_descriptors(engine):
+@pytest.mark.parametrize("mode", MODES, ids=_mode_id)
+def test_seal_rejects_bad_descriptors(engine, mode):
+    _configure(engine, mode)
     keys = np.zeros((1, 32), np.uint8)
     desc = np.zeros(4, DESC_DTYPE)
     desc[0] = (0, 17, 0)      # P % 16 != 0
@@ -250,10 +275,13 @@ def test_seal_rejects_bad_descriptors(engine):
     out, st = _gpu_seal(engine, keys, None, desc, np.zeros(4, np.uint64), buf)
     assert list(st) == [aead.PKT_INVALID] * 4
     assert np.array_equal(out, buf)
+    _reset(engine)
 
 
-def test_empty_payload_keepalive(engine):
+@pytest.mark.parametrize("mode", MODES, ids=_mode_id)
+def test_empty_payload_keepalive(engine, mode):
     """Keepalive seals an empty payload (rustyguard-core/src/time.rs:131): 32-byte frame."""
+    _configure(engine, mode)
     keys = np.frombuffer(bytes(range(32)), np.uint8).reshape(1, 32)
     desc = np.zeros(1, DESC_DTYPE)
     buf = np.zeros(32, np.uint8)
@@ -261,6 +289,7 @@ def test_empty_payload_keepalive(engine):
     want = buf.copy()
     oracle.seal_batch(keys, np.array([7], np.uint32), desc, np.array([5], np.uint64), want)
     assert np.array_equal(out, want)
+    _reset(engine)
 
 
 def test_host_path_matches_oracle(engine):
@@ -291,13 +320,13 @@ def test_full_config_digest(engine, name):
     b.fill()
     torch.cuda.synchronize()
     assert hashlib.sha256(b.host_buf().tobytes()).hexdigest() == dig["plain_sha256"]
-    for lanes in _lanes(engine):
-        engine.set_lanes_per_packet(lanes)
+    for mode in MODES:
+        _configure(engine, mode)
         b.fill()
         b.seal()
         torch.cuda.synchronize()
         assert (b.status[: w.n] == 0).all().item()
-        assert hashlib.sha256(b.host_buf().tobytes()).hexdigest() == dig["sealed_sha256"], lanes
+        assert hashlib.sha256(b.host_buf().tobytes()).hexdigest() == dig["sealed_sha256"], mode
         b.open()
         torch.cuda.synchronize()
         assert (b.status[: w.n] == 0).all().item()
@@ -310,4 +339,4 @@ def test_full_config_digest(engine, name):
         for d in w.desc[:: max(1, w.n // 500)]:
             o, p = int(d["offset"]), int(d["len"])
             assert np.array_equal(hb[o + 16:o + 16 + p], plain[o + 16:o + 16 + p])
-    engine.set_lanes_per_packet(0)
+    _reset(engine)

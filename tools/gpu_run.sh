@@ -39,6 +39,58 @@ for s in "$@"; do
     prof)
         run prof 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- \
             python3 bench.py --steps 30 --warmup 5 --cpu-seconds 0 ;;
+    pmc_list) run pmc_list 120 rocprofv3 -L ;;
+    pmc)
+        # separate passes (TCC FETCH_SIZE and WRITE_SIZE do not fit one pass; never combined with tracing domains)
+        W=${RG_PMC_WORKLOAD:-cfg2}
+        run pmc_sq 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE \
+            --kernel-trace --output-format csv -d gpurun_out/pmc_sq -o p -- python3 bench.py --workload $W --steps 5 --warmup 2 --cpu-seconds 0
+        run pmc_wait 300 rocprofv3 --pmc SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_SCA SQ_INSTS_LDS SQ_WAVES \
+            --kernel-trace --output-format csv -d gpurun_out/pmc_wait -o p -- python3 bench.py --workload $W --steps 5 --warmup 2 --cpu-seconds 0
+        run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch -o p -- \
+            python3 bench.py --workload $W --steps 5 --warmup 2 --cpu-seconds 0
+        run pmc_write 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write -o p -- \
+            python3 bench.py --workload $W --steps 5 --warmup 2 --cpu-seconds 0 ;;
+    pmc2)
+        W=${RG_PMC_WORKLOAD:-cfg2}
+        run pmc_a 300 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INST_LEVEL_VMEM SQ_BUSY_CYCLES \
+            --kernel-trace --output-format csv -d gpurun_out/pmc_a -o p -- python3 bench.py --workload $W --steps 5 --warmup 2 --cpu-seconds 0
+        run pmc_b 300 rocprofv3 --pmc TA_BUSY_avr TA_ADDR_STALLED_BY_TC_CYCLES_sum TA_DATA_STALLED_BY_TC_CYCLES_sum TA_TA_BUSY_sum GRBM_GUI_ACTIVE SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INST_CYCLES_VMEM_RD \
+            --kernel-trace --output-format csv -d gpurun_out/pmc_b -o p -- python3 bench.py --workload $W --steps 5 --warmup 2 --cpu-seconds 0
+        run pmc_c 300 rocprofv3 --pmc TCP_PENDING_STALL_CYCLES_sum TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum \
+            --kernel-trace --output-format csv -d gpurun_out/pmc_c -o p -- python3 bench.py --workload $W --steps 5 --warmup 2 --cpu-seconds 0 ;;
+    sweep)
+        W=${RG_WORKLOAD:-cfg2}
+        for l in 1 2 4; do for g in -1 0 2 3 4; do
+            run sweep_${W}_l${l}_g${g} 200 python bench.py --workload $W --lanes $l --wg-per-cu $g --steps 20 --warmup 3 --cpu-seconds 0
+        done; done
+        grep -h '"value"' gpurun_out/sweep_${W}_*.log | python3 -c "import sys,json
+for l in sys.stdin:
+    d=json.loads(l); c=d['config']; print(c['lanes_per_packet'], c['wg_per_cu'], d['value'], d['seal_ms'], d['open_ms'], d['gpu_ms_per_step'])" ;;
+    diag)
+        W=${RG_WORKLOAD:-cfg2}
+        for m in 0 1 2; do for l in 1 2; do
+            run diag_${W}_m${m}_l${l} 200 python bench.py --workload $W --lanes $l --debug-mode $m --steps 20 --warmup 3 --cpu-seconds 0
+        done; done
+        grep -H '"value"' gpurun_out/diag_${W}_*.log | python3 -c "import sys,json
+for l in sys.stdin:
+    f,j=l.split(':',1); d=json.loads(j); print(f.split('/')[-1], d['seal_ms'])" ;;
+    staged)
+        W=${RG_WORKLOAD:-cfg2}
+        for g in 0 1 2 4; do for c in 1 2; do
+            run st_${W}_g${g}_c${c} 200 python bench.py --workload $W --staged $g --wg-per-cu $c --steps 20 --warmup 3 --cpu-seconds 0
+        done; done
+        grep -H '"value"' gpurun_out/st_${W}_*.log | python3 -c "import sys,json
+for l in sys.stdin:
+    f,j=l.split(':',1); d=json.loads(j); print(f.split('/')[-1], d['value'], d['seal_ms'], d['open_ms'])" ;;
+    pmc_clock)
+        W=${RG_WORKLOAD:-cfg2}
+        for v in "l1:--lanes 1 --staged 0" "l1m1:--lanes 1 --staged 0 --debug-mode 1" "l1m2:--lanes 1 --staged 0 --debug-mode 2" "l2:--lanes 2 --staged 0" "g2:--staged 2"; do
+            name=${v%%:*}; flags=${v#*:}
+            run pmcclk_$name 240 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_WAVES SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY \
+                --kernel-trace --output-format csv -d gpurun_out/pmcclk_$name -o p -- python3 bench.py --workload $W $flags --steps 5 --warmup 2 --cpu-seconds 0 --no-graph
+        done ;;
+    stamps) run stamps 300 python tools/stamps.py --workload ${RG_WORKLOAD:-cfg2} --staged ${RG_G:-2} ;;
     *) echo "unknown step $s"; exit 2 ;;
     esac
 done

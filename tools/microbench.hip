@@ -7,6 +7,8 @@
 #include <cstdio>
 #include <cstdlib>
 
+#include "../rustyguard_amd/csrc/rg_device.h"
+
 #define CHECK(x)                                                              \
     do {                                                                      \
         hipError_t e = (x);                                                   \
@@ -131,18 +133,145 @@ __global__ void k_addco(uint32_t *out, uint32_t seed) {
     out[blockIdx.x * blockDim.x + threadIdx.x] = r;
 }
 
+// ChaCha20 blocks back to back (the exact device function the AEAD uses)
+constexpr int CHACHA_BLOCKS = 64;
+__global__ void k_chacha(uint32_t *out, uint32_t seed) {
+    rg::Key8 key;
+    for (int i = 0; i < 8; ++i) key.k[i] = seed * (i + 1) + threadIdx.x;
+    uint32_t acc = 0, ks[16];
+    for (int b = 0; b < CHACHA_BLOCKS; ++b) {
+        rg::chacha_block(key, b + 1, 0u, threadIdx.x, blockIdx.x, ks);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc ^= ks[i];
+    }
+    out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
+}
+
+__global__ void k_chacha2(uint32_t *out, uint32_t seed) {
+    rg::Key8 key;
+    for (int i = 0; i < 8; ++i) key.k[i] = seed * (i + 1) + threadIdx.x;
+    uint32_t acc = 0, ks[16], kt[16];
+    for (int b = 0; b < CHACHA_BLOCKS; b += 2) {
+        rg::chacha_block(key, b + 1, 0u, threadIdx.x, blockIdx.x, ks);
+        rg::chacha_block(key, b + 2, 0u, threadIdx.x, blockIdx.x, kt);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc ^= ks[i] ^ kt[i];
+    }
+    out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
+}
+
+// ChaCha with an in-kernel clock stamp: lane 0 of each wave records
+// (s_memtime delta, s_memrealtime delta) into clk[wave] (100 MHz real-time).
+__global__ void k_chacha_clk(uint32_t *out, uint32_t seed, unsigned long long *clk) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
+    rg::Key8 key;
+    for (int i = 0; i < 8; ++i) key.k[i] = seed * (i + 1) + threadIdx.x;
+    uint32_t acc = 0, ks[16];
+    for (int b = 0; b < 4 * CHACHA_BLOCKS; ++b) {
+        rg::chacha_block(key, b + 1, 0u, threadIdx.x, blockIdx.x, ks);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc ^= ks[i];
+    }
+    out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
+    if ((threadIdx.x & 63) == 0) {
+        const uint32_t wv = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+        clk[2 * wv] = t1 - t0;
+        clk[2 * wv + 1] = r1 - r0;
+    }
+}
+
+// Poly1305 blocks (clamped multiply + add) back to back
+constexpr int POLY_BLOCKS = 1024;
+__global__ void k_poly(uint32_t *out, uint32_t seed) {
+    const rg::Mul r = rg::make_mul(seed * 0x9e3779b9u, seed ^ threadIdx.x, seed + 7, seed * 3);
+    rg::Acc h = {threadIdx.x, seed, 1, 2, 0};
+    for (int b = 0; b < POLY_BLOCKS; ++b) {
+        rg::acc_mul(h, r);
+        rg::acc_add(h, b, seed, b * 3, 7, 1);
+    }
+    out[blockIdx.x * blockDim.x + threadIdx.x] = h.h0 ^ h.h1 ^ h.h2 ^ h.h3 ^ h.h4;
+}
+
+__global__ void k_polygen(uint32_t *out, uint32_t seed) {
+    rg::Acc g = {seed * 0x9e3779b9u, seed ^ threadIdx.x, seed + 7, seed * 3, 1};
+    const rg::Gen G = rg::make_gen(g);
+    rg::Acc h = {threadIdx.x, seed, 1, 2, 0};
+    for (int b = 0; b < POLY_BLOCKS; ++b) {
+        rg::acc_mul_gen(h, G);
+        rg::acc_add(h, b, seed, b * 3, 7, 1);
+    }
+    out[blockIdx.x * blockDim.x + threadIdx.x] = h.h0 ^ h.h1 ^ h.h2 ^ h.h3 ^ h.h4;
+}
+
+
+#define UNARY_KERNEL(NAME, ASM)                                                   \
+    __global__ void NAME(uint32_t *out, uint32_t seed) {                          \
+        uint32_t a[8];                                                            \
+        for (int i = 0; i < 8; ++i) a[i] = seed + threadIdx.x + i;                \
+        const uint32_t b = seed * 3 + 1, c = seed ^ 0x55;                         \
+        for (int it = 0; it < ITERS; ++it) {                                      \
+            _Pragma("unroll") for (int i = 0; i < 8; ++i) asm volatile(ASM : "+v"(a[i]) : "v"(b), "v"(c)); \
+        }                                                                         \
+        uint32_t r = 0;                                                           \
+        for (int i = 0; i < 8; ++i) r ^= a[i];                                    \
+        out[blockIdx.x * blockDim.x + threadIdx.x] = r;                           \
+    }
+
+UNARY_KERNEL(k_xor, "v_xor_b32 %0, %0, %1")
+UNARY_KERNEL(k_and, "v_and_b32 %0, %0, %1")
+UNARY_KERNEL(k_lshl, "v_lshlrev_b32 %0, 3, %0")
+UNARY_KERNEL(k_perm, "v_perm_b32 %0, %0, %0, %1")
+UNARY_KERNEL(k_xor3, "v_or3_b32 %0, %0, %1, %2")
+UNARY_KERNEL(k_add3, "v_add3_u32 %0, %0, %1, %2")
+UNARY_KERNEL(k_lshlor, "v_lshl_or_b32 %0, %0, 3, %1")
+UNARY_KERNEL(k_xad, "v_xad_u32 %0, %0, %1, %2")
+UNARY_KERNEL(k_alignbit2, "v_alignbit_b32 %0, %0, %1, 7")
+UNARY_KERNEL(k_add_e64, "v_add_u32_e64 %0, %0, %1")
+UNARY_KERNEL(k_xor_e64, "v_xor_b32_e64 %0, %0, %1")
+UNARY_KERNEL(k_mov, "v_mov_b32 %0, %1")
+UNARY_KERNEL(k_pkadd16, "v_pk_add_u16 %0, %0, %1")
+UNARY_KERNEL(k_xor_sdwa, "v_xor_b32_sdwa %0, %0, %1 dst_sel:DWORD dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 src1_sel:DWORD")
+UNARY_KERNEL(k_mix, "v_add_u32 %0, %0, %1\n\tv_xor_b32 %0, %0, %2\n\tv_alignbit_b32 %0, %0, %0, 16")
+
 typedef void (*kfn)(uint32_t *, uint32_t);
+
+// units processed per ns per CU (blocks for chacha/poly).  Dynamic LDS of
+// 160 KiB / waves_per_simd per 256-thread block forces exactly that many
+// blocks (= waves per SIMD) onto every CU.
+static double run_units(kfn f, int waves_per_simd, uint32_t *d, double units_per_lane) {
+    const int threads = 256;
+    const int blocks = 256 * waves_per_simd;
+    const size_t lds = (160 * 1024 / waves_per_simd) & ~255;
+    CHECK(hipFuncSetAttribute((const void *)f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    hipEvent_t a, b;
+    CHECK(hipEventCreate(&a));
+    CHECK(hipEventCreate(&b));
+    hipLaunchKernelGGL(f, dim3(blocks), dim3(threads), lds, 0, d, 1u);
+    CHECK(hipDeviceSynchronize());
+    CHECK(hipEventRecord(a));
+    for (int r = 0; r < 5; ++r) hipLaunchKernelGGL(f, dim3(blocks), dim3(threads), lds, 0, d, 1u);
+    CHECK(hipEventRecord(b));
+    CHECK(hipEventSynchronize(b));
+    float ms;
+    CHECK(hipEventElapsedTime(&ms, a, b));
+    return 5.0 * blocks * threads * units_per_lane / (ms * 1e6) / 256.0;
+}
 
 static double run(kfn f, int waves_per_simd, uint32_t *d, int insts_per_iter) {
     const int threads = 256;
     const int blocks = 256 * waves_per_simd; // 4 waves/block -> waves_per_simd waves per SIMD
+    const size_t lds = (160 * 1024 / waves_per_simd) & ~255;
+    CHECK(hipFuncSetAttribute((const void *)f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     hipEvent_t a, b;
     CHECK(hipEventCreate(&a));
     CHECK(hipEventCreate(&b));
-    hipLaunchKernelGGL(f, dim3(blocks), dim3(threads), 0, 0, d, 1u);
+    hipLaunchKernelGGL(f, dim3(blocks), dim3(threads), lds, 0, d, 1u);
     CHECK(hipDeviceSynchronize());
     CHECK(hipEventRecord(a));
-    for (int r = 0; r < 5; ++r) hipLaunchKernelGGL(f, dim3(blocks), dim3(threads), 0, 0, d, 1u);
+    for (int r = 0; r < 5; ++r) hipLaunchKernelGGL(f, dim3(blocks), dim3(threads), lds, 0, d, 1u);
     CHECK(hipEventRecord(b));
     CHECK(hipEventSynchronize(b));
     float ms;
@@ -154,14 +283,20 @@ static double run(kfn f, int waves_per_simd, uint32_t *d, int insts_per_iter) {
 
 int main() {
     uint32_t *d;
-    CHECK(hipMalloc(&d, 256 * 16 * 256 * 4));
+    CHECK(hipMalloc(&d, 256 * 16 * 256 * 4 * 2));
     struct {
         const char *name;
         kfn f;
         int per;
     } ks[] = {{"v_add_u32", k_add, 1},       {"v_alignbit_b32", k_alignbit, 1}, {"v_mad_u64_u32", k_mad64, 1},
               {"v_mul_lo_u32", k_mullo, 1},  {"v_mul_hi_u32", k_mulhi, 1},      {"v_mad_u32_u24", k_mul24, 1},
-              {"v_fma_f64", k_fma64, 1},     {"add_co+addc", k_addco, 2}};
+              {"v_fma_f64", k_fma64, 1},     {"add_co+addc", k_addco, 2},
+              {"v_xor_b32", k_xor, 1}, {"v_and_b32", k_and, 1}, {"v_lshlrev_b32", k_lshl, 1},
+              {"v_perm_b32", k_perm, 1}, {"v_or3_b32", k_xor3, 1}, {"v_add3_u32", k_add3, 1},
+              {"v_lshl_or_b32", k_lshlor, 1}, {"v_xad_u32", k_xad, 1}, {"v_alignbit_b32(2src)", k_alignbit2, 1},
+              {"v_add_u32_e64", k_add_e64, 1}, {"v_xor_b32_e64", k_xor_e64, 1}, {"v_mov_b32", k_mov, 1},
+              {"v_pk_add_u16", k_pkadd16, 1}, {"v_xor_b32_sdwa", k_xor_sdwa, 1},
+              {"add+xor+alignbit", k_mix, 3}};
     printf("{\"unit\": \"wave-instructions per ns per CU (x64 lanes)\", \"results\": [\n");
     bool first = true;
     for (auto &k : ks) {
@@ -169,6 +304,46 @@ int main() {
             double r = run(k.f, w, d, k.per);
             printf("%s{\"inst\": \"%s\", \"waves_per_simd\": %d, \"rate\": %.4f}\n", first ? "" : ",", k.name, w, r);
             first = false;
+        }
+    }
+    printf("], \"kernels\": [\n");
+    first = true;
+    struct {
+        const char *name;
+        kfn f;
+        double units;
+    } ku[] = {{"chacha_block", k_chacha, CHACHA_BLOCKS}, {"chacha_block_x2", k_chacha2, CHACHA_BLOCKS},
+              {"poly_clamped_block", k_poly, POLY_BLOCKS},
+              {"poly_general_block", k_polygen, POLY_BLOCKS}};
+    for (auto &k : ku) {
+        for (int w : {1, 2, 3, 4, 6, 8}) {
+            double r = run_units(k.f, w, d, k.units);
+            printf("%s{\"kernel\": \"%s\", \"waves_per_simd\": %d, \"per_ns_per_cu\": %.4f, "
+                   "\"chip_GB_s\": %.1f}\n", first ? "" : ",", k.name, w, r,
+                   r * 256 * ((k.f == k_chacha || k.f == k_chacha2) ? 64 : 16));
+            first = false;
+        }
+    }
+    printf("], \"clock\": [\n");
+    {
+        unsigned long long *dclk;
+        const int maxw = 256 * 8 * 4;
+        CHECK(hipMalloc(&dclk, sizeof(unsigned long long) * 2 * maxw));
+        CHECK(hipFuncSetAttribute((const void *)k_chacha_clk, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        bool f2 = true;
+        for (int w : {1, 2, 4, 8}) {
+            const int blocks = 256 * w;
+            const size_t lds = (160 * 1024 / w) & ~255;
+            for (int rep = 0; rep < 3; ++rep)
+                hipLaunchKernelGGL(k_chacha_clk, dim3(blocks), dim3(256), lds, 0, d, 1u, dclk);
+            CHECK(hipDeviceSynchronize());
+            static unsigned long long h[2 * 256 * 8 * 4];
+            CHECK(hipMemcpy(h, dclk, sizeof(unsigned long long) * 2 * blocks * 4, hipMemcpyDeviceToHost));
+            double sum = 0;
+            for (int i = 0; i < blocks * 4; ++i) sum += (double)h[2 * i] / (double)h[2 * i + 1] * 0.1;
+            printf("%s{\"waves_per_simd\": %d, \"clock_GHz\": %.3f, \"cycles_per_wave_block\": %.0f}\n",
+                   f2 ? "" : ",", w, sum / (blocks * 4), (double)h[0] / (4 * CHACHA_BLOCKS));
+            f2 = false;
         }
     }
     printf("]}\n");

@@ -1,0 +1,55 @@
+#!/usr/bin/env python3
+"""Section shares of the LDS-staged kernel from its s_memtime diagnostic build (debug mode 3)."""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from rustyguard_amd import workloads  # noqa: E402
+from rustyguard_amd.aead import Engine  # noqa: E402
+from rustyguard_amd.device import DeviceBatch  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--workload", default="cfg2")
+ap.add_argument("--staged", type=int, default=2)
+ap.add_argument("--wg-per-cu", type=int, default=1)
+args = ap.parse_args()
+eng = Engine(0)
+eng.set_staged(args.staged)
+eng.set_wg_per_cu(args.wg_per_cu)
+w = workloads.build(args.workload)
+b = DeviceBatch(eng, w)
+b.fill()
+dbg = torch.zeros(8 * 256 * 32, dtype=torch.int64, device="cuda")
+eng.set_debug_buffer(dbg)
+eng.set_debug_mode(3)
+out = {}
+for op in ("seal", "open"):
+    for rep in range(3):
+        # every measured open gets a freshly sealed batch (a repeated open would
+        # fail the tag check and time the restore path instead)
+        if op == "open":
+            eng.set_debug_mode(0)
+            b.seal()
+            torch.cuda.synchronize()
+            eng.set_debug_mode(3)
+        dbg.zero_()
+        b.seal() if op == "seal" else b.open()
+        torch.cuda.synchronize()
+        if op == "seal":
+            eng.set_debug_mode(0)
+            b.open()  # restore plaintext so each seal starts from the same state
+            torch.cuda.synchronize()
+            eng.set_debug_mode(3)
+    d = dbg.cpu().numpy().reshape(-1, 8)
+    d = d[d[:, 6] == 1]
+    names = ["setup", "store", "dma_issue", "dma_wait", "chunk", "tail"]
+    tot = d[:, :6].sum(axis=1)
+    out[op] = {"waves": int(len(d)), "cycles_per_wave_mean": float(tot.mean()),
+               "share": {n: round(float(d[:, k].sum() / tot.sum()), 4) for k, n in enumerate(names)}}
+print(json.dumps(out, indent=1))
