@@ -1,0 +1,133 @@
+"""CPU-only checks of the C ABI boundary (no GPU needed).
+
+* librg_aead.so loads and exports every function include/rg_aead.h declares;
+* the ctypes binding (rustyguard_amd/_lib.py) covers the same set;
+* the public structs have the layout the header promises (compiled with gcc);
+* without a GPU, rg_create fails cleanly with an error code (no crash), and
+  the product package never falls back to a CPU path.
+"""
+import ctypes
+import os
+import re
+import subprocess
+import sys
+import textwrap
+
+import pytest
+
+from conftest import REPO
+from rustyguard_amd import _lib
+
+HEADER = os.path.join(REPO, "include", "rg_aead.h")
+
+
+def header_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(rg_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_declares_the_batched_boundary():
+    fns = header_functions()
+    for must in ["rg_create", "rg_destroy", "rg_seal_batch_dev", "rg_open_batch_dev", "rg_seal_batch_host",
+                 "rg_open_batch_host", "rg_chacha20poly1305_enc", "rg_chacha20poly1305_dec",
+                 "rg_antireplay_would_accept", "rg_antireplay_mark_seen", "rg_send_batch", "rg_recv_batch"]:
+        assert must in fns
+
+
+def test_library_exports_every_header_symbol():
+    path = _lib.lib_path()
+    if not os.path.exists(path):
+        from rustyguard_amd import build
+
+        build.build()
+    L = ctypes.CDLL(path)
+    missing = [f for f in header_functions() if not hasattr(L, f)]
+    assert not missing, missing
+    out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r" T (rg_[a-z0-9_]+)", out))
+    assert set(header_functions()) <= exported
+
+
+def test_ctypes_binding_covers_header():
+    assert set(header_functions()) == set(_lib.SIGNATURES), set(header_functions()) ^ set(_lib.SIGNATURES)
+
+
+def test_abi_version():
+    assert _lib.lib().rg_abi_version() == 1
+
+
+def test_struct_layout_with_gcc(tmp_path):
+    src = tmp_path / "layout.c"
+    src.write_text(textwrap.dedent("""
+        #include <stdio.h>
+        #include <stddef.h>
+        #include "rg_aead.h"
+        int main(void) {
+            printf("%zu %zu %zu %zu %zu %zu\\n", sizeof(rg_pkt_desc), offsetof(rg_pkt_desc, offset),
+                   offsetof(rg_pkt_desc, len), offsetof(rg_pkt_desc, key_idx), sizeof(rg_antireplay),
+                   offsetof(rg_antireplay, last));
+            return 0;
+        }
+    """))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", "-Wall", "-Werror", "-I", os.path.dirname(HEADER), str(src), "-o", str(exe)],
+                   check=True)
+    vals = list(map(int, subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()))
+    assert vals == [16, 0, 8, 12, 33 * 8, 32 * 8]
+
+
+def test_header_compiles_as_cxx(tmp_path):
+    src = tmp_path / "h.cpp"
+    src.write_text('#include "rg_aead.h"\nint main() { return rg_abi_version() == 1 ? 0 : 1; }\n')
+    subprocess.run(["g++", "-std=c++17", "-Wall", "-Werror", "-fsyntax-only", "-I", os.path.dirname(HEADER), str(src)],
+                   check=True)
+
+
+def test_create_without_gpu_fails_cleanly():
+    """No silent CPU fallback: on a GPU-less host rg_create returns an error code."""
+    code = textwrap.dedent(f"""
+        import ctypes, sys
+        sys.path.insert(0, {REPO!r})
+        from rustyguard_amd import _lib
+        h = ctypes.c_void_p()
+        rc = _lib.lib().rg_create(0, ctypes.byref(h))
+        print(rc, _lib.lib().rg_last_error().decode())
+    """)
+    env = dict(os.environ, HIP_VISIBLE_DEVICES=os.environ.get("HIP_VISIBLE_DEVICES", ""))
+    try:
+        import torch
+
+        has_gpu = torch.cuda.is_available()
+    except Exception:
+        has_gpu = False
+    if has_gpu:
+        pytest.skip("a GPU is present")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0, r.stderr
+    rc = int(r.stdout.split()[0])
+    assert rc < 0
+
+
+def test_engine_raises_without_gpu():
+    try:
+        import torch
+
+        if torch.cuda.is_available():
+            pytest.skip("a GPU is present")
+    except ImportError:
+        pass
+    from rustyguard_amd.aead import Engine
+    from rustyguard_amd._lib import RgError
+
+    with pytest.raises(RgError):
+        Engine(0)
+
+
+def test_product_package_does_not_import_oracle():
+    pkg = os.path.join(REPO, "rustyguard_amd")
+    for root, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith((".py", ".cpp", ".hip", ".h")):
+                text = open(os.path.join(root, f)).read()
+                assert "from oracle" not in text and "import oracle" not in text and "rg_oracle" not in text, f
