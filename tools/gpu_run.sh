@@ -39,6 +39,13 @@ for s in "$@"; do
     prof)
         run prof 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- \
             python3 bench.py --steps 30 --warmup 5 --cpu-seconds 0 ;;
+    default) run bench_default 600 python bench.py ;;
+    pmc_hbm)
+        W=${RG_PMC_WORKLOAD:-cfg2}
+        run pmc_fetch_$W 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch_$W -o p -- \
+            python3 bench.py --workload $W --steps 5 --warmup 2 --cpu-seconds 0
+        run pmc_write_$W 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write_$W -o p -- \
+            python3 bench.py --workload $W --steps 5 --warmup 2 --cpu-seconds 0 ;;
     pmc_list) run pmc_list 120 rocprofv3 -L ;;
     pmc)
         # separate passes (TCC FETCH_SIZE and WRITE_SIZE do not fit one pass; never combined with tracing domains)
