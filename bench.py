@@ -52,14 +52,19 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(w, seconds: float, threads: int):
-    """CPU restatement (oracle/, RFC 8439 port) timed on this host's cores.
+def cpu_baseline(w, seconds: float, threads: int, impl: str = "port"):
+    """A CPU implementation timed on this host's cores over a bounded sample of the workload.
 
-    The reference's own CPU path (Rust + graviola 0.2.0) cannot be built here
-    (no cargo, crate not vendored), so kind = "port".
+    impl "port": the C RFC 8439 restatement in oracle/ (kind "port"; the
+    reference's own CPU path, Rust + graviola 0.2.0, cannot be built here: no
+    cargo, crate not vendored).  impl "openssl": OpenSSL EVP ChaCha20-Poly1305
+    (BASELINE.md CPU-B, an assembly-optimised stand-in for graviola).
     """
     from oracle import oracle  # checker / baseline only
 
+    if impl == "openssl" and not oracle.openssl_available():
+        return None
+    seal = oracle.openssl_seal_batch if impl == "openssl" else oracle.seal_batch
     n = min(w.n, 4096)
     desc = w.desc[:n].copy()
     base = int(desc["offset"][0])
@@ -73,18 +78,26 @@ def cpu_baseline(w, seconds: float, threads: int):
     payload = int(desc["len"].astype(np.int64).sum())
     reps, t0 = 0, time.perf_counter()
     while True:
-        oracle.seal_batch(w.keys, w.receivers, desc, ctr, buf, nthreads=threads)
-        st, _ = oracle.open_batch(w.keys, od, buf, nthreads=threads)
+        seal(w.keys, w.receivers, desc, ctr, buf, nthreads=threads)
+        if impl == "openssl":
+            st = oracle.openssl_open_batch(w.keys, od, buf, nthreads=threads)
+        else:
+            st, _ = oracle.open_batch(w.keys, od, buf, nthreads=threads)
         reps += 1
         el = time.perf_counter() - t0
         if el >= seconds:
             break
     assert (st == 0).all()
     gib = 2 * payload * reps / el / 2**30
-    return {"value": round(gib, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
-            "mpkt_s": round(2 * n * reps / el / 1e6, 4),
-            "sample": f"{n} packets of {w.name} (P={int(desc['len'][0])}) seal+open x{reps} in {el:.1f}s, "
-                      f"{threads} threads, C RFC 8439 restatement (oracle/rg_oracle.c)"}
+    what = ("C RFC 8439 restatement (oracle/rg_oracle.c)" if impl == "port" else
+            f"{oracle.openssl_version()} EVP_chacha20_poly1305, re-keyed per packet (oracle/rg_openssl_batch.c)")
+    out = {"value": round(gib, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
+           "mpkt_s": round(2 * n * reps / el / 1e6, 4),
+           "sample": f"{n} packets of {w.name} (mean P={payload / n:.1f}) seal+open x{reps} in {el:.1f}s, "
+                     f"{threads} threads, {what}"}
+    if impl == "openssl":
+        out["kind"] = "openssl (stand-in for graviola)"
+    return out
 
 
 def load_traffic(workload: str):
@@ -262,6 +275,9 @@ def main():
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         thr = args.cpu_threads or min(16, os.cpu_count() or 1)
         out["cpu_baseline"] = cpu_baseline(w, args.cpu_seconds, thr)
+        ossl = cpu_baseline(w, args.cpu_seconds / 2, thr, impl="openssl")
+        if ossl:
+            out["cpu_openssl"] = ossl
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

@@ -47,6 +47,12 @@ def lib():
         L.rg_oracle_mix64.argtypes = [ctypes.c_uint64]
         L.rg_oracle_mix64.restype = ctypes.c_uint64
         L.rg_oracle_synth_fill.argtypes = [u8p, u8p, u8p, ctypes.c_size_t, ctypes.c_uint64]
+        L.rg_openssl_available.restype = ctypes.c_int
+        L.rg_openssl_version.restype = ctypes.c_char_p
+        L.rg_openssl_seal_batch.argtypes = [u8p, u8p, u8p, u8p, ctypes.c_size_t, u8p, u8p, ctypes.c_int]
+        L.rg_openssl_seal_batch.restype = ctypes.c_int
+        L.rg_openssl_open_batch.argtypes = [u8p, u8p, ctypes.c_size_t, u8p, u8p, ctypes.c_int]
+        L.rg_openssl_open_batch.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -128,3 +134,31 @@ def mix64(x: int) -> int:
 def synth_fill(buf: np.ndarray, desc: np.ndarray, inner_len: np.ndarray, seed: int) -> None:
     inner = np.ascontiguousarray(inner_len, dtype=np.uint32)
     lib().rg_oracle_synth_fill(_ptr(buf), _ptr(desc), _ptr(inner), len(desc), seed)
+
+
+# ---- OpenSSL EVP ChaCha20-Poly1305 batches (CPU baseline "CPU-B", oracle/rg_openssl_batch.c)
+def openssl_available() -> bool:
+    return bool(lib().rg_openssl_available())
+
+
+def openssl_version() -> str:
+    return lib().rg_openssl_version().decode()
+
+
+def openssl_seal_batch(keys, receivers, desc, counters, buf, nthreads=1, status=None):
+    keys = np.ascontiguousarray(keys, dtype=np.uint8)
+    counters = np.ascontiguousarray(counters, dtype=np.uint64)
+    rec = None if receivers is None else np.ascontiguousarray(receivers, dtype=np.uint32)
+    rc = lib().rg_openssl_seal_batch(_ptr(keys), _ptr(rec), _ptr(desc), _ptr(counters), len(desc), _ptr(buf),
+                                     _ptr(status), nthreads)
+    if rc != 0:
+        raise RuntimeError("libcrypto.so.3 not available")
+
+
+def openssl_open_batch(keys, desc, buf, nthreads=1):
+    keys = np.ascontiguousarray(keys, dtype=np.uint8)
+    status = np.zeros(max(len(desc), 1), np.uint8)
+    rc = lib().rg_openssl_open_batch(_ptr(keys), _ptr(desc), len(desc), _ptr(buf), _ptr(status), nthreads)
+    if rc != 0:
+        raise RuntimeError("libcrypto.so.3 not available")
+    return status[: len(desc)]

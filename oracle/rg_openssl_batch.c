@@ -1,0 +1,151 @@
+/* TEST / BASELINE INFRASTRUCTURE ONLY -- never linked into the product.
+ *
+ * Multi-threaded batch seal/open through OpenSSL's EVP ChaCha20-Poly1305
+ * (libcrypto.so.3, dlopen'ed), the CPU baseline "CPU-B" of BASELINE.md §2: an
+ * assembly-optimised RFC 8439 implementation standing in for the reference's
+ * graviola 0.2.0 AEAD (Cargo.lock:370-373), which cannot be built here.  Same
+ * buffer contract as rg_oracle_seal_batch / rg_oracle_open_batch; like the
+ * reference (rustyguard-crypto/src/prim.rs:186-200, ChaCha20Poly1305::new per
+ * call) every packet re-keys the cipher context.
+ */
+#define _GNU_SOURCE
+#include <dlfcn.h>
+#include <pthread.h>
+#include <stddef.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "rg_oracle.h"
+
+typedef void EVP_CIPHER_CTX;
+typedef void EVP_CIPHER;
+
+static struct {
+    int ok;
+    EVP_CIPHER_CTX *(*ctx_new)(void);
+    void (*ctx_free)(EVP_CIPHER_CTX *);
+    const EVP_CIPHER *(*chacha)(void);
+    int (*cipher_init)(EVP_CIPHER_CTX *, const EVP_CIPHER *, void *, const uint8_t *, const uint8_t *, int);
+    int (*cipher_update)(EVP_CIPHER_CTX *, uint8_t *, int *, const uint8_t *, int);
+    int (*cipher_final)(EVP_CIPHER_CTX *, uint8_t *, int *);
+    int (*ctrl)(EVP_CIPHER_CTX *, int, int, void *);
+    const char *(*version)(int);
+} ssl;
+
+static pthread_once_t ssl_once = PTHREAD_ONCE_INIT;
+
+static void ssl_load(void) {
+    void *h = dlopen("libcrypto.so.3", RTLD_NOW | RTLD_LOCAL);
+    if (!h) return;
+    ssl.ctx_new = (EVP_CIPHER_CTX * (*)(void)) dlsym(h, "EVP_CIPHER_CTX_new");
+    ssl.ctx_free = (void (*)(EVP_CIPHER_CTX *))dlsym(h, "EVP_CIPHER_CTX_free");
+    ssl.chacha = (const EVP_CIPHER *(*)(void))dlsym(h, "EVP_chacha20_poly1305");
+    ssl.cipher_init = (int (*)(EVP_CIPHER_CTX *, const EVP_CIPHER *, void *, const uint8_t *, const uint8_t *, int))dlsym(
+        h, "EVP_CipherInit_ex");
+    ssl.cipher_update = (int (*)(EVP_CIPHER_CTX *, uint8_t *, int *, const uint8_t *, int))dlsym(h, "EVP_CipherUpdate");
+    ssl.cipher_final = (int (*)(EVP_CIPHER_CTX *, uint8_t *, int *))dlsym(h, "EVP_CipherFinal_ex");
+    ssl.ctrl = (int (*)(EVP_CIPHER_CTX *, int, int, void *))dlsym(h, "EVP_CIPHER_CTX_ctrl");
+    ssl.version = (const char *(*)(int))dlsym(h, "OpenSSL_version");
+    ssl.ok = ssl.ctx_new && ssl.ctx_free && ssl.chacha && ssl.cipher_init && ssl.cipher_update && ssl.cipher_final &&
+             ssl.ctrl;
+}
+
+/* 1 when libcrypto.so.3 with EVP_chacha20_poly1305 is available */
+int rg_openssl_available(void) {
+    pthread_once(&ssl_once, ssl_load);
+    return ssl.ok;
+}
+
+const char *rg_openssl_version(void) {
+    if (!rg_openssl_available() || !ssl.version) return "";
+    return ssl.version(0);
+}
+
+enum { CTRL_AEAD_GET_TAG = 0x10, CTRL_AEAD_SET_TAG = 0x11 };
+
+typedef struct {
+    int open;
+    const uint8_t *keys;
+    const uint32_t *receivers;
+    const rg_oracle_desc *desc;
+    const uint64_t *counters;
+    uint8_t *buf;
+    uint8_t *status;
+    size_t lo, hi;
+} job_t;
+
+static void put32(uint8_t *p, uint32_t v) {
+    for (int i = 0; i < 4; i++) p[i] = (uint8_t)(v >> (8 * i));
+}
+static void put64(uint8_t *p, uint64_t v) {
+    for (int i = 0; i < 8; i++) p[i] = (uint8_t)(v >> (8 * i));
+}
+static uint64_t get64(const uint8_t *p) {
+    uint64_t v = 0;
+    for (int i = 7; i >= 0; i--) v = (v << 8) | p[i];
+    return v;
+}
+
+static void *worker(void *arg) {
+    job_t *j = (job_t *)arg;
+    EVP_CIPHER_CTX *c = ssl.ctx_new();
+    uint8_t nonce[12];
+    for (size_t i = j->lo; i < j->hi; i++) {
+        const rg_oracle_desc *d = &j->desc[i];
+        uint8_t *frame = j->buf + d->offset;
+        const uint8_t *key = j->keys + 32 * (size_t)d->key_idx;
+        int outl = 0, ok = 1;
+        if (!j->open) {
+            const uint64_t ctr = j->counters[i];
+            rg_oracle_wg_nonce(ctr, nonce);
+            ok &= ssl.cipher_init(c, ssl.chacha(), NULL, key, nonce, 1);
+            ok &= ssl.cipher_update(c, frame + 16, &outl, frame + 16, (int)d->len);
+            ok &= ssl.cipher_final(c, frame + 16 + d->len, &outl);
+            ok &= ssl.ctrl(c, CTRL_AEAD_GET_TAG, 16, frame + 16 + d->len);
+            if (j->receivers) {
+                put32(frame, 4u);
+                put32(frame + 4, j->receivers[d->key_idx]);
+                put64(frame + 8, ctr);
+            }
+        } else {
+            const uint32_t P = d->len - 32;
+            rg_oracle_wg_nonce(get64(frame + 8), nonce);
+            ok &= ssl.cipher_init(c, ssl.chacha(), NULL, key, nonce, 0);
+            ok &= ssl.ctrl(c, CTRL_AEAD_SET_TAG, 16, frame + 16 + P);
+            ok &= ssl.cipher_update(c, frame + 16, &outl, frame + 16, (int)P);
+            ok &= ssl.cipher_final(c, frame + 16 + P, &outl) > 0;
+        }
+        if (j->status) j->status[i] = ok ? RG_ORACLE_OK : RG_ORACLE_DECRYPT_ERR;
+    }
+    ssl.ctx_free(c);
+    return NULL;
+}
+
+static int run(job_t proto, size_t n, int nthreads) {
+    if (!rg_openssl_available()) return -1;
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    pthread_t th[256];
+    job_t jobs[256];
+    for (int t = 0; t < nthreads; t++) {
+        jobs[t] = proto;
+        jobs[t].lo = n * (size_t)t / (size_t)nthreads;
+        jobs[t].hi = n * (size_t)(t + 1) / (size_t)nthreads;
+    }
+    for (int t = 0; t < nthreads; t++) pthread_create(&th[t], NULL, worker, &jobs[t]);
+    for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+    return 0;
+}
+
+/* seal: desc.len = P; open: desc.len = W = P + 32 (seal output, ciphertext framed) */
+int rg_openssl_seal_batch(const uint8_t *keys, const uint32_t *receivers, const rg_oracle_desc *desc,
+                          const uint64_t *counters, size_t n, uint8_t *buf, uint8_t *status, int nthreads) {
+    job_t p = {0, keys, receivers, desc, counters, buf, status, 0, 0};
+    return run(p, n, nthreads);
+}
+
+int rg_openssl_open_batch(const uint8_t *keys, const rg_oracle_desc *desc, size_t n, uint8_t *buf, uint8_t *status,
+                          int nthreads) {
+    job_t p = {1, keys, NULL, desc, NULL, buf, status, 0, 0};
+    return run(p, n, nthreads);
+}

@@ -97,3 +97,24 @@ def test_oracle_open_rejects_every_single_bit_flip_of_tag():
         t = bytearray(tag)
         t[bit // 8] ^= 1 << (bit % 8)
         assert oracle.aead_open(key, oracle.wg_nonce(7), b"", ct, bytes(t)) is None
+
+
+def test_openssl_batch_baseline_matches_oracle():
+    """The OpenSSL CPU baseline (oracle/rg_openssl_batch.c) computes the same frames as the oracle."""
+    from rustyguard_amd import workloads as wl
+
+    if not oracle.openssl_available():
+        pytest.skip("libcrypto.so.3 not present")
+    w = wl.imix(300)
+    a = np.zeros(w.buf_bytes, np.uint8)
+    oracle.synth_fill(a, w.desc, w.inner_len, w.data_seed)
+    b = a.copy()
+    oracle.seal_batch(w.keys, w.receivers, w.desc, w.counters, a)
+    oracle.openssl_seal_batch(w.keys, w.receivers, w.desc, w.counters, b, nthreads=3)
+    assert np.array_equal(a, b)
+    od = w.open_desc()
+    st = oracle.openssl_open_batch(w.keys, od, b, nthreads=2)
+    assert (st == 0).all()
+    a[int(od["offset"][7]) + 20] ^= 1
+    st = oracle.openssl_open_batch(w.keys, od, a, nthreads=1)
+    assert st[7] == oracle.DECRYPT_ERR and (np.delete(st, 7) == 0).all()
