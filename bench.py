@@ -48,7 +48,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--e2e", action="store_true", help="also time the pinned host->GPU->host path")
-    ap.add_argument("--verify", action="store_true", help="check statuses after the timed region")
+    ap.add_argument("--no-verify", dest="verify", action="store_false",
+                    help="skip the status check after the timed region (on by default, outside the timing)")
     return ap.parse_args()
 
 

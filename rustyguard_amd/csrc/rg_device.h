@@ -11,6 +11,14 @@
 namespace rg {
 
 // ---------------------------------------------------------------- ChaCha20
+// wave-uniform copies via s_readfirstlane.  The builtin works on int: go
+// through uint32_t so that a set bit 31 is never sign-extended into a 64-bit
+// value (byte offsets past 2 GiB).
+__device__ __forceinline__ uint32_t uniform_u32(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ uint64_t uniform_u64(uint64_t v) {
+    return ((uint64_t)uniform_u32((uint32_t)(v >> 32)) << 32) | (uint64_t)uniform_u32((uint32_t)v);
+}
+
 __device__ __forceinline__ uint32_t rotl(uint32_t v, int n) { return __builtin_rotateleft32(v, n); }
 
 #define RG_QR(a, b, c, d)                         \

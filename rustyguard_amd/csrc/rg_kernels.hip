@@ -490,8 +490,7 @@ __global__ __launch_bounds__(256) void staged_kernel(SealArgs sa, OpenArgs oa) {
             const uint64_t o = __shfl_xor(lo, m);
             lo = o < lo ? o : lo;
         }
-        lo = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(lo >> 32)) << 32) |
-             __builtin_amdgcn_readfirstlane((uint32_t)lo);
+        lo = uniform_u64(lo);
         if (lo == ~0ull) lo = 0;
         const uint64_t span_cap = buf_len - lo;
         const uint32_t nrec = span_cap > kOOB ? kOOB : (uint32_t)span_cap;
@@ -507,7 +506,7 @@ __global__ __launch_bounds__(256) void staged_kernel(SealArgs sa, OpenArgs oa) {
             const uint32_t o = __shfl_xor(Wl, m);
             Wl = o > Wl ? o : Wl;
         }
-        const uint32_t W = __builtin_amdgcn_readfirstlane(Wl);
+        const uint32_t W = uniform_u32(Wl);
         // DMA/store address table: instruction q serves packet pq = q*PKT_PER_INST + lane/PPW,
         // piece k = (lane % PPW) ^ swz(pq)
         uint32_t tb[PPW], tlim[PPW];

@@ -340,3 +340,56 @@ def test_full_config_digest(engine, name):
             o, p = int(d["offset"]), int(d["len"])
             assert np.array_equal(hb[o + 16:o + 16 + p], plain[o + 16:o + 16 + p])
     _reset(engine)
+
+
+@pytest.mark.parametrize("mode", MODES, ids=_mode_id)
+def test_frames_past_2_and_4_gib(engine, mode):
+    """Byte offsets with bit 31 / bit 32 set (large device arenas, BASELINE config 5 on one GPU)."""
+    _configure(engine, mode)
+    rng = np.random.default_rng(99)
+    marks = [0, 1 << 31, 1 << 32, 3 << 31]
+    offs = []
+    for m in marks:
+        base = max(0, m - 1536 * 40)
+        offs += [base + 1536 * k for k in range(80)]
+    n = len(offs)
+    P = rng.integers(0, 95, n) * 16
+    desc = np.zeros(n, DESC_DTYPE)
+    desc["offset"] = offs
+    desc["len"] = P
+    desc["key_idx"] = rng.integers(0, 2, n)
+    keys = rng.integers(0, 256, (2, 32), dtype=np.uint8)
+    rec = np.array([7, 9], np.uint32)
+    ctr = rng.integers(0, 2**40, n, dtype=np.uint64)
+    total = offs[-1] + 1536 + 64
+    buf = torch.zeros(total, dtype=torch.uint8, device="cuda")
+    frames = []
+    for i in range(n):
+        f = rng.integers(0, 256, int(P[i]) + 32, dtype=np.uint8)
+        frames.append(f)
+        buf[offs[i]: offs[i] + len(f)] = _dev(f)
+    st = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    engine.seal_dev(_dev(keys), _dev(rec.view(np.int32)), _dev(desc.view(np.uint8).reshape(-1, 16)),
+                    _dev(ctr.view(np.int64)), buf, st)
+    torch.cuda.synchronize()
+    assert (st.cpu().numpy() == 0).all()
+    for i in range(n):
+        ref = frames[i].copy()
+        one = np.zeros(1, DESC_DTYPE)
+        one[0] = (0, P[i], desc["key_idx"][i])
+        oracle.seal_batch(keys, rec, one, ctr[i:i + 1], ref)
+        got = buf[offs[i]: offs[i] + len(ref)].cpu().numpy()
+        assert np.array_equal(got, ref), (i, offs[i])
+    od = desc.copy()
+    od["len"] += 32
+    ctr_out = torch.zeros(n, dtype=torch.int64, device="cuda")
+    engine.open_dev(_dev(keys), _dev(od.view(np.uint8).reshape(-1, 16)), buf, st, ctr_out)
+    torch.cuda.synchronize()
+    assert (st.cpu().numpy() == 0).all()
+    assert np.array_equal(ctr_out.cpu().numpy().view(np.uint64), ctr)
+    for i in range(0, n, 7):
+        got = buf[offs[i] + 16: offs[i] + 16 + int(P[i])].cpu().numpy()
+        assert np.array_equal(got, frames[i][16:16 + int(P[i])])
+    del buf
+    torch.cuda.empty_cache()
+    _reset(engine)
