@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--lanes", type=int, default=0, help="lanes per packet (0 = auto)")
     ap.add_argument("--wg-per-cu", type=int, default=0, help="resident workgroups per CU (0 = auto, -1 = plain grid)")
     ap.add_argument("--staged", type=int, default=-1, help="LDS-staged window chunks (0 = lane-pass kernels, -1 = default)")
+    ap.add_argument("--plan", type=int, default=-1, help="size-class planner: 1 on, 0 off, -1 library default (on)")
+    ap.add_argument("--segments", type=int, default=0, help="segments per packet for the tile kernels (0 = auto)")
     ap.add_argument("--debug-mode", type=int, default=0, help="seal diagnostics (invalid output): 1 compute-only, 2 memory-only")
     ap.add_argument("--no-graph", action="store_true", help="launch eagerly instead of replaying a captured HIP graph")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget (0 = skip)")
@@ -136,6 +138,10 @@ def main():
         eng.set_debug_mode(args.debug_mode)
     if args.staged >= 0:
         eng.set_staged(args.staged)
+    if args.plan >= 0:
+        eng.set_plan(bool(args.plan))
+    if args.segments:
+        eng.set_segments(args.segments)
     if args.workload == "cfg5":
         w = workloads.build("cfg5", rank, world)
     else:
@@ -254,7 +260,8 @@ def main():
                    "mean_payload_bytes": round(payload / max(w.n, 1), 2), "wire_bytes_per_gpu": w.wire_bytes,
                    "sessions": int(w.meta.get("sessions", 1)), "parallelism": f"split{world} (no collective)",
                    "kernel": (f"lane-pass, {eng.lanes_per_packet(w.n)} lanes/packet" if args.staged == 0 else
-                              f"lds-staged, {args.staged if args.staged > 0 else 2} chunks/window"),
+                              f"lds-staged tiles, {args.staged if args.staged > 0 else 2} chunks/window, "
+                              f"planner {'off' if args.plan == 0 else 'on'}, segments {args.segments or 'auto'}"),
                    "wg_per_cu": args.wg_per_cu or "auto"},
         "mpkt_s": round(total_pkts / tmax / 1e6, 3),
         "seal_ms": round(seal_ms, 5),

@@ -112,15 +112,26 @@ int rg_set_lanes_per_packet(rg_ctx *ctx, int lanes);
 int rg_get_lanes_per_packet(rg_ctx *ctx, size_t n);
 int rg_set_wg_per_cu(rg_ctx *ctx, int wg_per_cu);
 /* Kernel choice: 0 = lane-pass kernels (K lanes per packet, direct loads),
- * 1/2/4 = LDS-staged tiles (one packet per lane, coalesced LDS-DMA windows
- * of that many 64-byte chunks). */
+ * 1/2 = LDS-staged tiles (one packet (segment) per lane, coalesced LDS-DMA
+ * windows of that many 64-byte chunks; default 2). */
 int rg_set_staged(rg_ctx *ctx, int window_chunks);
+/* Tile kernels: 1 (default) = a device-side planner first sorts the batch into
+ * size classes so that every 64-packet tile holds packets of similar length;
+ * 0 = tiles take packets in array order.  Device-API calls that share a
+ * context use one set of planner buffers: issue them on one stream (or order
+ * them) -- the host-memory API has its own per pipeline stream. */
+int rg_set_plan(rg_ctx *ctx, int on);
+/* Segments per packet for the tile kernels: 0 (default) = per size class,
+ * aiming at two resident waves per SIMD; 1/2/4 = split every packet into that
+ * many contiguous segments on separate waves (Poly1305 partial sums combined
+ * as sum_j A_j r^{N_j}). */
+int rg_set_segments(rg_ctx *ctx, int segments);
 /* Diagnostics only (profiling the seal kernel, output is NOT a valid seal):
  * 0 = normal, 1 = compute only (no payload loads/stores), 2 = memory only. */
 int rg_set_debug_mode(rg_ctx *ctx, int mode);
 /* mode 3 (staged kernels): per-wave s_memtime section totals are written to
  * this device buffer, 8 x u64 per wave (setup, store, dma-issue, dma-wait,
- * chunk, tail, valid, 0). */
+ * chunk, tail, valid, real-time ticks at 100 MHz). */
 int rg_set_debug_buffer(rg_ctx *ctx, void *dev_ptr);
 
 /* ----------------------------------------- host-memory batch (blocking) */

@@ -33,6 +33,8 @@ SIGNATURES = {
     "rg_set_wg_per_cu": (c_int, [c_vp, c_int]),
     "rg_set_debug_mode": (c_int, [c_vp, c_int]),
     "rg_set_staged": (c_int, [c_vp, c_int]),
+    "rg_set_plan": (c_int, [c_vp, c_int]),
+    "rg_set_segments": (c_int, [c_vp, c_int]),
     "rg_set_debug_buffer": (c_int, [c_vp, c_vp]),
     "rg_seal_batch_host": (c_int, [c_vp, c_u8p, c_vp, c_u32, c_vp, c_vp, c_size, c_u8p, c_size, c_u8p]),
     "rg_open_batch_host": (c_int, [c_vp, c_u8p, c_u32, c_vp, c_size, c_u8p, c_size, c_u8p, c_vp]),

@@ -77,9 +77,33 @@ struct HostBuf {
     }
 };
 
+// planner work lists (rg_tile.hip): class counts + [kClasses][cap] indices
+struct PlanBuf {
+    DevBuf counts, lists;
+    uint32_t cap = 0;
+    hipError_t reserve(size_t n) {
+        if (!counts.p) { // counters + done count; the tile kernels leave them zeroed
+            hipError_t e = counts.reserve((rg::kClasses + 1) * sizeof(uint32_t));
+            if (e == hipSuccess) e = hipMemset(counts.p, 0, (rg::kClasses + 1) * sizeof(uint32_t));
+            if (e != hipSuccess) return e;
+        }
+        hipError_t e = hipSuccess;
+        if (n <= cap) return e;
+        e = lists.reserve((size_t)rg::kClasses * n * sizeof(uint32_t));
+        if (e == hipSuccess) cap = (uint32_t)n;
+        return e;
+    }
+    void release() {
+        counts.release();
+        lists.release();
+        cap = 0;
+    }
+};
+
 // one pipeline lane of the host path
 struct Slot {
     hipStream_t stream = nullptr;
+    PlanBuf plan;
     DevBuf d_buf, d_desc, d_ctr, d_status, d_ctr_out;
     HostBuf h_desc, h_ctr, h_status, h_ctr_out;
     // bookkeeping of the slice in flight
@@ -96,6 +120,9 @@ struct rg_ctx {
     int cus = 0;
     int debug_mode = 0;
     int staged_g = 2; // 0 = lane-pass kernels, else LDS-staged windows of G chunks (default: 2)
+    int plan = 1;     // size-class planner before the tile kernel (0 = packets in array order)
+    int segments = 0; // segments per packet: 0 = automatic, else 1 / 2 / 4
+    PlanBuf plan_dev; // planner lists of the device API (calls on one ctx are stream-ordered)
     uint64_t *dbg = nullptr; // diagnostics buffer (device), stamp builds only
     int max_wg[2][3] = {{0, 0, 0}, {0, 0, 0}}; // [seal, open][K = 1, 2, 4]
     std::mutex mu;
@@ -135,6 +162,7 @@ int rg_create(int device, rg_ctx **out) {
     {
         hipError_t e = hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device);
         if (e == hipSuccess) e = rg::prepare_kernels(c->max_wg);
+        if (e == hipSuccess) e = rg::prepare_tile_kernels();
         if (e != hipSuccess) {
             delete c;
             return set_err(RG_EDEVICE, "kernel setup", e);
@@ -159,9 +187,11 @@ void rg_destroy(rg_ctx *ctx) {
             (void)hipStreamSynchronize(s.stream);
             (void)hipStreamDestroy(s.stream);
         }
+        s.plan.release();
         s.d_buf.release(); s.d_desc.release(); s.d_ctr.release(); s.d_status.release(); s.d_ctr_out.release();
         s.h_desc.release(); s.h_ctr.release(); s.h_status.release(); s.h_ctr_out.release();
     }
+    ctx->plan_dev.release();
     ctx->d_keys.release();
     ctx->d_recv.release();
     ctx->d_general.release();
@@ -196,8 +226,22 @@ int rg_set_wg_per_cu(rg_ctx *ctx, int wg) {
 
 int rg_set_staged(rg_ctx *ctx, int g) {
     if (!ctx) return set_err(RG_EINVAL, "null context");
-    if (g != 0 && g != 1 && g != 2 && g != 4) return set_err(RG_EINVAL, "staged window must be 0, 1, 2 or 4 chunks");
+    if (g != 0 && g != 1 && g != 2) return set_err(RG_EINVAL, "staged window must be 0, 1 or 2 chunks");
     ctx->staged_g = g;
+    return RG_OK;
+}
+
+int rg_set_plan(rg_ctx *ctx, int on) {
+    if (!ctx) return set_err(RG_EINVAL, "null context");
+    if (on != 0 && on != 1) return set_err(RG_EINVAL, "plan must be 0 or 1");
+    ctx->plan = on;
+    return RG_OK;
+}
+
+int rg_set_segments(rg_ctx *ctx, int k) {
+    if (!ctx) return set_err(RG_EINVAL, "null context");
+    if (k != 0 && k != 1 && k != 2 && k != 4) return set_err(RG_EINVAL, "segments must be 0, 1, 2 or 4");
+    ctx->segments = k;
     return RG_OK;
 }
 
@@ -236,36 +280,45 @@ static rg::Launch launch_cfg(rg_ctx *ctx, size_t n, bool open) {
     return L;
 }
 
-// Staged kernel residency: one 4-wave workgroup per CU handles 4 tiles of 64
-// packets at a time; a second resident workgroup (2 waves per SIMD) pays off
-// once every CU has at least two workgroups' worth of tiles.
-static int staged_wg_per_cu(rg_ctx *ctx, size_t n) {
-    if (ctx->wg_per_cu > 0) return ctx->wg_per_cu;
-    const size_t tiles = (n + 63) / 64;
-    const size_t wgs = (tiles + 3) / 4;
-    return wgs >= (size_t)ctx->cus * 2 ? 2 : 1;
+// Tile kernels: persistent grid of 4-wave workgroups, two resident per CU
+// (2 waves per SIMD: the VGPR budget of the kernel).  With the planner the
+// work lists and the per-class segment counts are built on the device; without
+// it packets stay in array order and the segment count follows from n.
+static hipError_t launch_tiles_any(rg_ctx *ctx, const rg::SealArgs *sa, const rg::OpenArgs *oa, PlanBuf &pb,
+                                   const rg::Launch &L0, hipStream_t st) {
+    const uint32_t n = sa ? sa->n : oa->n;
+    rg::Launch L = L0;
+    rg::TilePlan tp{};
+    tp.target_lanes = (uint32_t)std::max(1, ctx->cus) * 256u; // one wave per SIMD
+    tp.fixed_k = (uint32_t)ctx->segments;
+    if (ctx->plan) {
+        hipError_t e = pb.reserve(n);
+        if (e != hipSuccess) return e;
+        tp.counts = static_cast<uint32_t *>(pb.counts.p);
+        tp.lists = static_cast<uint32_t *>(pb.lists.p);
+        tp.cap = pb.cap;
+        e = rg::launch_plan(sa ? sa->desc : oa->desc, n, oa != nullptr, tp, st);
+        if (e != hipSuccess) return e;
+    } else if (!tp.fixed_k) {
+        tp.fixed_k = n >= tp.target_lanes ? 1u : 2ull * n >= tp.target_lanes ? 2u : 4u;
+    }
+    return rg::launch_tiles(sa, oa, L.staged_g, tp, L, st);
 }
 
-static hipError_t launch_seal_any(rg_ctx *ctx, const rg::SealArgs &a0, hipStream_t st) {
+static hipError_t launch_seal_any(rg_ctx *ctx, const rg::SealArgs &a0, PlanBuf &pb, hipStream_t st) {
     rg::SealArgs a = a0;
     a.dbg = ctx->debug_mode == 3 ? ctx->dbg : nullptr;
     rg::Launch L = launch_cfg(ctx, a.n, false);
-    if (L.staged_g > 0 && (L.debug_mode == 0 || L.debug_mode == 3)) {
-        L.wg_per_cu = staged_wg_per_cu(ctx, a.n);
-        return rg::launch_staged(&a, nullptr, L.staged_g, L, st);
-    }
+    if (L.staged_g > 0 && (L.debug_mode == 0 || L.debug_mode == 3)) return launch_tiles_any(ctx, &a, nullptr, pb, L, st);
     return rg::launch_seal(a, L, st);
 }
 
-static hipError_t launch_open_any(rg_ctx *ctx, const rg::OpenArgs &a0, hipStream_t st) {
+static hipError_t launch_open_any(rg_ctx *ctx, const rg::OpenArgs &a0, PlanBuf &pb, hipStream_t st) {
     rg::OpenArgs a = a0;
     a.dbg = ctx->debug_mode == 3 ? ctx->dbg : nullptr;
     rg::Launch L = launch_cfg(ctx, a.n, true);
     L.debug_mode = ctx->debug_mode == 3 ? 3 : 0;
-    if (L.staged_g > 0) {
-        L.wg_per_cu = staged_wg_per_cu(ctx, a.n);
-        return rg::launch_staged(nullptr, &a, L.staged_g, L, st);
-    }
+    if (L.staged_g > 0) return launch_tiles_any(ctx, nullptr, &a, pb, L, st);
     return rg::launch_open(a, L, st);
 }
 
@@ -288,7 +341,7 @@ int rg_seal_batch_dev(rg_ctx *ctx, const uint8_t *keys, const uint32_t *receiver
     a.status = status;
     a.nkeys = nkeys;
     a.n = (uint32_t)n;
-    RG_HIP(launch_seal_any(ctx, a, (hipStream_t)stream), "seal launch");
+    RG_HIP(launch_seal_any(ctx, a, ctx->plan_dev, (hipStream_t)stream), "seal launch");
     return RG_OK;
 }
 
@@ -308,7 +361,7 @@ int rg_open_batch_dev(rg_ctx *ctx, const uint8_t *keys, uint32_t nkeys, const rg
     a.counters_out = counters_out;
     a.nkeys = nkeys;
     a.n = (uint32_t)n;
-    RG_HIP(launch_open_any(ctx, a, (hipStream_t)stream), "open launch");
+    RG_HIP(launch_open_any(ctx, a, ctx->plan_dev, (hipStream_t)stream), "open launch");
     return RG_OK;
 }
 
@@ -424,7 +477,7 @@ int host_batch(rg_ctx *ctx, bool open, uint32_t nkeys, const rg_pkt_desc *desc, 
             a.status = static_cast<uint8_t *>(s.d_status.p);
             a.nkeys = nkeys;
             a.n = (uint32_t)m;
-            RG_HIP(launch_seal_any(ctx, a, st), "seal launch");
+            RG_HIP(launch_seal_any(ctx, a, s.plan, st), "seal launch");
         } else {
             RG_HIP(s.d_ctr_out.reserve(m * 8), "alloc ctr_out");
             RG_HIP(s.h_ctr_out.reserve(m * 8), "alloc h_ctr_out");
@@ -437,7 +490,7 @@ int host_batch(rg_ctx *ctx, bool open, uint32_t nkeys, const rg_pkt_desc *desc, 
             a.counters_out = static_cast<uint64_t *>(s.d_ctr_out.p);
             a.nkeys = nkeys;
             a.n = (uint32_t)m;
-            RG_HIP(launch_open_any(ctx, a, st), "open launch");
+            RG_HIP(launch_open_any(ctx, a, s.plan, st), "open launch");
             RG_HIP(hipMemcpyAsync(s.h_ctr_out.p, s.d_ctr_out.p, m * 8, hipMemcpyDeviceToHost, st), "D2H ctr");
         }
         if (span) RG_HIP(hipMemcpyAsync(buf + lo, s.d_buf.p, span, hipMemcpyDeviceToHost, st), "D2H frames");

@@ -198,6 +198,20 @@ __device__ __forceinline__ void stream_block_hooked(const Stream &st, uint32_t b
     out[15] = x15 + st.n2;
 }
 
+// key-table row idx (8 LE words)
+__device__ __forceinline__ Key8 load_key(const uint32_t *keys, uint32_t idx) {
+    const uint4 *kp = reinterpret_cast<const uint4 *>(keys + 8ull * idx);
+    uint4 a = kp[0], b = kp[1];
+    Key8 k;
+    k.k[0] = a.x; k.k[1] = a.y; k.k[2] = a.z; k.k[3] = a.w;
+    k.k[4] = b.x; k.k[5] = b.y; k.k[6] = b.z; k.k[7] = b.w;
+    return k;
+}
+
+__device__ __forceinline__ uint4 xor4(uint4 m, const uint32_t *ks) {
+    return make_uint4(m.x ^ ks[0], m.y ^ ks[1], m.z ^ ks[2], m.w ^ ks[3]);
+}
+
 // ---------------------------------------------------------------- Poly1305
 // Accumulator h = h0 + h1 2^32 + h2 2^64 + h3 2^96 + h4 2^128, h4 small (< 8).
 struct Acc {
@@ -387,6 +401,46 @@ __device__ __forceinline__ void acc_mul_gen(Acc &h, const Gen &G) {
     t = (t >> 32) + ((d4 & M) << 8);
     h.h3 = (uint32_t)t;
     h.h4 = (uint32_t)(t >> 32); // < 4
+}
+
+// h += o (both partially reduced), then fold h4 back below 5
+__device__ __forceinline__ void acc_add_acc(Acc &h, const Acc &o) {
+    uint32_t k;
+    h.h0 = addc(h.h0, o.h0, 0, k);
+    h.h1 = addc(h.h1, o.h1, k, k);
+    h.h2 = addc(h.h2, o.h2, k, k);
+    h.h3 = addc(h.h3, o.h3, k, k);
+    h.h4 = h.h4 + o.h4 + k;
+}
+
+// partial reduction: bits >= 130 folded back (2^130 == 5), h4 <= 4 on exit
+__device__ __forceinline__ void acc_fold(Acc &h) {
+    const uint32_t c = (h.h4 >> 2) + (h.h4 & ~3u);
+    uint32_t k;
+    h.h0 = addc(h.h0, c, 0, k);
+    h.h1 = addc(h.h1, 0, k, k);
+    h.h2 = addc(h.h2, 0, k, k);
+    h.h3 = addc(h.h3, 0, k, k);
+    h.h4 = (h.h4 & 3u) + k;
+}
+
+// r^e mod 2^130-5 for a per-lane exponent e < 2^bits (bits wave-uniform):
+// left-to-right square-and-multiply, squarings with the general multiplier,
+// the multiply by r with the clamped one; branch-free per lane.
+__device__ __forceinline__ Acc acc_pow(const Mul &r, uint32_t e, uint32_t bits) {
+    Acc x = {1, 0, 0, 0, 0};
+    for (int b = (int)bits - 1; b >= 0; --b) {
+        acc_mul_gen(x, make_gen(x));
+        Acc y = x;
+        acc_mul(y, r);
+        const bool take = (e >> b) & 1u;
+        x.h0 = take ? y.h0 : x.h0;
+        x.h1 = take ? y.h1 : x.h1;
+        x.h2 = take ? y.h2 : x.h2;
+        x.h3 = take ? y.h3 : x.h3;
+        x.h4 = take ? y.h4 : x.h4;
+    }
+    return x;
 }
 
 __device__ __forceinline__ uint64_t mix64(uint64_t x) {

@@ -61,11 +61,25 @@ struct Launch {
 };
 constexpr uint32_t kLdsPerCu = 160u * 1024u;
 
+// Size-class work lists built by the planner (rg_tile.hip).  counts == nullptr:
+// identity order (packet i in tile i / 64), one segment count fixed_k for all.
+constexpr uint32_t kClasses = 37;
+struct TilePlan {
+    const uint32_t *counts; // [kClasses] packets per class, then [kClasses] = finished-workgroup count
+    const uint32_t *lists;  // [kClasses][cap] packet indices
+    uint32_t cap;
+    uint32_t target_lanes; // segment sizing: aim for this many busy lanes (0 = no splitting)
+    uint32_t fixed_k;      // 0 = per class from the counts, else 1 / 2 / 4 segments for every packet
+    uint32_t pad_;
+};
+
 hipError_t launch_seal(const SealArgs &a, const Launch &L, hipStream_t s);
 hipError_t launch_open(const OpenArgs &a, const Launch &L, hipStream_t s);
-// LDS-staged tile kernel (one packet per lane, coalesced LDS-DMA windows of G chunks);
-// exactly one of sa / oa is non-null
-hipError_t launch_staged(const SealArgs *sa, const OpenArgs *oa, int G, const Launch &L, hipStream_t s);
+// Planner + LDS-staged tile kernel (rg_tile.hip); exactly one of sa / oa is non-null.
+hipError_t launch_plan(const rg_pkt_desc *desc, uint32_t n, bool open, const TilePlan &tp, hipStream_t s);
+hipError_t launch_tiles(const SealArgs *sa, const OpenArgs *oa, int G, const TilePlan &tp, const Launch &L,
+                        hipStream_t s);
+hipError_t prepare_tile_kernels();
 // sets the dynamic-LDS attribute and returns max resident workgroups per CU
 // for [seal, open][K = 1, 2, 4]
 hipError_t prepare_kernels(int max_wg[2][3]);

@@ -13,19 +13,6 @@
 
 namespace rg {
 
-__device__ __forceinline__ Key8 load_key(const uint32_t *keys, uint32_t idx) {
-    const uint4 *kp = reinterpret_cast<const uint4 *>(keys + 8ull * idx);
-    uint4 a = kp[0], b = kp[1];
-    Key8 k;
-    k.k[0] = a.x; k.k[1] = a.y; k.k[2] = a.z; k.k[3] = a.w;
-    k.k[4] = b.x; k.k[5] = b.y; k.k[6] = b.z; k.k[7] = b.w;
-    return k;
-}
-
-__device__ __forceinline__ uint4 xor4(uint4 m, const uint32_t *ks) {
-    return make_uint4(m.x ^ ks[0], m.y ^ ks[1], m.z ^ ks[2], m.w ^ ks[3]);
-}
-
 // ------------------------------------------------------------ K lanes
 // K lanes cooperate on one packet (K = 1, 2, 4; groups never straddle a
 // wave).  Payload chunk c (64 B, keystream block c+1) belongs to lane
@@ -336,371 +323,6 @@ template <int K> __global__ __launch_bounds__(256) void open_kernel(OpenArgs a) 
     for (uint32_t i = blockIdx.x * per_block + threadIdx.x / K; i < a.n; i += stride) open_packet<K>(a, i, j);
 }
 
-// ------------------------------------------------------ LDS-staged tiles
-// One wave owns a tile of 64 packets, one packet per lane (serial Horner with
-// the clamped r: the cheapest Poly1305 chain).  Payload moves HBM <-> LDS in
-// windows of G chunks per packet with coalesced wave-wide transfers:
-//
-//   * LDS-DMA (buffer_load_dwordx4 ... lds): instruction i reads the windows
-//     of 64/PPW packets, PPW = 4G lanes per packet each fetching one 16-byte
-//     piece, i.e. whole contiguous 64G-byte runs.  The LDS image is
-//     lane-linear, slot(p, pos) = p*PPW + pos, and the XOR swizzle goes on the
-//     SOURCE side (piece k = pos ^ f(p)) so that the per-packet ds_read_b128
-//     of one piece by 64 lanes is bank-conflict free.
-//   * compute: lane p reads its chunk's 4 pieces, XORs the keystream, writes
-//     the result back to the same slots and MACs the ciphertext;
-//   * write-back: lane l reads slot 64i+l (linear) and buffer_store's it to the
-//     same address the DMA read it from.
-//
-// Pieces past a packet's payload get an out-of-range buffer offset: the
-// descriptor's range check turns such a load into zeros and drops such a
-// store, so every wave issues exactly PPW DMA + PPW store instructions per
-// window and the vmcnt waits below are exact.  Windows are double-buffered:
-// the DMA of window w+1 overlaps the keystream work on window w.
-constexpr uint32_t kOOB = 0xFFFFFFF0u;
-
-typedef int v4i __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ v4i make_rsrc(const uint8_t *base, uint32_t num_records) {
-    const uint64_t a = (uint64_t)base;
-    v4i r;
-    r.x = __builtin_amdgcn_readfirstlane((int)(uint32_t)a);
-    r.y = __builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32)); // stride 0
-    r.z = __builtin_amdgcn_readfirstlane((int)num_records);
-    r.w = 0x00020000; // raw buffer, 32-bit data format (gfx9 family)
-    return r;
-}
-
-// one LDS-DMA wave-instruction: 16 bytes per lane to lds_byte + 16 * lane
-__device__ __forceinline__ void dma16(const v4i &rsrc, uint32_t voff, uint32_t lds_byte) {
-    uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\t"
-                 "s_mov_b32 m0, %3\n\t"
-                 "s_nop 0\n\t"
-                 "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
-                 "s_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(voff), "s"(rsrc), "s"(lds_byte)
-                 : "memory");
-}
-
-typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ void store16(const v4i &rsrc, uint32_t voff, const uint4 &v) {
-    v4u d;
-    d.x = v.x;
-    d.y = v.y;
-    d.z = v.z;
-    d.w = v.w;
-    asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen\n\t"
-                 "s_nop 1"
-                 :
-                 : "v"(d), "v"(voff), "s"(rsrc)
-                 : "memory");
-}
-
-template <int N> __device__ __forceinline__ void wait_vm() {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-template <int G> struct StagedCfg {
-    static constexpr uint32_t PPW = 4 * G;            // 16-byte pieces per packet per window
-    static constexpr uint32_t PKT_PER_INST = 64 / PPW; // packets covered by one DMA instruction
-    static constexpr uint32_t BUF = 64 * PPW * 16;     // bytes per window buffer per wave
-    static constexpr uint32_t WAVE_LDS = 2 * BUF;      // double-buffered
-};
-
-// swizzle: makes slot(p, k ^ f(p)) distinct mod 16 over each ds_read_b128 lane group
-template <int G> __device__ __forceinline__ uint32_t swz(uint32_t p) {
-    constexpr uint32_t PPW = StagedCfg<G>::PPW;
-    return (p / (16 / PPW)) % PPW;
-}
-
-// diagnostic-build stamp (STAMP kernels only): shader-clock cycles, SGPR result
-__device__ __forceinline__ uint64_t stamp() {
-    uint64_t t;
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-    return t;
-}
-
-template <int G, bool OPEN, bool STAMP = false>
-__global__ __launch_bounds__(256) void staged_kernel(SealArgs sa, OpenArgs oa) {
-    uint64_t t_setup = 0, t_store = 0, t_issue = 0, t_wait = 0, t_chunk = 0, t_tail = 0, t_mark = 0;
-    if constexpr (STAMP) t_mark = stamp();
-    using Cfg = StagedCfg<G>;
-    constexpr uint32_t PPW = Cfg::PPW;
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds_raw[];
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t wave = threadIdx.x >> 6;
-    const uint32_t n = OPEN ? oa.n : sa.n;
-    const uint32_t ntiles = (n + 63) / 64;
-    const uint32_t nwaves = gridDim.x * 4;
-    uint8_t *const buf = OPEN ? oa.buf : sa.buf;
-    const uint64_t buf_len = OPEN ? oa.buf_len : sa.buf_len;
-    const uint32_t lds_wave = (uint32_t)(uintptr_t)(lds_raw) + wave * Cfg::WAVE_LDS;
-    uint4 *const lds4 = reinterpret_cast<uint4 *>(lds_raw + wave * Cfg::WAVE_LDS);
-
-    for (uint32_t tile = blockIdx.x * 4 + wave; tile < ntiles; tile += nwaves) {
-        if constexpr (STAMP) {
-            const uint64_t t = stamp();
-            t_tail += t - t_mark;
-            t_mark = t;
-        }
-        const uint32_t i = tile * 64 + lane;
-        // ---- per-lane packet setup (one packet per lane)
-        bool live = i < n;
-        rg_pkt_desc d = {0, 0, 0};
-        if (live) d = OPEN ? oa.desc[i] : sa.desc[i];
-        uint8_t st = 0xFF;
-        uint32_t P = 0;
-        uint64_t ctr = 0;
-        if (live) {
-            if constexpr (!OPEN) {
-                P = d.len;
-                const bool ok = d.key_idx < sa.nkeys && (P & 15u) == 0 && (d.offset & 15u) == 0 &&
-                                P <= kMaxPayload && d.offset <= buf_len && P + 32 <= buf_len - d.offset;
-                if (!ok) st = d.key_idx == RG_KEY_SKIP ? RG_PKT_REJECTED : RG_PKT_INVALID;
-                else ctr = sa.counters[i];
-            } else {
-                const uint32_t W = d.len;
-                if (d.key_idx == RG_KEY_SKIP) st = RG_PKT_REJECTED;
-                else if ((d.offset & 15u) != 0) st = RG_PKT_UNALIGNED;
-                else if (d.key_idx >= oa.nkeys || W > kMaxPayload + 32 || d.offset > buf_len ||
-                         W > buf_len - d.offset || W < 4)
-                    st = RG_PKT_INVALID;
-                if (st == 0xFF) {
-                    const uint4 hdr = *reinterpret_cast<const uint4 *>(buf + d.offset);
-                    if (hdr.x != 4u) st = RG_PKT_NOT_DATA;
-                    else if ((W & 15u) != 0 || W < 16) st = RG_PKT_INVALID;
-                    else {
-                        ctr = ((uint64_t)hdr.w << 32) | hdr.z;
-                        if (W < 32) st = RG_PKT_DECRYPT_ERR;
-                    }
-                }
-                if (st == 0xFF) P = W - 32;
-            }
-        }
-        const bool work = live && st == 0xFF;
-        const uint32_t nb = work ? P >> 4 : 0; // 16-byte blocks of this lane's packet
-        const uint32_t C = (nb + 3) >> 2;      // 64-byte chunks
-        // ---- tile addressing: buffer descriptor based at the lowest frame of the tile
-        uint64_t lo = work ? d.offset : ~0ull;
-#pragma unroll
-        for (int m = 32; m >= 1; m >>= 1) {
-            const uint64_t o = __shfl_xor(lo, m);
-            lo = o < lo ? o : lo;
-        }
-        lo = uniform_u64(lo);
-        if (lo == ~0ull) lo = 0;
-        const uint64_t span_cap = buf_len - lo;
-        const uint32_t nrec = span_cap > kOOB ? kOOB : (uint32_t)span_cap;
-        const v4i rsrc = make_rsrc(buf + lo, nrec);
-        // payload base of this lane's packet relative to the descriptor (kOOB if unusable)
-        uint32_t my_base = kOOB;
-        if (work && d.offset - lo + 16 + (uint64_t)P <= nrec) my_base = (uint32_t)(d.offset - lo) + 16;
-        const uint32_t myC = my_base == kOOB ? 0 : C;
-        // windows for the whole wave (uniform)
-        uint32_t Wl = (myC + G - 1) / G;
-#pragma unroll
-        for (int m = 32; m >= 1; m >>= 1) {
-            const uint32_t o = __shfl_xor(Wl, m);
-            Wl = o > Wl ? o : Wl;
-        }
-        const uint32_t W = uniform_u32(Wl);
-        // DMA/store address table: instruction q serves packet pq = q*PKT_PER_INST + lane/PPW,
-        // piece k = (lane % PPW) ^ swz(pq)
-        uint32_t tb[PPW], tlim[PPW];
-#pragma unroll
-        for (uint32_t q = 0; q < PPW; ++q) {
-            const uint32_t pq = q * Cfg::PKT_PER_INST + lane / PPW;
-            const uint32_t k = (lane % PPW) ^ swz<G>(pq);
-            const uint32_t b = __shfl(my_base, pq);
-            const uint32_t blocks = __shfl(myC == 0 ? 0u : nb, pq);
-            tb[q] = b == kOOB ? kOOB : b + 16 * k;
-            tlim[q] = blocks > k ? blocks - k : 0; // piece valid in window w iff w*PPW < tlim
-        }
-        // ---- keys, one-time key
-        const uint32_t n1 = (uint32_t)ctr, n2 = (uint32_t)(ctr >> 32);
-        const Key8 key = load_key(OPEN ? oa.keys : sa.keys, work ? d.key_idx : 0u);
-        const Stream stm = make_stream(key, 0u, n1, n2);
-        uint32_t ks[16];
-        stream_block(stm, 0, ks);
-        const Mul r = make_mul(ks[0], ks[1], ks[2], ks[3]);
-        const uint32_t s0 = ks[4], s1 = ks[5], s2 = ks[6], s3 = ks[7];
-        Acc acc = {0, 0, 0, 0, 0};
-
-        // ---- chunk loop, software-pipelined: the keystream block of chunk c+1
-        // is generated in the same basic block as the Poly1305 of chunk c, so
-        // the two independent dependency chains interleave.
-        auto voff_of = [&](uint32_t q, uint32_t w) -> uint32_t {
-            return (tb[q] != kOOB && w * PPW < tlim[q]) ? tb[q] + w * PPW * 16 : kOOB;
-        };
-        auto issue_dma = [&](uint32_t w) {
-            const uint32_t lbase = lds_wave + (w & 1) * Cfg::BUF;
-#pragma unroll
-            for (uint32_t q = 0; q < PPW; ++q) dma16(rsrc, voff_of(q, w), __builtin_amdgcn_readfirstlane(lbase + q * 1024));
-        };
-        auto store_window = [&](uint32_t w) {
-            const uint4 *win = lds4 + (w & 1) * (Cfg::BUF / 16);
-            // all LDS reads first (one lgkmcnt wait), then the coalesced stores
-            uint4 v[PPW];
-#pragma unroll
-            for (uint32_t q = 0; q < PPW; ++q) v[q] = win[q * 64 + lane];
-#pragma unroll
-            for (uint32_t q = 0; q < PPW; ++q) store16(rsrc, voff_of(q, w), v[q]);
-        };
-        if constexpr (STAMP) {
-            const uint64_t t = stamp();
-            t_setup += t - t_mark;
-            t_mark = t;
-        }
-        const uint32_t Cmax = W * G; // wave-uniform chunk count (multiple of G)
-        const uint32_t f = swz<G>(lane);
-        uint32_t ksc[16];
-        stream_block(stm, 1, ksc);
-        for (uint32_t c = 0; c < Cmax; ++c) {
-            const uint32_t w = c / G, cl = c % G;
-            if (cl == 0) { // window boundary (wave-uniform)
-                if constexpr (STAMP) {
-                    const uint64_t t = stamp();
-                    t_chunk += t - t_mark;
-                    t_mark = t;
-                }
-                if (w > 0) store_window(w - 1);
-                if constexpr (STAMP) {
-                    const uint64_t t = stamp();
-                    t_store += t - t_mark;
-                    t_mark = t;
-                }
-                const bool more = w + 1 < W;
-                if (w == 0) {
-                    issue_dma(0);
-                    if (more) issue_dma(1);
-                } else if (more) {
-                    issue_dma(w + 1);
-                }
-                if constexpr (STAMP) {
-                    const uint64_t t = stamp();
-                    t_issue += t - t_mark;
-                    t_mark = t;
-                }
-                if (w == 0) {
-                    if (more) wait_vm<PPW>();
-                    else wait_vm<0>();
-                } else {
-                    // wait for DMA(w); younger: stores(w-1) and DMA(w+1)
-                    if (more) wait_vm<2 * PPW>();
-                    else wait_vm<PPW>();
-                }
-                if constexpr (STAMP) {
-                    const uint64_t t = stamp();
-                    t_wait += t - t_mark;
-                    t_mark = t;
-                }
-            }
-            uint4 *win = lds4 + (w & 1) * (Cfg::BUF / 16);
-            // blocks of this chunk that belong to the lane's payload (0..4)
-            const uint32_t cnt = c < myC ? (nb - 4 * c < 4 ? nb - 4 * c : 4) : 0;
-            const uint32_t sl0 = lane * PPW + ((4 * cl + 0) ^ f);
-            const uint32_t sl1 = lane * PPW + ((4 * cl + 1) ^ f);
-            const uint32_t sl2 = lane * PPW + ((4 * cl + 2) ^ f);
-            const uint32_t sl3 = lane * PPW + ((4 * cl + 3) ^ f);
-            const uint4 m0 = win[sl0], m1 = win[sl1], m2 = win[sl2], m3 = win[sl3];
-            // The LDS reads land while the first ChaCha rounds of the next block
-            // run: XOR + write-back sit in the hook after double round 0, the
-            // four Poly1305 blocks after double rounds 1, 3, 5 and 7.
-            uint4 x0, x1, x2, x3;
-            uint32_t ksn[16];
-            stream_block_hooked(stm, c + 2, ksn, [&](int dr) {
-                if (dr == 0) {
-                    x0 = xor4(m0, ksc + 0);
-                    x1 = xor4(m1, ksc + 4);
-                    x2 = xor4(m2, ksc + 8);
-                    x3 = xor4(m3, ksc + 12);
-                    // unconditional: pieces outside the payload are never stored
-                    // (their buffer offsets are out of range)
-                    win[sl0] = x0;
-                    win[sl1] = x1;
-                    win[sl2] = x2;
-                    win[sl3] = x3;
-                }
-                if (dr == 1) acc_block_pred(acc, OPEN ? m0 : x0, r, cnt > 0);
-                if (dr == 3) acc_block_pred(acc, OPEN ? m1 : x1, r, cnt > 1);
-                if (dr == 5) acc_block_pred(acc, OPEN ? m2 : x2, r, cnt > 2);
-                if (dr == 7) acc_block_pred(acc, OPEN ? m3 : x3, r, cnt > 3);
-                if (dr % 2 == 1) pin_acc(acc);
-            });
-#pragma unroll
-            for (int t = 0; t < 16; ++t) ksc[t] = ksn[t];
-        }
-        if constexpr (STAMP) {
-            const uint64_t t = stamp();
-            t_chunk += t - t_mark;
-            t_mark = t;
-        }
-        if (W > 0) store_window(W - 1);
-        wait_vm<0>(); // drain this tile's stores before the per-packet tail touches the frames
-        if (!live) continue;
-        uint8_t *frame = buf + d.offset;
-        if (st != 0xFF) {
-            if constexpr (!OPEN) {
-                if (sa.status) sa.status[i] = st;
-            } else {
-                oa.status[i] = st;
-                if (oa.counters_out) oa.counters_out[i] = ctr;
-            }
-            continue;
-        }
-        if (my_base == kOOB) { // tile span too large for a 32-bit buffer offset (not produced by rg_* callers)
-            if constexpr (!OPEN) {
-                if (sa.status) sa.status[i] = RG_PKT_INVALID;
-            } else {
-                oa.status[i] = RG_PKT_INVALID;
-            }
-            continue;
-        }
-        // h = acc * r  (multiply-then-add form closes with one more r), length block, finish
-        acc_add(acc, 0, 0, P, 0, 1);
-        acc_mul(acc, r);
-        uint32_t tag[4];
-        acc_finish(acc, s0, s1, s2, s3, tag);
-        if constexpr (!OPEN) {
-            if (sa.receivers) *reinterpret_cast<uint4 *>(frame) = make_uint4(4u, sa.receivers[d.key_idx], n1, n2);
-            *reinterpret_cast<uint4 *>(frame + 16 + P) = make_uint4(tag[0], tag[1], tag[2], tag[3]);
-            if (sa.status) sa.status[i] = RG_PKT_OK;
-        } else {
-            const uint4 want = *reinterpret_cast<const uint4 *>(frame + 16 + P);
-            const uint32_t diff = (tag[0] ^ want.x) | (tag[1] ^ want.y) | (tag[2] ^ want.z) | (tag[3] ^ want.w);
-            if (diff != 0) {
-                // forged/corrupt: re-apply the keystream so the frame is left unchanged
-                uint4 *pl = reinterpret_cast<uint4 *>(frame + 16);
-                for (uint32_t c = 0; 4 * c < nb; ++c) {
-                    const uint32_t cnt = nb - 4 * c < 4 ? nb - 4 * c : 4;
-                    stream_block(stm, c + 1, ks);
-                    for (uint32_t q = 0; q < cnt; ++q) pl[4 * c + q] = xor4(pl[4 * c + q], ks + 4 * q);
-                }
-            }
-            oa.status[i] = diff == 0 ? RG_PKT_OK : RG_PKT_DECRYPT_ERR;
-            if (oa.counters_out) oa.counters_out[i] = ctr;
-        }
-    }
-    if constexpr (STAMP) {
-        const uint64_t t = stamp();
-        t_tail += t - t_mark;
-        uint64_t *dbg = OPEN ? oa.dbg : sa.dbg;
-        if (dbg && lane == 0) {
-            uint64_t *o = dbg + 8 * (blockIdx.x * 4 + wave);
-            o[0] = t_setup;
-            o[1] = t_store;
-            o[2] = t_issue;
-            o[3] = t_wait;
-            o[4] = t_chunk;
-            o[5] = t_tail;
-            o[6] = 1;
-        }
-    }
-}
-
 // --------------------------------------------------------------- general
 // One lane per message, byte-granular: any nonce, any AAD, any length.  Used
 // by the per-message CryptoPrimatives drop-in (handshake-sized messages).
@@ -816,50 +438,7 @@ hipError_t launch_open(const OpenArgs &a, const Launch &L, hipStream_t s) {
     return launch_k<OpenArgs, open_kernel<1>, open_kernel<2>, open_kernel<4>>(a, L, s);
 }
 
-template <int G> static uint32_t staged_lds_per_wg() { return 4 * StagedCfg<G>::WAVE_LDS; }
-
-hipError_t launch_staged(const SealArgs *sa, const OpenArgs *oa, int G, const Launch &L, hipStream_t s) {
-    const uint32_t n = sa ? sa->n : oa->n;
-    if (n == 0) return hipSuccess;
-    SealArgs a = sa ? *sa : SealArgs{};
-    OpenArgs b = oa ? *oa : OpenArgs{};
-    const uint64_t tiles = (n + 63) / 64;
-    const uint64_t want = (tiles + 3) / 4;
-    const int wpc = L.wg_per_cu > 0 ? L.wg_per_cu : 1;
-    const uint64_t cap = (uint64_t)L.cus * wpc;
-    const uint32_t blocks = (uint32_t)(want < cap || cap == 0 ? want : cap);
-    uint32_t need = G == 1 ? staged_lds_per_wg<1>() : G == 2 ? staged_lds_per_wg<2>() : staged_lds_per_wg<4>();
-    uint32_t lds = (kLdsPerCu / wpc) & ~255u;
-    if (lds < need) lds = need;
-    if (lds > kLdsPerCu) return hipErrorInvalidValue;
-#define RG_STAGED(GG)                                                                                  \
-    if (L.debug_mode == 3) {                                                                           \
-        if (sa) hipLaunchKernelGGL((staged_kernel<GG, false, true>), dim3(blocks), dim3(256), lds, s, a, b); \
-        else hipLaunchKernelGGL((staged_kernel<GG, true, true>), dim3(blocks), dim3(256), lds, s, a, b);     \
-    } else if (sa) hipLaunchKernelGGL((staged_kernel<GG, false>), dim3(blocks), dim3(256), lds, s, a, b); \
-    else hipLaunchKernelGGL((staged_kernel<GG, true>), dim3(blocks), dim3(256), lds, s, a, b);
-    switch (G) {
-    case 1: RG_STAGED(1) break;
-    case 2: RG_STAGED(2) break;
-    case 4: RG_STAGED(4) break;
-    default: return hipErrorInvalidValue;
-    }
-#undef RG_STAGED
-    return hipGetLastError();
-}
-
 hipError_t prepare_kernels(int lanes_max_wg[2][3]) {
-    {
-        void *fs[12] = {(void *)staged_kernel<1, false>, (void *)staged_kernel<2, false>, (void *)staged_kernel<4, false>,
-                        (void *)staged_kernel<1, true>,  (void *)staged_kernel<2, true>,  (void *)staged_kernel<4, true>,
-                        (void *)staged_kernel<1, false, true>, (void *)staged_kernel<2, false, true>,
-                        (void *)staged_kernel<4, false, true>, (void *)staged_kernel<1, true, true>,
-                        (void *)staged_kernel<2, true, true>,  (void *)staged_kernel<4, true, true>};
-        for (void *f : fs) {
-            hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsPerCu);
-            if (e != hipSuccess) return e;
-        }
-    }
     // allow up to the whole 160 KiB LDS as dynamic shared memory, and report
     // how many 256-thread workgroups of each kernel fit on a CU (VGPR bound)
     void *seal[3] = {(void *)seal_kernel<1>, (void *)seal_kernel<2>, (void *)seal_kernel<4>};

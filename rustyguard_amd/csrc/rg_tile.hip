@@ -1,0 +1,709 @@
+// rg_tile.hip -- the batched transport kernels (default path of
+// rg_{seal,open}_batch_*): a size-bucketing planner and the LDS-staged tile
+// kernel.  Replaces N x Core::chacha20poly1305_{enc,dec}
+// (rustyguard-crypto/src/prim.rs:179-201) as driven by EncryptionKey::encrypt
+// / DecryptionKey::decrypt (prim.rs:386-437) for WireGuard data packets.
+//
+// Planner (plan_kernel): every packet is put in the work list of its size
+// class (its number of 64-byte chunks, exact up to 16, then 1.5x steps), so
+// the tile kernel can build tiles of equally long packets: a 64-packet tile
+// runs as long as its longest packet.
+//
+// Tile kernel (tile_kernel<G, OPEN>): a 256-thread workgroup (4 waves) takes
+// one "group" at a time: 4 tiles of 64 packets (K = 1), 2 tiles each split
+// into 2 contiguous segments on 2 waves (K = 2), or 1 tile split into 4
+// segments (K = 4).  The class -> K choice comes from the class counts alone
+// (target: about two waves per SIMD of work), every workgroup derives the
+// same schedule from them.  Within a wave, lane l owns (a segment of) packet
+// l of the tile and keeps its ChaCha state and Poly1305 accumulator in VGPRs;
+// payload moves HBM -> LDS -> HBM in double-buffered windows of G chunks per
+// lane with coalesced LDS-DMA loads and buffer stores (see StagedCfg).
+//
+// Segments: segment j of a packet covers chunks [jL, min(C, (j+1)L)),
+// L = ceil(C/K), keystream blocks from jL + 1; its lane runs its own Horner
+// chain A_j over its blocks.  With N_j = blocks after segment j,
+//   h = sum_j A_j r^{N_j}   (RFC 8439 Poly1305 of the whole ciphertext),
+// so each segment multiplies by r^{N_j} (acc_pow) and the sums meet in LDS.
+#include "rg_device.h"
+#include "rg_internal.h"
+
+namespace rg {
+
+// ------------------------------------------------------------ size classes
+// class c: c chunks for c <= 16; above, upper bounds 24, 32, 48, 64, ..., 16384
+__host__ __device__ __forceinline__ uint32_t class_hi(uint32_t c) {
+    if (c <= 16) return c;
+    const uint32_t j = c - 17;
+    return (j & 1u) ? (1u << (j / 2 + 5)) : (3u << (j / 2 + 3));
+}
+
+__device__ __forceinline__ uint32_t class_of(uint32_t chunks) {
+    if (chunks <= 16) return chunks;
+    uint32_t c = 17;
+    while (c < kClasses - 1 && class_hi(c) < chunks) ++c;
+    return c;
+}
+
+// Each workgroup classifies kPlanPer x 256 consecutive packets: per wave and
+// class one ballot -> one LDS atomic (runs of consecutive packets stay
+// together), then one global atomic per class and workgroup.  Uniform batches
+// therefore keep tiles of 64 consecutive frames.
+constexpr uint32_t kPlanPer = 2;
+
+__global__ __launch_bounds__(256) void plan_kernel(const rg_pkt_desc *desc, uint32_t n, uint32_t open,
+                                                   uint32_t *counts, uint32_t *lists, uint32_t cap) {
+    __shared__ uint32_t hist[kClasses];
+    __shared__ uint32_t gbase[kClasses];
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    if (tid < kClasses) hist[tid] = 0;
+    __syncthreads();
+    const uint32_t first = blockIdx.x * 256 * kPlanPer;
+    uint32_t cls[kPlanPer], rank[kPlanPer];
+#pragma unroll
+    for (uint32_t k = 0; k < kPlanPer; ++k) {
+        const uint32_t i = first + k * 256 + tid;
+        uint32_t c = ~0u;
+        if (i < n) {
+            const uint32_t len = desc[i].len;
+            uint32_t P = open ? (len >= 32 ? len - 32 : 0) : len;
+            if (P > kMaxPayload) P = 0;
+            c = class_of((P + 63) / 64);
+        }
+        cls[k] = c;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < kPlanPer; ++k) {
+        uint32_t c = cls[k], r = 0;
+        uint64_t pending = __ballot(c != ~0u);
+        while (pending) {
+            const int leader = __ffsll((unsigned long long)pending) - 1;
+            const uint32_t b = __shfl(c, leader);
+            const uint64_t m = __ballot(c == b);
+            uint32_t base = 0;
+            if ((int)lane == leader) base = atomicAdd(&hist[b], (uint32_t)__popcll(m));
+            base = __shfl(base, leader);
+            if (c == b) r = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+            pending &= ~m;
+        }
+        rank[k] = r;
+    }
+    __syncthreads();
+    if (tid < kClasses) gbase[tid] = hist[tid] ? atomicAdd(&counts[tid], hist[tid]) : 0u;
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < kPlanPer; ++k) {
+        if (cls[k] != ~0u) lists[(uint64_t)cls[k] * cap + gbase[cls[k]] + rank[k]] = first + k * 256 + tid;
+    }
+}
+
+// ------------------------------------------------------------ LDS-DMA helpers
+// Pieces past a payload get an out-of-range buffer offset: the descriptor's
+// range check turns such a load into zeros and drops such a store, so every
+// wave issues exactly PPW DMA + PPW store instructions per window and the
+// vmcnt waits are exact.
+constexpr uint32_t kOOB = 0xFFFFFFF0u;
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ v4i make_rsrc(const uint8_t *base, uint32_t num_records) {
+    const uint64_t a = (uint64_t)base;
+    v4i r;
+    r.x = (int)uniform_u32((uint32_t)a);
+    r.y = (int)uniform_u32((uint32_t)(a >> 32)); // stride 0
+    r.z = (int)uniform_u32(num_records);
+    r.w = 0x00020000; // raw buffer, 32-bit data format (gfx9 family)
+    return r;
+}
+
+// one LDS-DMA wave-instruction: 16 bytes per lane to lds_byte + 16 * lane
+__device__ __forceinline__ void dma16(const v4i &rsrc, uint32_t voff, uint32_t lds_byte) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\t"
+                 "s_mov_b32 m0, %3\n\t"
+                 "s_nop 0\n\t"
+                 "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+                 "s_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(voff), "s"(rsrc), "s"(lds_byte)
+                 : "memory");
+}
+
+__device__ __forceinline__ void store16(const v4i &rsrc, uint32_t voff, const uint4 &v) {
+    v4u d;
+    d.x = v.x;
+    d.y = v.y;
+    d.z = v.z;
+    d.w = v.w;
+    asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen\n\t"
+                 "s_nop 1"
+                 :
+                 : "v"(d), "v"(voff), "s"(rsrc)
+                 : "memory");
+}
+
+template <int N> __device__ __forceinline__ void wait_vm() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Window geometry: PPW 16-byte pieces per lane per window; DMA instruction q
+// serves packets q*PKT_PER_INST .. +PKT_PER_INST-1, PPW lanes per packet, one
+// whole contiguous 64G-byte run each (coalesced).  The LDS image is
+// lane-linear, slot(p, pos) = p*PPW + pos, and an XOR swizzle on the SOURCE
+// side (piece k = pos ^ swz(p)) makes the per-lane ds_read_b128 of one piece
+// by 64 lanes bank-conflict free.
+template <int G> struct StagedCfg {
+    static constexpr uint32_t PPW = 4 * G;
+    static constexpr uint32_t PKT_PER_INST = 64 / PPW;
+    static constexpr uint32_t BUF = 64 * PPW * 16;  // bytes per window buffer per wave
+    static constexpr uint32_t WAVE_LDS = 2 * BUF;   // double-buffered
+    static constexpr uint32_t COMB = 8 * 6 * 64 * 4; // segment hand-off slots, one per wave
+    static constexpr uint32_t FLAGS = 2 * 8 * 4;     // ready / ack generation per wave slot
+    static constexpr uint32_t WG_LDS = 8 * WAVE_LDS + COMB + FLAGS;
+};
+
+template <int G> __device__ __forceinline__ uint32_t swz(uint32_t p) {
+    constexpr uint32_t PPW = StagedCfg<G>::PPW;
+    return (p / (16 / PPW)) % PPW;
+}
+
+// diagnostic-build stamps (STAMP kernels only)
+__device__ __forceinline__ uint64_t stamp() {
+    uint64_t t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+}
+__device__ __forceinline__ uint64_t realtime() { // 100 MHz constant clock
+    uint64_t t;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+}
+
+constexpr uint32_t kMinSegment = 4;
+
+__device__ __forceinline__ uint32_t pow2ceil(uint32_t x) { return x <= 1 ? 1u : 1u << (32 - __clz(x - 1)); }
+
+// ------------------------------------------------------------ schedule
+// Lane p of every wave describes bucket p of the processing order (largest
+// class first).  Identical in every wave of the grid.
+struct Sched {
+    uint32_t cls, cnt, K, g_end; // this lane's bucket
+    uint32_t total_groups;
+};
+
+__device__ __forceinline__ Sched make_sched(const TilePlan &tp, uint32_t n) {
+    const uint32_t p = threadIdx.x & 63;
+    Sched s;
+    s.cls = 0;
+    s.cnt = 0;
+    s.K = 1;
+    uint32_t crep = 0;
+    if (tp.counts) {
+        if (p < kClasses) {
+            s.cls = kClasses - 1 - p;
+            s.cnt = tp.counts[s.cls];
+            crep = class_hi(s.cls);
+        }
+    } else if (p == 0) {
+        s.cnt = n; // identity order: one bucket, K fixed by the host
+    }
+    // chunk total -> target segment length T, then K per class
+    uint64_t tot = (uint64_t)s.cnt * crep;
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) tot += __shfl_xor(tot, m);
+    if (tp.counts) {
+        if (tp.fixed_k) {
+            s.K = tp.fixed_k;
+        } else {
+            // segment length: the chunk total spread over target_lanes, never
+            // below kMinSegment chunks (each segment pays a key block and r^N)
+            const uint64_t tl = tp.target_lanes ? tp.target_lanes : 1;
+            uint32_t T = (uint32_t)((tot + tl - 1) / tl);
+            if (T < kMinSegment) T = kMinSegment;
+            const uint32_t want = (crep + T - 1) / T;
+            s.K = want >= 4 ? 4u : pow2ceil(want);
+        }
+    } else {
+        s.K = tp.fixed_k ? tp.fixed_k : 1u;
+    }
+    const uint32_t tiles = (s.cnt + 63) / 64;
+    const uint32_t groups = (tiles * s.K + 3) / 4;
+    // inclusive prefix over lanes
+    uint32_t x = groups;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d);
+        if ((int)p >= d) x += y;
+    }
+    s.g_end = x;
+    s.total_groups = uniform_u32(__shfl(x, 63));
+    return s;
+}
+
+// ------------------------------------------------------------ tile kernel
+template <int G, bool OPEN, bool STAMP = false>
+__global__ __launch_bounds__(512) void tile_kernel(SealArgs sa, OpenArgs oa, TilePlan tp) {
+    using Cfg = StagedCfg<G>;
+    constexpr uint32_t PPW = Cfg::PPW;
+    uint64_t t_setup = 0, t_store = 0, t_issue = 0, t_wait = 0, t_chunk = 0, t_tail = 0, t_mark = 0, rt0 = 0;
+    if constexpr (STAMP) {
+        rt0 = realtime();
+        t_mark = stamp();
+    }
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds_raw[];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = threadIdx.x >> 6; // 0..7
+    const uint32_t half = wave >> 2;        // two independent 4-wave halves
+    const uint32_t hw = wave & 3;           // wave within the half
+    const uint32_t n = OPEN ? oa.n : sa.n;
+    uint8_t *const buf = OPEN ? oa.buf : sa.buf;
+    const uint64_t buf_len = OPEN ? oa.buf_len : sa.buf_len;
+    const uint32_t lds_wave = (uint32_t)(uintptr_t)(lds_raw) + wave * Cfg::WAVE_LDS;
+    uint4 *const lds4 = reinterpret_cast<uint4 *>(lds_raw + wave * Cfg::WAVE_LDS);
+    uint32_t *const comb = reinterpret_cast<uint32_t *>(lds_raw + 8 * Cfg::WAVE_LDS); // [wave][6][64]
+    volatile uint32_t *const f_ready = reinterpret_cast<volatile uint32_t *>(lds_raw + 8 * Cfg::WAVE_LDS + Cfg::COMB);
+    volatile uint32_t *const f_ack = f_ready + 8;
+    if (threadIdx.x < 16) f_ready[threadIdx.x] = 0;
+    __syncthreads();
+
+    // Group schedule: the groups (largest class first) are dealt to the
+    // 2 x gridDim.x half-workgroup slots in snake order; slot s of round 0 is
+    // half 0 of workgroup s and slot 2G-1-s half 1 of workgroup s, so every CU
+    // pairs a large group with a small one and, with fewer groups than CUs,
+    // gets at most one.  The halves never synchronise with each other; the K
+    // segment waves of one tile hand over their Poly1305 sums through LDS slots
+    // guarded by per-wave generation flags.
+    const Sched sc = make_sched(tp, n);
+    const uint32_t S = 2 * gridDim.x;
+    const uint32_t my_slot = half == 0 ? blockIdx.x : S - 1 - blockIdx.x;
+    uint32_t gen = 0;
+    for (uint32_t base = 0; base < sc.total_groups; base += S) {
+        ++gen;
+        const uint32_t round = base / S;
+        const uint32_t g = base + ((round & 1) ? S - 1 - my_slot : my_slot);
+        if (g >= sc.total_groups) continue; // uniform over the half
+        if constexpr (STAMP) {
+            const uint64_t t = stamp();
+            t_tail += t - t_mark;
+            t_mark = t;
+        }
+        // ---- which bucket / tile / segment this wave works on (wave-uniform)
+        const uint32_t pb = (uint32_t)__popcll(__ballot(sc.g_end <= g)); // buckets fully before g
+        const uint32_t cls = uniform_u32(__shfl(sc.cls, pb));
+        const uint32_t cnt = uniform_u32(__shfl(sc.cnt, pb));
+        const uint32_t K = uniform_u32(__shfl(sc.K, pb));
+        const uint32_t g0 = pb == 0 ? 0u : uniform_u32(__shfl(sc.g_end, pb - 1));
+        const uint32_t tiles_per_group = 4 / K;
+        const uint32_t tile = (g - g0) * tiles_per_group + hw / K;
+        const uint32_t seg = hw % K;
+        const uint32_t slot = tile * 64 + lane;
+        const bool live = slot < cnt;
+        const uint32_t i = live ? (tp.counts ? tp.lists[(uint64_t)cls * tp.cap + slot] : slot) : 0u;
+
+        // ---- per-lane packet setup and validation (same order as the reference)
+        rg_pkt_desc d = {0, 0, 0};
+        if (live) d = OPEN ? oa.desc[i] : sa.desc[i];
+        uint8_t st = 0xFF;
+        uint32_t P = 0;
+        uint64_t ctr = 0;
+        if (live) {
+            if constexpr (!OPEN) {
+                P = d.len;
+                const bool ok = d.key_idx < sa.nkeys && (P & 15u) == 0 && (d.offset & 15u) == 0 &&
+                                P <= kMaxPayload && d.offset <= buf_len && P + 32 <= buf_len - d.offset;
+                if (!ok) st = d.key_idx == RG_KEY_SKIP ? RG_PKT_REJECTED : RG_PKT_INVALID;
+                else ctr = sa.counters[i];
+            } else {
+                const uint32_t W = d.len;
+                if (d.key_idx == RG_KEY_SKIP) st = RG_PKT_REJECTED;
+                else if ((d.offset & 15u) != 0) st = RG_PKT_UNALIGNED;              // lib.rs:613-615
+                else if (d.key_idx >= oa.nkeys || W > kMaxPayload + 32 || d.offset > buf_len ||
+                         W > buf_len - d.offset || W < 4)
+                    st = RG_PKT_INVALID;
+                if (st == 0xFF) {
+                    const uint4 hdr = *reinterpret_cast<const uint4 *>(buf + d.offset);
+                    if (hdr.x != 4u) st = RG_PKT_NOT_DATA;                            // lib.rs:621-628
+                    else if ((W & 15u) != 0 || W < 16) st = RG_PKT_INVALID;             // types/lib.rs:181-196
+                    else {
+                        ctr = ((uint64_t)hdr.w << 32) | hdr.z;
+                        if (W < 32) st = RG_PKT_DECRYPT_ERR;                            // prim.rs:427-429
+                    }
+                }
+                if (st == 0xFF) P = W - 32;
+            }
+        }
+        const bool work = live && st == 0xFF;
+        const uint32_t nb = work ? P >> 4 : 0; // 16-byte blocks of the packet
+        const uint32_t C = (nb + 3) >> 2;      // 64-byte chunks
+        const uint32_t L = (C + K - 1) / K;    // segment length in chunks
+        const uint32_t c0 = seg * L < C ? seg * L : C;
+        const uint32_t c1 = c0 + L < C ? c0 + L : C;
+        const uint32_t b0 = 4 * c0;
+        const uint32_t b1 = 4 * c1 < nb ? 4 * c1 : nb;
+        const uint32_t snb = b1 - b0;     // blocks of this segment
+        const uint32_t after = nb - b1;   // blocks after this segment
+        const uint32_t segC = c1 - c0;
+        // ---- tile addressing: buffer descriptor based at the lowest frame of the tile
+        uint64_t lo = work ? d.offset : ~0ull;
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) {
+            const uint64_t o = __shfl_xor(lo, m);
+            lo = o < lo ? o : lo;
+        }
+        lo = uniform_u64(lo);
+        if (lo == ~0ull) lo = 0;
+        const uint64_t span_cap = buf_len - lo;
+        const uint32_t nrec = span_cap > kOOB ? kOOB : (uint32_t)span_cap;
+        const v4i rsrc = make_rsrc(buf + lo, nrec);
+        const bool addressable = work && d.offset - lo + 16 + (uint64_t)P <= nrec;
+        // segment payload base relative to the descriptor (kOOB if unusable)
+        const uint32_t my_base = addressable ? (uint32_t)(d.offset - lo) + 16 + 64 * c0 : kOOB;
+        const uint32_t myC = addressable ? segC : 0;
+        uint32_t Wl = (myC + G - 1) / G;
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) {
+            const uint32_t o = __shfl_xor(Wl, m);
+            Wl = o > Wl ? o : Wl;
+        }
+        const uint32_t W = uniform_u32(Wl);
+        // DMA/store address table: instruction q serves lane pq = q*PKT_PER_INST + lane/PPW,
+        // piece k = (lane % PPW) ^ swz(pq)
+        uint32_t tb[PPW], tlim[PPW];
+#pragma unroll
+        for (uint32_t q = 0; q < PPW; ++q) {
+            const uint32_t pq = q * Cfg::PKT_PER_INST + lane / PPW;
+            const uint32_t k = (lane % PPW) ^ swz<G>(pq);
+            const uint32_t b = __shfl(my_base, pq);
+            const uint32_t blocks = __shfl(myC == 0 ? 0u : snb, pq);
+            tb[q] = b == kOOB ? kOOB : b + 16 * k;
+            tlim[q] = blocks > k ? blocks - k : 0; // piece valid in window w iff w*PPW < tlim
+        }
+        // ---- key and one-time Poly1305 key (block 0)
+        const uint32_t n1 = (uint32_t)ctr, n2 = (uint32_t)(ctr >> 32);
+        const Key8 key = load_key(OPEN ? oa.keys : sa.keys, work ? d.key_idx : 0u);
+        const Stream stm = make_stream(key, 0u, n1, n2);
+        uint32_t ks[16];
+        stream_block(stm, 0, ks);
+        const Mul r = make_mul(ks[0], ks[1], ks[2], ks[3]);
+        const uint32_t s0 = ks[4], s1 = ks[5], s2 = ks[6], s3 = ks[7];
+        Acc acc = {0, 0, 0, 0, 0};
+
+        auto voff_of = [&](uint32_t q, uint32_t w) -> uint32_t {
+            return (tb[q] != kOOB && w * PPW < tlim[q]) ? tb[q] + w * PPW * 16 : kOOB;
+        };
+        auto issue_dma = [&](uint32_t w) {
+            const uint32_t lbase = lds_wave + (w & 1) * Cfg::BUF;
+#pragma unroll
+            for (uint32_t q = 0; q < PPW; ++q) dma16(rsrc, voff_of(q, w), uniform_u32(lbase + q * 1024));
+        };
+        auto store_window = [&](uint32_t w) {
+            const uint4 *win = lds4 + (w & 1) * (Cfg::BUF / 16);
+            uint4 v[PPW];
+#pragma unroll
+            for (uint32_t q = 0; q < PPW; ++q) v[q] = win[q * 64 + lane];
+#pragma unroll
+            for (uint32_t q = 0; q < PPW; ++q) store16(rsrc, voff_of(q, w), v[q]);
+        };
+        if constexpr (STAMP) {
+            const uint64_t t = stamp();
+            t_setup += t - t_mark;
+            t_mark = t;
+        }
+        // ---- chunk loop, software-pipelined: the keystream block of chunk c+1
+        // is generated in the same basic block as the XOR / Poly1305 of chunk c
+        const uint32_t Cmax = W * G;
+        const uint32_t f = swz<G>(lane);
+        uint32_t ksc[16];
+        stream_block(stm, c0 + 1, ksc);
+        for (uint32_t c = 0; c < Cmax; ++c) {
+            const uint32_t w = c / G, cl = c % G;
+            if (cl == 0) { // window boundary (wave-uniform)
+                if constexpr (STAMP) {
+                    const uint64_t t = stamp();
+                    t_chunk += t - t_mark;
+                    t_mark = t;
+                }
+                if (w > 0) store_window(w - 1);
+                if constexpr (STAMP) {
+                    const uint64_t t = stamp();
+                    t_store += t - t_mark;
+                    t_mark = t;
+                }
+                const bool more = w + 1 < W;
+                if (w == 0) {
+                    issue_dma(0);
+                    if (more) issue_dma(1);
+                } else if (more) {
+                    issue_dma(w + 1);
+                }
+                if constexpr (STAMP) {
+                    const uint64_t t = stamp();
+                    t_issue += t - t_mark;
+                    t_mark = t;
+                }
+                if (w == 0) {
+                    if (more) wait_vm<PPW>();
+                    else wait_vm<0>();
+                } else {
+                    // wait for DMA(w); younger: stores(w-1) and DMA(w+1)
+                    if (more) wait_vm<2 * PPW>();
+                    else wait_vm<PPW>();
+                }
+                if constexpr (STAMP) {
+                    const uint64_t t = stamp();
+                    t_wait += t - t_mark;
+                    t_mark = t;
+                }
+            }
+            uint4 *win = lds4 + (w & 1) * (Cfg::BUF / 16);
+            // blocks of this chunk that belong to the segment (0..4)
+            const uint32_t cnt4 = c < myC ? (snb - 4 * c < 4 ? snb - 4 * c : 4) : 0;
+            const uint32_t sl0 = lane * PPW + ((4 * cl + 0) ^ f);
+            const uint32_t sl1 = lane * PPW + ((4 * cl + 1) ^ f);
+            const uint32_t sl2 = lane * PPW + ((4 * cl + 2) ^ f);
+            const uint32_t sl3 = lane * PPW + ((4 * cl + 3) ^ f);
+            const uint4 m0 = win[sl0], m1 = win[sl1], m2 = win[sl2], m3 = win[sl3];
+            // XOR + write-back after double round 0, Poly1305 blocks after 1, 3, 5, 7
+            uint4 x0, x1, x2, x3;
+            uint32_t ksn[16];
+            stream_block_hooked(stm, c0 + c + 2, ksn, [&](int dr) {
+                if (dr == 0) {
+                    x0 = xor4(m0, ksc + 0);
+                    x1 = xor4(m1, ksc + 4);
+                    x2 = xor4(m2, ksc + 8);
+                    x3 = xor4(m3, ksc + 12);
+                    win[sl0] = x0; // pieces outside the payload are never stored
+                    win[sl1] = x1;
+                    win[sl2] = x2;
+                    win[sl3] = x3;
+                }
+                if (dr == 1) acc_block_pred(acc, OPEN ? m0 : x0, r, cnt4 > 0);
+                if (dr == 3) acc_block_pred(acc, OPEN ? m1 : x1, r, cnt4 > 1);
+                if (dr == 5) acc_block_pred(acc, OPEN ? m2 : x2, r, cnt4 > 2);
+                if (dr == 7) acc_block_pred(acc, OPEN ? m3 : x3, r, cnt4 > 3);
+                if (dr % 2 == 1) pin_acc(acc);
+            });
+#pragma unroll
+            for (int t = 0; t < 16; ++t) ksc[t] = ksn[t];
+        }
+        if constexpr (STAMP) {
+            const uint64_t t = stamp();
+            t_chunk += t - t_mark;
+            t_mark = t;
+        }
+        if (W > 0) store_window(W - 1);
+        wait_vm<0>(); // this tile's stores drained before the tail touches the frames
+        if (work && !addressable) {
+            // frame outside the tile's 32-bit buffer window (tiles of far-apart
+            // frames, e.g. mixed sizes in arenas > 4 GiB): same segment, direct
+            // 16-byte global accesses
+            uint4 *pl = reinterpret_cast<uint4 *>(buf + d.offset + 16);
+            for (uint32_t c = c0; c < c1; ++c) {
+                const uint32_t hi = 4 * c + 4 < nb ? 4 * c + 4 : nb;
+                stream_block(stm, c + 1, ks);
+                for (uint32_t q = 4 * c; q < hi; ++q) {
+                    const uint4 m = pl[q];
+                    const uint4 x = xor4(m, ks + 4 * (q - 4 * c));
+                    pl[q] = x;
+                    acc_block(acc, OPEN ? m : x, r);
+                }
+            }
+        }
+
+        // ---- segments: h = sum_j A_j r^{N_j}, summed by segment 0.
+        // Hand-off protocol per wave slot w (hw > 0) and generation gen:
+        //   segment j > 0 : wait ack[w] == gen-1, write A_j r^{N_j} to the slot, ready[w] = gen
+        //   segment 0     : wait ready[w+s] == gen, read, ..., ack[w+s] = gen
+        //                   (open: after writing the verdict into row 5 of the slot)
+        //   no hand-off   : wait ack[w] == gen-1, then ready[w] = ack[w] = gen
+        // so every slot's flags advance by exactly one per generation.
+        uint32_t *const mine = comb + wave * 6 * 64;
+        bool bad = false;
+        if (K > 1 && seg + 1 < K) { // every segment but the last needs r^{N_j}
+            uint32_t emax = after;
+#pragma unroll
+            for (int m = 32; m >= 1; m >>= 1) {
+                const uint32_t o = __shfl_xor(emax, m);
+                emax = o > emax ? o : emax;
+            }
+            emax = uniform_u32(emax);
+            const Acc x = acc_pow(r, after, emax == 0 ? 0u : 32 - __clz(emax));
+            acc_mul_gen(acc, make_gen(x));
+        }
+        if (hw > 0) {
+            while (f_ack[wave] != gen - 1) __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            if (K > 1 && seg > 0) {
+                mine[0 * 64 + lane] = acc.h0;
+                mine[1 * 64 + lane] = acc.h1;
+                mine[2 * 64 + lane] = acc.h2;
+                mine[3 * 64 + lane] = acc.h3;
+                mine[4 * 64 + lane] = acc.h4;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup"); // slot written before the flag
+                if (lane == 0) f_ready[wave] = gen;
+            } else if (lane == 0) {
+                f_ready[wave] = gen;
+                f_ack[wave] = gen;
+            }
+        }
+        if (K > 1 && seg == 0) {
+            for (uint32_t s = 1; s < K; ++s) {
+                while (f_ready[wave + s] != gen) __builtin_amdgcn_s_sleep(1);
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                const uint32_t *o = comb + (wave + s) * 6 * 64;
+                const Acc a = {o[0 * 64 + lane], o[1 * 64 + lane], o[2 * 64 + lane], o[3 * 64 + lane],
+                               o[4 * 64 + lane]};
+                acc_add_acc(acc, a);
+                acc_fold(acc);
+            }
+            if constexpr (!OPEN) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup"); // slots read before the ack
+                if (lane == 0)
+                    for (uint32_t s = 1; s < K; ++s) f_ack[wave + s] = gen;
+            }
+        }
+        // ---- tail on segment 0: length block, finish, header/tag or verify
+        uint32_t tag[4] = {0, 0, 0, 0};
+        uint8_t *frame = buf + d.offset;
+        if (seg == 0 && live) {
+            if (st != 0xFF) {
+                if constexpr (!OPEN) {
+                    if (sa.status) sa.status[i] = st;
+                } else {
+                    oa.status[i] = st;
+                    if (oa.counters_out) oa.counters_out[i] = ctr;
+                }
+            } else {
+                acc_add(acc, 0, 0, P, 0, 1); // le64(aad_len = 0) || le64(P)
+                acc_mul(acc, r);
+                acc_finish(acc, s0, s1, s2, s3, tag);
+                if constexpr (!OPEN) {
+                    if (sa.receivers)
+                        *reinterpret_cast<uint4 *>(frame) = make_uint4(4u, sa.receivers[d.key_idx], n1, n2);
+                    *reinterpret_cast<uint4 *>(frame + 16 + P) = make_uint4(tag[0], tag[1], tag[2], tag[3]);
+                    if (sa.status) sa.status[i] = RG_PKT_OK;
+                } else {
+                    const uint4 want = *reinterpret_cast<const uint4 *>(frame + 16 + P);
+                    const uint32_t diff =
+                        (tag[0] ^ want.x) | (tag[1] ^ want.y) | (tag[2] ^ want.z) | (tag[3] ^ want.w);
+                    bad = diff != 0;
+                    oa.status[i] = bad ? RG_PKT_DECRYPT_ERR : RG_PKT_OK;
+                    if (oa.counters_out) oa.counters_out[i] = ctr;
+                }
+            }
+        }
+        if constexpr (OPEN) {
+            // forged / corrupt: every segment re-applies its keystream so the frame is unchanged
+            if (K > 1) {
+                if (seg == 0) {
+                    for (uint32_t s = 1; s < K; ++s) comb[(wave + s) * 6 * 64 + 5 * 64 + lane] = bad ? 1u : 0u;
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    if (lane == 0)
+                        for (uint32_t s = 1; s < K; ++s) f_ack[wave + s] = gen;
+                } else {
+                    while (f_ack[wave] != gen) __builtin_amdgcn_s_sleep(1);
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                    bad = mine[5 * 64 + lane] != 0;
+                }
+            }
+            if (bad) {
+                uint4 *pl = reinterpret_cast<uint4 *>(frame + 16);
+                for (uint32_t c = c0; c < c1; ++c) {
+                    const uint32_t hi = 4 * c + 4 < nb ? 4 * c + 4 : nb;
+                    stream_block(stm, c + 1, ks);
+                    for (uint32_t q = 4 * c; q < hi; ++q) pl[q] = xor4(pl[q], ks + 4 * (q - 4 * c));
+                }
+            }
+        }
+    }
+    if (tp.counts) {
+        // the last workgroup to finish clears the planner counters for the next
+        // batch (every workgroup read them in make_sched before getting here)
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t *ctl = const_cast<uint32_t *>(tp.counts);
+            __atomic_thread_fence(__ATOMIC_SEQ_CST);
+            if (atomicAdd(&ctl[kClasses], 1u) == gridDim.x - 1) {
+                for (uint32_t c = 0; c <= kClasses; ++c) ctl[c] = 0;
+                __atomic_thread_fence(__ATOMIC_SEQ_CST);
+            }
+        }
+    }
+    if constexpr (STAMP) {
+        const uint64_t t = stamp();
+        t_tail += t - t_mark;
+        uint64_t *dbg = OPEN ? oa.dbg : sa.dbg;
+        if (dbg && lane == 0) {
+            uint64_t *o = dbg + 8 * (blockIdx.x * 8 + wave);
+            o[0] = t_setup;
+            o[1] = t_store;
+            o[2] = t_issue;
+            o[3] = t_wait;
+            o[4] = t_chunk;
+            o[5] = t_tail;
+            o[6] = 1;
+            o[7] = realtime() - rt0;
+        }
+    }
+}
+
+// ------------------------------------------------------------ launch
+template <int G> static constexpr uint32_t tile_lds() { return StagedCfg<G>::WG_LDS; }
+static_assert(StagedCfg<2>::WG_LDS <= kLdsPerCu, "8 waves of G = 2 windows must fit the LDS");
+
+hipError_t launch_plan(const rg_pkt_desc *desc, uint32_t n, bool open, const TilePlan &tp, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    // counters start at zero: cleared at allocation and by the last workgroup
+    // of every tile kernel that consumed them
+    hipLaunchKernelGGL(plan_kernel, dim3((n + 256 * kPlanPer - 1) / (256 * kPlanPer)), dim3(256), 0, s, desc, n, open ? 1u : 0u,
+                       const_cast<uint32_t *>(tp.counts), const_cast<uint32_t *>(tp.lists), tp.cap);
+    return hipGetLastError();
+}
+
+hipError_t launch_tiles(const SealArgs *sa, const OpenArgs *oa, int G, const TilePlan &tp, const Launch &L,
+                        hipStream_t s) {
+    const uint32_t n = sa ? sa->n : oa->n;
+    if (n == 0) return hipSuccess;
+    SealArgs a = sa ? *sa : SealArgs{};
+    OpenArgs b = oa ? *oa : OpenArgs{};
+    // one 8-wave workgroup per CU (the whole LDS is reserved, so placement is
+    // one per CU by construction)
+    uint32_t blocks = (uint32_t)(L.cus > 0 ? L.cus : 1);
+    if (!tp.counts) { // identity order: the host knows the group count
+        const uint64_t k = tp.fixed_k ? tp.fixed_k : 1;
+        const uint64_t groups = (((uint64_t)n + 63) / 64 * k + 3) / 4;
+        if (groups < blocks) blocks = (uint32_t)groups;
+    }
+    if (blocks == 0) blocks = 1;
+    const uint32_t need = G == 1 ? tile_lds<1>() : tile_lds<2>();
+    if (G != 1 && G != 2) return hipErrorInvalidValue;
+    if (need > kLdsPerCu) return hipErrorInvalidValue;
+    const uint32_t lds = kLdsPerCu;
+#define RG_TILES(GG)                                                                                          \
+    if (L.debug_mode == 3) {                                                                                  \
+        if (sa) hipLaunchKernelGGL((tile_kernel<GG, false, true>), dim3(blocks), dim3(512), lds, s, a, b, tp); \
+        else hipLaunchKernelGGL((tile_kernel<GG, true, true>), dim3(blocks), dim3(512), lds, s, a, b, tp);     \
+    } else if (sa) hipLaunchKernelGGL((tile_kernel<GG, false>), dim3(blocks), dim3(512), lds, s, a, b, tp);   \
+    else hipLaunchKernelGGL((tile_kernel<GG, true>), dim3(blocks), dim3(512), lds, s, a, b, tp);
+    if (G == 1) {
+        RG_TILES(1)
+    } else {
+        RG_TILES(2)
+    }
+#undef RG_TILES
+    return hipGetLastError();
+}
+
+hipError_t prepare_tile_kernels() {
+    void *fs[8] = {(void *)tile_kernel<1, false>,       (void *)tile_kernel<2, false>,
+                   (void *)tile_kernel<1, true>,        (void *)tile_kernel<2, true>,
+                   (void *)tile_kernel<1, false, true>, (void *)tile_kernel<2, false, true>,
+                   (void *)tile_kernel<1, true, true>,  (void *)tile_kernel<2, true, true>};
+    for (void *f : fs) {
+        hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsPerCu);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+} // namespace rg

@@ -68,27 +68,35 @@ def _gpu_open(engine, keys, desc_open, buf):
 
 
 # kernel configurations every parity test runs under: lane-pass kernels with
-# K lanes per packet, and the LDS-staged tile kernel with G-chunk windows
-MODES = [("lane", 1), ("lane", 2), ("lane", 4), ("staged", 1), ("staged", 2), ("staged", 4)]
+# K lanes per packet, and the LDS-staged tile kernel with G-chunk windows,
+# the size-class planner on/off and 1/2/4 segments per packet (0 = automatic)
+MODES = [("lane", 1), ("lane", 2), ("lane", 4),
+         ("tile", 2, 1, 0), ("tile", 1, 1, 1), ("tile", 2, 1, 2), ("tile", 2, 1, 4),
+         ("tile", 2, 0, 1), ("tile", 2, 0, 2), ("tile", 1, 0, 4), ("tile", 1, 1, 0)]
 
 
 def _configure(engine, mode):
-    kind, v = mode
-    if kind == "lane":
+    _reset(engine)
+    if mode[0] == "lane":
         engine.set_staged(0)
-        engine.set_lanes_per_packet(v)
+        engine.set_lanes_per_packet(mode[1])
     else:
-        engine.set_lanes_per_packet(0)
-        engine.set_staged(v)
+        _, g, plan, k = mode
+        engine.set_staged(g)
+        engine.set_plan(bool(plan))
+        engine.set_segments(k)
 
 
 def _reset(engine):
-    engine.set_staged(0)
+    """library defaults"""
+    engine.set_staged(2)
+    engine.set_plan(True)
+    engine.set_segments(0)
     engine.set_lanes_per_packet(0)
 
 
 def _mode_id(m):
-    return f"{m[0]}{m[1]}"
+    return f"lane{m[1]}" if m[0] == "lane" else f"tile_g{m[1]}_p{m[2]}_k{m[3]}"
 
 
 # ------------------------------------------------------------ reference pins
@@ -199,6 +207,39 @@ def test_random_batches_vs_oracle(engine, mode, seed):
     assert np.array_equal(co, ctr)
     for d in desc[:200]:
         o, p = int(d["offset"]), int(d["len"])
+        assert np.array_equal(back[o + 16: o + 16 + p], buf[o + 16: o + 16 + p])
+    _reset(engine)
+
+
+@pytest.mark.parametrize("mode", MODES, ids=_mode_id)
+def test_large_payload_mix_vs_oracle(engine, mode):
+    """Every size class of the planner (up to the 1 MiB payload limit), shuffled with small packets,
+    then opened back; one large frame forged to check the segmented restore path."""
+    _configure(engine, mode)
+    rng = np.random.default_rng(31)
+    big = [1 << 20, 65520, 40000 // 16 * 16, 16384, 4096 + 16, 2048, 1040, 1024]
+    sizes = np.array(big + list(rng.integers(0, 100, 200) * 16))
+    rng.shuffle(sizes)
+    n = len(sizes)
+    keys, rec, desc, ctr, buf = _random_batch(rng, n, nkeys=3, sizes=sizes)
+    want = buf.copy()
+    oracle.seal_batch(keys, rec, desc, ctr, want, nthreads=8)
+    got, st = _gpu_seal(engine, keys, rec, desc, ctr, buf)
+    assert (st == aead.PKT_OK).all()
+    assert np.array_equal(got, want)
+    od = desc.copy()
+    od["len"] += 32
+    j = int(np.argmax(sizes))
+    tampered = got.copy()
+    tampered[int(od[j]["offset"]) + 16 + int(sizes[j]) // 2] ^= 0x10
+    back, st, co = _gpu_open(engine, keys, od, tampered)
+    ok = np.ones(n, bool)
+    ok[j] = False
+    assert (st[ok] == aead.PKT_OK).all() and st[j] == aead.PKT_DECRYPT_ERR
+    o, w = int(od[j]["offset"]), int(od[j]["len"])
+    assert np.array_equal(back[o:o + w], tampered[o:o + w])
+    for i in np.nonzero(ok)[0][::7]:
+        o, p = int(desc[i]["offset"]), int(desc[i]["len"])
         assert np.array_equal(back[o + 16: o + 16 + p], buf[o + 16: o + 16 + p])
     _reset(engine)
 

@@ -46,6 +46,15 @@ for s in "$@"; do
             python3 bench.py --workload $W --steps 5 --warmup 2 --cpu-seconds 0
         run pmc_write_$W 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write_$W -o p -- \
             python3 bench.py --workload $W --steps 5 --warmup 2 --cpu-seconds 0 ;;
+    tiles)
+        W=${RG_WORKLOAD:-cfg2}
+        for v in "p1k0:--plan 1" "p0k1:--plan 0 --segments 1" "p0k2:--plan 0 --segments 2" "p1k2:--plan 1 --segments 2" "p1k4:--plan 1 --segments 4" "g1p1:--staged 1 --plan 1" "p0k4:--plan 0 --segments 4"; do
+            name=${v%%:*}; flags=${v#*:}
+            run tiles_${W}_$name 200 python bench.py --workload $W $flags --steps 20 --warmup 3 --cpu-seconds 0
+        done
+        grep -H '"value"' gpurun_out/tiles_${W}_*.log | python3 -c "import sys,json
+for l in sys.stdin:
+    f,j=l.split(':',1); d=json.loads(j); print(f.split('/')[-1], d['value'], d['seal_ms'], d['open_ms'])" ;;
     pmc_list) run pmc_list 120 rocprofv3 -L ;;
     pmc)
         # separate passes (TCC FETCH_SIZE and WRITE_SIZE do not fit one pass; never combined with tracing domains)
@@ -97,7 +106,13 @@ for l in sys.stdin:
             run pmcclk_$name 240 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_WAVES SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY \
                 --kernel-trace --output-format csv -d gpurun_out/pmcclk_$name -o p -- python3 bench.py --workload $W $flags --steps 5 --warmup 2 --cpu-seconds 0 --no-graph
         done ;;
-    stamps) run stamps 300 python tools/stamps.py --workload ${RG_WORKLOAD:-cfg2} --staged ${RG_G:-2} ;;
+    pmc_sq)
+        W=${RG_PMC_WORKLOAD:-cfg2}
+        run pmcsq_$W 240 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_WAVES SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY \
+            --kernel-trace --output-format csv -d gpurun_out/pmcsq_$W -o p -- python3 bench.py --workload $W --steps 5 --warmup 2 --cpu-seconds 0 --no-graph
+        run pmcsq2_$W 240 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_VMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_LDS \
+            --kernel-trace --output-format csv -d gpurun_out/pmcsq2_$W -o p -- python3 bench.py --workload $W --steps 5 --warmup 2 --cpu-seconds 0 --no-graph ;;
+    stamps) run stamps_${RG_WORKLOAD:-cfg2} 300 python tools/stamps.py --workload ${RG_WORKLOAD:-cfg2} --staged ${RG_G:-2} --wg-per-cu ${RG_WPC:-0} ${RG_STAMP_FLAGS:-} ;;
     *) echo "unknown step $s"; exit 2 ;;
     esac
 done

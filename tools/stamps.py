@@ -17,11 +17,17 @@ from rustyguard_amd.device import DeviceBatch  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--workload", default="cfg2")
 ap.add_argument("--staged", type=int, default=2)
-ap.add_argument("--wg-per-cu", type=int, default=1)
+ap.add_argument("--wg-per-cu", type=int, default=0)
+ap.add_argument("--plan", type=int, default=-1)
+ap.add_argument("--segments", type=int, default=0)
 args = ap.parse_args()
 eng = Engine(0)
 eng.set_staged(args.staged)
-eng.set_wg_per_cu(args.wg_per_cu)
+if args.wg_per_cu:
+    eng.set_wg_per_cu(args.wg_per_cu)
+if args.plan >= 0:
+    eng.set_plan(bool(args.plan))
+eng.set_segments(args.segments)
 w = workloads.build(args.workload)
 b = DeviceBatch(eng, w)
 b.fill()
@@ -50,6 +56,11 @@ for op in ("seal", "open"):
     d = d[d[:, 6] == 1]
     names = ["setup", "store", "dma_issue", "dma_wait", "chunk", "tail"]
     tot = d[:, :6].sum(axis=1)
+    rt = d[:, 7].astype(np.float64) / 100e6  # s_memrealtime ticks at 100 MHz
+    q = np.percentile(rt * 1e6, [0, 10, 50, 90, 99, 100])
     out[op] = {"waves": int(len(d)), "cycles_per_wave_mean": float(tot.mean()),
+               "wave_us_mean": round(float(rt.mean()) * 1e6, 2),
+               "wave_us_pct_0_10_50_90_99_100": [round(float(x), 1) for x in q],
+               "shader_clock_ghz": round(float(tot.sum() / rt.sum()) / 1e9, 3),
                "share": {n: round(float(d[:, k].sum() / tot.sum()), 4) for k, n in enumerate(names)}}
 print(json.dumps(out, indent=1))
