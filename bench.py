@@ -43,7 +43,7 @@ def parse():
     ap.add_argument("--lanes", type=int, default=0, help="lanes per packet (0 = auto)")
     ap.add_argument("--wg-per-cu", type=int, default=0, help="resident workgroups per CU (0 = auto, -1 = plain grid)")
     ap.add_argument("--staged", type=int, default=-1, help="LDS-staged window chunks (0 = lane-pass kernels, -1 = default)")
-    ap.add_argument("--plan", type=int, default=-1, help="size-class planner: 1 on, 0 off, -1 library default (on)")
+    ap.add_argument("--plan", type=int, default=-1, help="size-class planner: 0 off, 1 on, 2 auto, -1 library default (auto)")
     ap.add_argument("--segments", type=int, default=0, help="segments per packet for the tile kernels (0 = auto)")
     ap.add_argument("--debug-mode", type=int, default=0, help="seal diagnostics (invalid output): 1 compute-only, 2 memory-only")
     ap.add_argument("--no-graph", action="store_true", help="launch eagerly instead of replaying a captured HIP graph")
@@ -139,7 +139,7 @@ def main():
     if args.staged >= 0:
         eng.set_staged(args.staged)
     if args.plan >= 0:
-        eng.set_plan(bool(args.plan))
+        eng.set_plan(args.plan)
     if args.segments:
         eng.set_segments(args.segments)
     if args.workload == "cfg5":
@@ -261,7 +261,7 @@ def main():
                    "sessions": int(w.meta.get("sessions", 1)), "parallelism": f"split{world} (no collective)",
                    "kernel": (f"lane-pass, {eng.lanes_per_packet(w.n)} lanes/packet" if args.staged == 0 else
                               f"lds-staged tiles, {args.staged if args.staged > 0 else 2} chunks/window, "
-                              f"planner {'off' if args.plan == 0 else 'on'}, segments {args.segments or 'auto'}"),
+                              f"planner {({0: 'off', 1: 'on'}).get(args.plan, 'auto')}, segments {args.segments or 'auto'}"),
                    "wg_per_cu": args.wg_per_cu or "auto"},
         "mpkt_s": round(total_pkts / tmax / 1e6, 3),
         "seal_ms": round(seal_ms, 5),

@@ -115,11 +115,14 @@ int rg_set_wg_per_cu(rg_ctx *ctx, int wg_per_cu);
  * 1/2 = LDS-staged tiles (one packet (segment) per lane, coalesced LDS-DMA
  * windows of that many 64-byte chunks; default 2). */
 int rg_set_staged(rg_ctx *ctx, int window_chunks);
-/* Tile kernels: 1 (default) = a device-side planner first sorts the batch into
- * size classes so that every 64-packet tile holds packets of similar length;
- * 0 = tiles take packets in array order.  Device-API calls that share a
- * context use one set of planner buffers: issue them on one stream (or order
- * them) -- the host-memory API has its own per pipeline stream. */
+/* Tile kernels: a device-side planner can first sort the batch into size
+ * classes so that every 64-packet tile holds packets of similar length.
+ * 0 = off (tiles take packets in array order), 1 = always, 2 (default) =
+ * auto: plan unless the last planned batch of this context held a single size
+ * class (re-checked every 32nd call).  Results are identical in every mode.
+ * Device-API calls that share a context use one set of planner buffers: issue
+ * them on one stream (or order them) -- the host-memory API has its own per
+ * pipeline stream. */
 int rg_set_plan(rg_ctx *ctx, int on);
 /* Segments per packet for the tile kernels: 0 (default) = per size class,
  * aiming at two resident waves per SIMD; 1/2/4 = split every packet into that

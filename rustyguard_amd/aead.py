@@ -111,9 +111,9 @@ class Engine:
         """0 = lane-pass kernels; 1/2/4 = LDS-staged tile kernel with that window."""
         check(self._L.rg_set_staged(self._h, window_chunks), "rg_set_staged")
 
-    def set_plan(self, on: bool):
-        """Device-side size-class planner before the tile kernels (default on)."""
-        check(self._L.rg_set_plan(self._h, 1 if on else 0), "rg_set_plan")
+    def set_plan(self, mode):
+        """Size-class planner before the tile kernels: 0/False off, 1/True on, 2 auto (default)."""
+        check(self._L.rg_set_plan(self._h, int(mode)), "rg_set_plan")
 
     def set_segments(self, k: int):
         """Segments per packet for the tile kernels: 0 = automatic, 1/2/4 = forced."""

@@ -81,11 +81,28 @@ struct HostBuf {
 struct PlanBuf {
     DevBuf counts, lists;
     uint32_t cap = 0;
+    // auto planning: the tile kernel reports the number of size classes of the
+    // last planned batch into host-mapped memory (read without synchronising;
+    // a stale value only costs or saves one planner pass)
+    volatile uint32_t *h_classes = nullptr;
+    uint32_t *d_classes = nullptr;
+    uint64_t calls = 0;
     hipError_t reserve(size_t n) {
         if (!counts.p) { // counters + done count; the tile kernels leave them zeroed
             hipError_t e = counts.reserve((rg::kClasses + 1) * sizeof(uint32_t));
             if (e == hipSuccess) e = hipMemset(counts.p, 0, (rg::kClasses + 1) * sizeof(uint32_t));
             if (e != hipSuccess) return e;
+        }
+        if (!h_classes) {
+            void *hp = nullptr;
+            hipError_t e = hipHostMalloc(&hp, 64, hipHostMallocMapped | hipHostMallocCoherent);
+            if (e != hipSuccess) return e;
+            h_classes = static_cast<volatile uint32_t *>(hp);
+            *h_classes = ~0u; // unknown: plan
+            void *dp = nullptr;
+            e = hipHostGetDevicePointer(&dp, hp, 0);
+            if (e != hipSuccess) return e;
+            d_classes = static_cast<uint32_t *>(dp);
         }
         hipError_t e = hipSuccess;
         if (n <= cap) return e;
@@ -97,6 +114,15 @@ struct PlanBuf {
         counts.release();
         lists.release();
         cap = 0;
+        if (h_classes) (void)hipHostFree(const_cast<uint32_t *>(h_classes));
+        h_classes = nullptr;
+        d_classes = nullptr;
+    }
+    // auto mode: plan unless the last planned batch held a single size class;
+    // re-check every 32nd call
+    bool want_plan() {
+        const bool check = (calls++ % 32) == 0;
+        return check || !h_classes || *h_classes != 1u;
     }
 };
 
@@ -120,7 +146,7 @@ struct rg_ctx {
     int cus = 0;
     int debug_mode = 0;
     int staged_g = 2; // 0 = lane-pass kernels, else LDS-staged windows of G chunks (default: 2)
-    int plan = 1;     // size-class planner before the tile kernel (0 = packets in array order)
+    int plan = 2;     // size-class planner: 0 off (array order), 1 always, 2 auto (skip for single-class batches)
     int segments = 0; // segments per packet: 0 = automatic, else 1 / 2 / 4
     PlanBuf plan_dev; // planner lists of the device API (calls on one ctx are stream-ordered)
     uint64_t *dbg = nullptr; // diagnostics buffer (device), stamp builds only
@@ -233,7 +259,7 @@ int rg_set_staged(rg_ctx *ctx, int g) {
 
 int rg_set_plan(rg_ctx *ctx, int on) {
     if (!ctx) return set_err(RG_EINVAL, "null context");
-    if (on != 0 && on != 1) return set_err(RG_EINVAL, "plan must be 0 or 1");
+    if (on < 0 || on > 2) return set_err(RG_EINVAL, "plan must be 0 (off), 1 (on) or 2 (auto)");
     ctx->plan = on;
     return RG_OK;
 }
@@ -291,12 +317,19 @@ static hipError_t launch_tiles_any(rg_ctx *ctx, const rg::SealArgs *sa, const rg
     rg::TilePlan tp{};
     tp.target_lanes = (uint32_t)std::max(1, ctx->cus) * 256u; // one wave per SIMD
     tp.fixed_k = (uint32_t)ctx->segments;
-    if (ctx->plan) {
+    bool plan = ctx->plan == 1;
+    if (ctx->plan == 2) {
+        hipError_t e = pb.reserve(n);
+        if (e != hipSuccess) return e;
+        plan = pb.want_plan();
+    }
+    if (plan) {
         hipError_t e = pb.reserve(n);
         if (e != hipSuccess) return e;
         tp.counts = static_cast<uint32_t *>(pb.counts.p);
         tp.lists = static_cast<uint32_t *>(pb.lists.p);
         tp.cap = pb.cap;
+        tp.classes_out = pb.d_classes;
         e = rg::launch_plan(sa ? sa->desc : oa->desc, n, oa != nullptr, tp, st);
         if (e != hipSuccess) return e;
     } else if (!tp.fixed_k) {

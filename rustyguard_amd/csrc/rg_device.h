@@ -294,6 +294,17 @@ __device__ __forceinline__ void acc_block_pred(Acc &h, const uint4 &m, const Mul
     h.h4 = valid ? t.h4 : h.h4;
 }
 
+// h = valid ? h * r : h, branch-free
+__device__ __forceinline__ void acc_mul_pred(Acc &h, const Mul &r, bool valid) {
+    Acc t = h;
+    acc_mul(t, r);
+    h.h0 = valid ? t.h0 : h.h0;
+    h.h1 = valid ? t.h1 : h.h1;
+    h.h2 = valid ? t.h2 : h.h2;
+    h.h3 = valid ? t.h3 : h.h3;
+    h.h4 = valid ? t.h4 : h.h4;
+}
+
 // empty asm that makes h opaque here: later Poly work cannot move above this
 // point and earlier work cannot sink below it (zero instructions)
 __device__ __forceinline__ void pin_acc(Acc &h) {
@@ -422,25 +433,6 @@ __device__ __forceinline__ void acc_fold(Acc &h) {
     h.h2 = addc(h.h2, 0, k, k);
     h.h3 = addc(h.h3, 0, k, k);
     h.h4 = (h.h4 & 3u) + k;
-}
-
-// r^e mod 2^130-5 for a per-lane exponent e < 2^bits (bits wave-uniform):
-// left-to-right square-and-multiply, squarings with the general multiplier,
-// the multiply by r with the clamped one; branch-free per lane.
-__device__ __forceinline__ Acc acc_pow(const Mul &r, uint32_t e, uint32_t bits) {
-    Acc x = {1, 0, 0, 0, 0};
-    for (int b = (int)bits - 1; b >= 0; --b) {
-        acc_mul_gen(x, make_gen(x));
-        Acc y = x;
-        acc_mul(y, r);
-        const bool take = (e >> b) & 1u;
-        x.h0 = take ? y.h0 : x.h0;
-        x.h1 = take ? y.h1 : x.h1;
-        x.h2 = take ? y.h2 : x.h2;
-        x.h3 = take ? y.h3 : x.h3;
-        x.h4 = take ? y.h4 : x.h4;
-    }
-    return x;
 }
 
 __device__ __forceinline__ uint64_t mix64(uint64_t x) {

@@ -70,7 +70,7 @@ struct TilePlan {
     uint32_t cap;
     uint32_t target_lanes; // segment sizing: aim for this many busy lanes (0 = no splitting)
     uint32_t fixed_k;      // 0 = per class from the counts, else 1 / 2 / 4 segments for every packet
-    uint32_t pad_;
+    uint32_t *classes_out; // host-mapped: number of non-empty classes of the batch (or nullptr)
 };
 
 hipError_t launch_seal(const SealArgs &a, const Launch &L, hipStream_t s);

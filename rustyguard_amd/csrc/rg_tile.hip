@@ -22,10 +22,14 @@
 // Segments: segment j of a packet covers chunks [jL, min(C, (j+1)L)),
 // L = ceil(C/K), keystream blocks from jL + 1; its lane runs its own Horner
 // chain A_j over its blocks.  With N_j = blocks after segment j,
-//   h = sum_j A_j r^{N_j}   (RFC 8439 Poly1305 of the whole ciphertext),
-// so each segment multiplies by r^{N_j} (acc_pow) and the sums meet in LDS.
+//   h = sum_j A_j r^{N_j}   (RFC 8439 Poly1305 of the whole ciphertext)
+//     = (..(A_0 q_1 + A_1) q_2 + ..) q_{K-1} + A_{K-1},  q_j = r^{n_j},
+// so segments j > 0 also track q_j (one clamped multiply per block) and hand
+// (A_j, q_j) to segment 0 through LDS.
 #include "rg_device.h"
 #include "rg_internal.h"
+
+#include <type_traits>
 
 namespace rg {
 
@@ -146,6 +150,10 @@ template <int N> __device__ __forceinline__ void wait_vm() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// segment hand-off slot per wave: rows 0-4 partial sum A_j, 5-9 q_j = r^{n_j},
+// 10 the open verdict sent back by segment 0
+constexpr uint32_t kSlotRows = 11;
+
 // Window geometry: PPW 16-byte pieces per lane per window; DMA instruction q
 // serves packets q*PKT_PER_INST .. +PKT_PER_INST-1, PPW lanes per packet, one
 // whole contiguous 64G-byte run each (coalesced).  The LDS image is
@@ -157,7 +165,7 @@ template <int G> struct StagedCfg {
     static constexpr uint32_t PKT_PER_INST = 64 / PPW;
     static constexpr uint32_t BUF = 64 * PPW * 16;  // bytes per window buffer per wave
     static constexpr uint32_t WAVE_LDS = 2 * BUF;   // double-buffered
-    static constexpr uint32_t COMB = 8 * 6 * 64 * 4; // segment hand-off slots, one per wave
+    static constexpr uint32_t COMB = 8 * kSlotRows * 64 * 4; // segment hand-off slots, one per wave
     static constexpr uint32_t FLAGS = 2 * 8 * 4;     // ready / ack generation per wave slot
     static constexpr uint32_t WG_LDS = 8 * WAVE_LDS + COMB + FLAGS;
 };
@@ -260,7 +268,7 @@ __global__ __launch_bounds__(512) void tile_kernel(SealArgs sa, OpenArgs oa, Til
     const uint64_t buf_len = OPEN ? oa.buf_len : sa.buf_len;
     const uint32_t lds_wave = (uint32_t)(uintptr_t)(lds_raw) + wave * Cfg::WAVE_LDS;
     uint4 *const lds4 = reinterpret_cast<uint4 *>(lds_raw + wave * Cfg::WAVE_LDS);
-    uint32_t *const comb = reinterpret_cast<uint32_t *>(lds_raw + 8 * Cfg::WAVE_LDS); // [wave][6][64]
+    uint32_t *const comb = reinterpret_cast<uint32_t *>(lds_raw + 8 * Cfg::WAVE_LDS); // [wave][kSlotRows][64]
     volatile uint32_t *const f_ready = reinterpret_cast<volatile uint32_t *>(lds_raw + 8 * Cfg::WAVE_LDS + Cfg::COMB);
     volatile uint32_t *const f_ack = f_ready + 8;
     if (threadIdx.x < 16) f_ready[threadIdx.x] = 0;
@@ -274,7 +282,8 @@ __global__ __launch_bounds__(512) void tile_kernel(SealArgs sa, OpenArgs oa, Til
     // segment waves of one tile hand over their Poly1305 sums through LDS slots
     // guarded by per-wave generation flags.
     const Sched sc = make_sched(tp, n);
-    const uint32_t S = 2 * gridDim.x;
+    const uint32_t halves = blockDim.x / 256; // 1 when the host launched 4-wave workgroups
+    const uint32_t S = halves * gridDim.x;
     const uint32_t my_slot = half == 0 ? blockIdx.x : S - 1 - blockIdx.x;
     uint32_t gen = 0;
     for (uint32_t base = 0; base < sc.total_groups; base += S) {
@@ -341,7 +350,6 @@ __global__ __launch_bounds__(512) void tile_kernel(SealArgs sa, OpenArgs oa, Til
         const uint32_t b0 = 4 * c0;
         const uint32_t b1 = 4 * c1 < nb ? 4 * c1 : nb;
         const uint32_t snb = b1 - b0;     // blocks of this segment
-        const uint32_t after = nb - b1;   // blocks after this segment
         const uint32_t segC = c1 - c0;
         // ---- tile addressing: buffer descriptor based at the lowest frame of the tile
         uint64_t lo = work ? d.offset : ~0ull;
@@ -411,10 +419,22 @@ __global__ __launch_bounds__(512) void tile_kernel(SealArgs sa, OpenArgs oa, Til
         }
         // ---- chunk loop, software-pipelined: the keystream block of chunk c+1
         // is generated in the same basic block as the XOR / Poly1305 of chunk c
-        const uint32_t Cmax = W * G;
+        // iterations: the longest segment of the wave (the last window may be partial)
+        uint32_t Cl = myC;
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) {
+            const uint32_t o = __shfl_xor(Cl, m);
+            Cl = o > Cl ? o : Cl;
+        }
+        const uint32_t Cmax = uniform_u32(Cl);
         const uint32_t f = swz<G>(lane);
+        // segments after the first also track q = r^{blocks absorbed} (one
+        // more clamped multiply per block) for the combine below
+        Acc pw = {1, 0, 0, 0, 0};
+        auto run_chunks = [&](auto track_tag) {
+        constexpr bool TRACK = decltype(track_tag)::value;
         uint32_t ksc[16];
-        stream_block(stm, c0 + 1, ksc);
+        if (Cmax > 0) stream_block(stm, c0 + 1, ksc);
         for (uint32_t c = 0; c < Cmax; ++c) {
             const uint32_t w = c / G, cl = c % G;
             if (cl == 0) { // window boundary (wave-uniform)
@@ -463,6 +483,25 @@ __global__ __launch_bounds__(512) void tile_kernel(SealArgs sa, OpenArgs oa, Til
             const uint32_t sl2 = lane * PPW + ((4 * cl + 2) ^ f);
             const uint32_t sl3 = lane * PPW + ((4 * cl + 3) ^ f);
             const uint4 m0 = win[sl0], m1 = win[sl1], m2 = win[sl2], m3 = win[sl3];
+            if (c + 1 == Cmax) { // last chunk: no next keystream block to overlap with
+                const uint4 x0 = xor4(m0, ksc + 0), x1 = xor4(m1, ksc + 4), x2 = xor4(m2, ksc + 8),
+                            x3 = xor4(m3, ksc + 12);
+                win[sl0] = x0;
+                win[sl1] = x1;
+                win[sl2] = x2;
+                win[sl3] = x3;
+                acc_block_pred(acc, OPEN ? m0 : x0, r, cnt4 > 0);
+                acc_block_pred(acc, OPEN ? m1 : x1, r, cnt4 > 1);
+                acc_block_pred(acc, OPEN ? m2 : x2, r, cnt4 > 2);
+                acc_block_pred(acc, OPEN ? m3 : x3, r, cnt4 > 3);
+                if constexpr (TRACK) {
+                    acc_mul_pred(pw, r, cnt4 > 0);
+                    acc_mul_pred(pw, r, cnt4 > 1);
+                    acc_mul_pred(pw, r, cnt4 > 2);
+                    acc_mul_pred(pw, r, cnt4 > 3);
+                }
+                break;
+            }
             // XOR + write-back after double round 0, Poly1305 blocks after 1, 3, 5, 7
             uint4 x0, x1, x2, x3;
             uint32_t ksn[16];
@@ -482,10 +521,21 @@ __global__ __launch_bounds__(512) void tile_kernel(SealArgs sa, OpenArgs oa, Til
                 if (dr == 5) acc_block_pred(acc, OPEN ? m2 : x2, r, cnt4 > 2);
                 if (dr == 7) acc_block_pred(acc, OPEN ? m3 : x3, r, cnt4 > 3);
                 if (dr % 2 == 1) pin_acc(acc);
+                if constexpr (TRACK) {
+                    if (dr == 2) acc_mul_pred(pw, r, cnt4 > 0);
+                    if (dr == 4) acc_mul_pred(pw, r, cnt4 > 1);
+                    if (dr == 6) acc_mul_pred(pw, r, cnt4 > 2);
+                    if (dr == 8) acc_mul_pred(pw, r, cnt4 > 3);
+                    if (dr % 2 == 0 && dr > 0) pin_acc(pw);
+                }
             });
 #pragma unroll
             for (int t = 0; t < 16; ++t) ksc[t] = ksn[t];
         }
+        };
+        const bool track = K > 1 && seg > 0; // wave-uniform
+        if (track) run_chunks(std::true_type{});
+        else run_chunks(std::false_type{});
         if constexpr (STAMP) {
             const uint64_t t = stamp();
             t_chunk += t - t_mark;
@@ -506,30 +556,20 @@ __global__ __launch_bounds__(512) void tile_kernel(SealArgs sa, OpenArgs oa, Til
                     const uint4 x = xor4(m, ks + 4 * (q - 4 * c));
                     pl[q] = x;
                     acc_block(acc, OPEN ? m : x, r);
+                    if (track) acc_mul(pw, r);
                 }
             }
         }
 
         // ---- segments: h = sum_j A_j r^{N_j}, summed by segment 0.
         // Hand-off protocol per wave slot w (hw > 0) and generation gen:
-        //   segment j > 0 : wait ack[w] == gen-1, write A_j r^{N_j} to the slot, ready[w] = gen
+        //   segment j > 0 : wait ack[w] == gen-1, write (A_j, q_j) to the slot, ready[w] = gen
         //   segment 0     : wait ready[w+s] == gen, read, ..., ack[w+s] = gen
-        //                   (open: after writing the verdict into row 5 of the slot)
+        //                   (open: after writing the verdict into row 10 of the slot)
         //   no hand-off   : wait ack[w] == gen-1, then ready[w] = ack[w] = gen
         // so every slot's flags advance by exactly one per generation.
-        uint32_t *const mine = comb + wave * 6 * 64;
+        uint32_t *const mine = comb + wave * kSlotRows * 64;
         bool bad = false;
-        if (K > 1 && seg + 1 < K) { // every segment but the last needs r^{N_j}
-            uint32_t emax = after;
-#pragma unroll
-            for (int m = 32; m >= 1; m >>= 1) {
-                const uint32_t o = __shfl_xor(emax, m);
-                emax = o > emax ? o : emax;
-            }
-            emax = uniform_u32(emax);
-            const Acc x = acc_pow(r, after, emax == 0 ? 0u : 32 - __clz(emax));
-            acc_mul_gen(acc, make_gen(x));
-        }
         if (hw > 0) {
             while (f_ack[wave] != gen - 1) __builtin_amdgcn_s_sleep(1);
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -539,6 +579,11 @@ __global__ __launch_bounds__(512) void tile_kernel(SealArgs sa, OpenArgs oa, Til
                 mine[2 * 64 + lane] = acc.h2;
                 mine[3 * 64 + lane] = acc.h3;
                 mine[4 * 64 + lane] = acc.h4;
+                mine[5 * 64 + lane] = pw.h0;
+                mine[6 * 64 + lane] = pw.h1;
+                mine[7 * 64 + lane] = pw.h2;
+                mine[8 * 64 + lane] = pw.h3;
+                mine[9 * 64 + lane] = pw.h4;
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup"); // slot written before the flag
                 if (lane == 0) f_ready[wave] = gen;
             } else if (lane == 0) {
@@ -547,12 +592,16 @@ __global__ __launch_bounds__(512) void tile_kernel(SealArgs sa, OpenArgs oa, Til
             }
         }
         if (K > 1 && seg == 0) {
+            // Horner over the segments: h = (..(A_0 q_1 + A_1) q_2 + ..) + A_{K-1}
             for (uint32_t s = 1; s < K; ++s) {
                 while (f_ready[wave + s] != gen) __builtin_amdgcn_s_sleep(1);
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                const uint32_t *o = comb + (wave + s) * 6 * 64;
+                const uint32_t *o = comb + (wave + s) * kSlotRows * 64;
                 const Acc a = {o[0 * 64 + lane], o[1 * 64 + lane], o[2 * 64 + lane], o[3 * 64 + lane],
                                o[4 * 64 + lane]};
+                const Acc q = {o[5 * 64 + lane], o[6 * 64 + lane], o[7 * 64 + lane], o[8 * 64 + lane],
+                               o[9 * 64 + lane]};
+                acc_mul_gen(acc, make_gen(q));
                 acc_add_acc(acc, a);
                 acc_fold(acc);
             }
@@ -596,14 +645,14 @@ __global__ __launch_bounds__(512) void tile_kernel(SealArgs sa, OpenArgs oa, Til
             // forged / corrupt: every segment re-applies its keystream so the frame is unchanged
             if (K > 1) {
                 if (seg == 0) {
-                    for (uint32_t s = 1; s < K; ++s) comb[(wave + s) * 6 * 64 + 5 * 64 + lane] = bad ? 1u : 0u;
+                    for (uint32_t s = 1; s < K; ++s) comb[(wave + s) * kSlotRows * 64 + 10 * 64 + lane] = bad ? 1u : 0u;
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                     if (lane == 0)
                         for (uint32_t s = 1; s < K; ++s) f_ack[wave + s] = gen;
                 } else {
                     while (f_ack[wave] != gen) __builtin_amdgcn_s_sleep(1);
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                    bad = mine[5 * 64 + lane] != 0;
+                    bad = mine[10 * 64 + lane] != 0;
                 }
             }
             if (bad) {
@@ -613,19 +662,6 @@ __global__ __launch_bounds__(512) void tile_kernel(SealArgs sa, OpenArgs oa, Til
                     stream_block(stm, c + 1, ks);
                     for (uint32_t q = 4 * c; q < hi; ++q) pl[q] = xor4(pl[q], ks + 4 * (q - 4 * c));
                 }
-            }
-        }
-    }
-    if (tp.counts) {
-        // the last workgroup to finish clears the planner counters for the next
-        // batch (every workgroup read them in make_sched before getting here)
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            uint32_t *ctl = const_cast<uint32_t *>(tp.counts);
-            __atomic_thread_fence(__ATOMIC_SEQ_CST);
-            if (atomicAdd(&ctl[kClasses], 1u) == gridDim.x - 1) {
-                for (uint32_t c = 0; c <= kClasses; ++c) ctl[c] = 0;
-                __atomic_thread_fence(__ATOMIC_SEQ_CST);
             }
         }
     }
@@ -643,6 +679,26 @@ __global__ __launch_bounds__(512) void tile_kernel(SealArgs sa, OpenArgs oa, Til
             o[5] = t_tail;
             o[6] = 1;
             o[7] = realtime() - rt0;
+        }
+    }
+    if (tp.counts) {
+        // the last workgroup to finish clears the planner counters for the next
+        // batch (every workgroup read them in make_sched before getting here)
+        // and reports how many size classes the batch used (auto planning)
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t *ctl = const_cast<uint32_t *>(tp.counts);
+            __atomic_thread_fence(__ATOMIC_SEQ_CST);
+            if (atomicAdd(&ctl[kClasses], 1u) == gridDim.x - 1) {
+                uint32_t used = 0;
+                for (uint32_t c = 0; c < kClasses; ++c) {
+                    used += ctl[c] != 0;
+                    ctl[c] = 0;
+                }
+                ctl[kClasses] = 0;
+                if (tp.classes_out) *reinterpret_cast<volatile uint32_t *>(tp.classes_out) = used;
+                __atomic_thread_fence(__ATOMIC_SEQ_CST);
+            }
         }
     }
 }
@@ -669,10 +725,14 @@ hipError_t launch_tiles(const SealArgs *sa, const OpenArgs *oa, int G, const Til
     // one 8-wave workgroup per CU (the whole LDS is reserved, so placement is
     // one per CU by construction)
     uint32_t blocks = (uint32_t)(L.cus > 0 ? L.cus : 1);
+    uint32_t threads = 512;
     if (!tp.counts) { // identity order: the host knows the group count
         const uint64_t k = tp.fixed_k ? tp.fixed_k : 1;
         const uint64_t groups = (((uint64_t)n + 63) / 64 * k + 3) / 4;
-        if (groups < blocks) blocks = (uint32_t)groups;
+        if (groups <= blocks) { // at most one group per CU: 4-wave workgroups
+            blocks = (uint32_t)groups;
+            threads = 256;
+        }
     }
     if (blocks == 0) blocks = 1;
     const uint32_t need = G == 1 ? tile_lds<1>() : tile_lds<2>();
@@ -681,10 +741,10 @@ hipError_t launch_tiles(const SealArgs *sa, const OpenArgs *oa, int G, const Til
     const uint32_t lds = kLdsPerCu;
 #define RG_TILES(GG)                                                                                          \
     if (L.debug_mode == 3) {                                                                                  \
-        if (sa) hipLaunchKernelGGL((tile_kernel<GG, false, true>), dim3(blocks), dim3(512), lds, s, a, b, tp); \
-        else hipLaunchKernelGGL((tile_kernel<GG, true, true>), dim3(blocks), dim3(512), lds, s, a, b, tp);     \
-    } else if (sa) hipLaunchKernelGGL((tile_kernel<GG, false>), dim3(blocks), dim3(512), lds, s, a, b, tp);   \
-    else hipLaunchKernelGGL((tile_kernel<GG, true>), dim3(blocks), dim3(512), lds, s, a, b, tp);
+        if (sa) hipLaunchKernelGGL((tile_kernel<GG, false, true>), dim3(blocks), dim3(threads), lds, s, a, b, tp); \
+        else hipLaunchKernelGGL((tile_kernel<GG, true, true>), dim3(blocks), dim3(threads), lds, s, a, b, tp);     \
+    } else if (sa) hipLaunchKernelGGL((tile_kernel<GG, false>), dim3(blocks), dim3(threads), lds, s, a, b, tp);   \
+    else hipLaunchKernelGGL((tile_kernel<GG, true>), dim3(blocks), dim3(threads), lds, s, a, b, tp);
     if (G == 1) {
         RG_TILES(1)
     } else {

@@ -71,7 +71,7 @@ def _gpu_open(engine, keys, desc_open, buf):
 # K lanes per packet, and the LDS-staged tile kernel with G-chunk windows,
 # the size-class planner on/off and 1/2/4 segments per packet (0 = automatic)
 MODES = [("lane", 1), ("lane", 2), ("lane", 4),
-         ("tile", 2, 1, 0), ("tile", 1, 1, 1), ("tile", 2, 1, 2), ("tile", 2, 1, 4),
+         ("tile", 2, 2, 0), ("tile", 2, 1, 0), ("tile", 1, 1, 1), ("tile", 2, 1, 2), ("tile", 2, 1, 4),
          ("tile", 2, 0, 1), ("tile", 2, 0, 2), ("tile", 1, 0, 4), ("tile", 1, 1, 0)]
 
 
@@ -83,14 +83,14 @@ def _configure(engine, mode):
     else:
         _, g, plan, k = mode
         engine.set_staged(g)
-        engine.set_plan(bool(plan))
+        engine.set_plan(plan)
         engine.set_segments(k)
 
 
 def _reset(engine):
     """library defaults"""
     engine.set_staged(2)
-    engine.set_plan(True)
+    engine.set_plan(2)
     engine.set_segments(0)
     engine.set_lanes_per_packet(0)
 

@@ -48,8 +48,8 @@ for s in "$@"; do
             python3 bench.py --workload $W --steps 5 --warmup 2 --cpu-seconds 0 ;;
     tiles)
         W=${RG_WORKLOAD:-cfg2}
-        for v in "p1k0:--plan 1" "p0k1:--plan 0 --segments 1" "p0k2:--plan 0 --segments 2" "p1k2:--plan 1 --segments 2" "p1k4:--plan 1 --segments 4" "g1p1:--staged 1 --plan 1" "p0k4:--plan 0 --segments 4"; do
-            name=${v%%:*}; flags=${v#*:}
+        for v in ${RG_TILES:-"auto:" "p1k0:--plan 1" "p0k1:--plan 0 --segments 1" "p1k1:--plan 1 --segments 1" "p1k2:--plan 1 --segments 2" "g1auto:--staged 1"}; do
+            name=${v%%:*}; flags=${v#*:}; flags=${flags//_/ }
             run tiles_${W}_$name 200 python bench.py --workload $W $flags --steps 20 --warmup 3 --cpu-seconds 0
         done
         grep -H '"value"' gpurun_out/tiles_${W}_*.log | python3 -c "import sys,json

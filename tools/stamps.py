@@ -26,7 +26,7 @@ eng.set_staged(args.staged)
 if args.wg_per_cu:
     eng.set_wg_per_cu(args.wg_per_cu)
 if args.plan >= 0:
-    eng.set_plan(bool(args.plan))
+    eng.set_plan(args.plan)
 eng.set_segments(args.segments)
 w = workloads.build(args.workload)
 b = DeviceBatch(eng, w)
@@ -53,6 +53,8 @@ for op in ("seal", "open"):
             torch.cuda.synchronize()
             eng.set_debug_mode(3)
     d = dbg.cpu().numpy().reshape(-1, 8)
+    os.makedirs("gpurun_out", exist_ok=True)
+    np.save(f"gpurun_out/stamps_raw_{args.workload}_{op}.npy", d)
     d = d[d[:, 6] == 1]
     names = ["setup", "store", "dma_issue", "dma_wait", "chunk", "tail"]
     tot = d[:, :6].sum(axis=1)
