@@ -27,8 +27,8 @@ for s in "$@"; do
     case $s in
     micro) run micro 120 tools/build/microbench ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    test) run pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
-    testall) run pytest_gpu 900 python -m pytest tests -m gpu -q ;;
+    test) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
+    testall) run pytest_gpu 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread ;;
     bench) run bench 400 python bench.py --steps 50 --warmup 10 --cpu-seconds 10 ;;
     benchq) run bench 300 python bench.py --steps 30 --warmup 5 --cpu-seconds 0 ;;
     bench_all)

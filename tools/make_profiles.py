@@ -27,7 +27,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def kind_of(name: str):
     """seal / open for the transport kernels, None otherwise."""
-    if "staged_kernel<" in name:
+    if "staged_kernel<" in name or "tile_kernel<" in name:
         args = name.split("<", 1)[1].split(">", 1)[0].split(",")
         return "open" if args[1].strip() == "true" else "seal"
     if "seal_kernel<" in name or "seal_tile" in name:
