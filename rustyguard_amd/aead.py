@@ -108,7 +108,8 @@ class Engine:
         check(self._L.rg_set_lanes_per_packet(self._h, lanes), "rg_set_lanes_per_packet")
 
     def set_staged(self, window_chunks: int):
-        """0 = lane-pass kernels; 1/2/4 = LDS-staged tile kernel with that window."""
+        """Kernel family: 0 = lane-pass kernels; 1/2 = LDS-staged tile kernel with that window;
+        3 = row kernel (wave-specialised ChaCha20 / Poly1305 waves)."""
         check(self._L.rg_set_staged(self._h, window_chunks), "rg_set_staged")
 
     def set_plan(self, mode):

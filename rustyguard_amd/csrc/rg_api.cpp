@@ -189,6 +189,7 @@ int rg_create(int device, rg_ctx **out) {
         hipError_t e = hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device);
         if (e == hipSuccess) e = rg::prepare_kernels(c->max_wg);
         if (e == hipSuccess) e = rg::prepare_tile_kernels();
+        if (e == hipSuccess) e = rg::prepare_row_kernels();
         if (e != hipSuccess) {
             delete c;
             return set_err(RG_EDEVICE, "kernel setup", e);
@@ -252,7 +253,7 @@ int rg_set_wg_per_cu(rg_ctx *ctx, int wg) {
 
 int rg_set_staged(rg_ctx *ctx, int g) {
     if (!ctx) return set_err(RG_EINVAL, "null context");
-    if (g != 0 && g != 1 && g != 2) return set_err(RG_EINVAL, "staged window must be 0, 1 or 2 chunks");
+    if (g < 0 || g > 3) return set_err(RG_EINVAL, "kernel must be 0 (lane-pass), 1/2 (tile windows) or 3 (rows)");
     ctx->staged_g = g;
     return RG_OK;
 }
@@ -315,6 +316,26 @@ static hipError_t launch_tiles_any(rg_ctx *ctx, const rg::SealArgs *sa, const rg
     const uint32_t n = sa ? sa->n : oa->n;
     rg::Launch L = L0;
     rg::TilePlan tp{};
+    if (L.staged_g == 3) { // row kernel: identity tiles, or the planner's lists for mixed sizes
+        bool plan = ctx->plan == 1;
+        if (ctx->plan == 2) {
+            hipError_t e = pb.reserve(n);
+            if (e != hipSuccess) return e;
+            plan = pb.want_plan();
+        }
+        if (plan) {
+            hipError_t e = pb.reserve(n);
+            if (e != hipSuccess) return e;
+            tp.counts = static_cast<uint32_t *>(pb.counts.p);
+            tp.lists = static_cast<uint32_t *>(pb.lists.p);
+            tp.cap = pb.cap;
+            tp.classes_out = pb.d_classes;
+            e = rg::launch_plan(sa ? sa->desc : oa->desc, n, oa != nullptr, tp, st);
+            if (e != hipSuccess) return e;
+        }
+        L.wg_per_cu = ctx->wg_per_cu > 0 ? ctx->wg_per_cu : 2;
+        return rg::launch_rows(sa, oa, tp, L, st);
+    }
     tp.target_lanes = (uint32_t)std::max(1, ctx->cus) * 256u; // one wave per SIMD
     tp.fixed_k = (uint32_t)ctx->segments;
     bool plan = ctx->plan == 1;

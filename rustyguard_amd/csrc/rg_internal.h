@@ -80,6 +80,11 @@ hipError_t launch_plan(const rg_pkt_desc *desc, uint32_t n, bool open, const Til
 hipError_t launch_tiles(const SealArgs *sa, const OpenArgs *oa, int G, const TilePlan &tp, const Launch &L,
                         hipStream_t s);
 hipError_t prepare_tile_kernels();
+// Row kernel (rg_rows.hip): wave-specialised workgroups over identity tiles
+// (tp.counts == nullptr) or the planner's size-class lists.
+constexpr uint32_t kRowMaxTilesWG = 2048; // tiles per workgroup (LDS row table)
+hipError_t launch_rows(const SealArgs *sa, const OpenArgs *oa, const TilePlan &tp, const Launch &L, hipStream_t s);
+hipError_t prepare_row_kernels();
 // sets the dynamic-LDS attribute and returns max resident workgroups per CU
 // for [seal, open][K = 1, 2, 4]
 hipError_t prepare_kernels(int max_wg[2][3]);

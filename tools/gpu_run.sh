@@ -101,11 +101,12 @@ for l in sys.stdin:
     f,j=l.split(':',1); d=json.loads(j); print(f.split('/')[-1], d['value'], d['seal_ms'], d['open_ms'])" ;;
     pmc_clock)
         W=${RG_WORKLOAD:-cfg2}
-        for v in "l1:--lanes 1 --staged 0" "l1m1:--lanes 1 --staged 0 --debug-mode 1" "l1m2:--lanes 1 --staged 0 --debug-mode 2" "l2:--lanes 2 --staged 0" "g2:--staged 2"; do
-            name=${v%%:*}; flags=${v#*:}
+        for v in ${RG_PMC_VARIANTS:-"l1:--lanes_1_--staged_0" "l1m1:--lanes_1_--staged_0_--debug-mode_1" "l1m2:--lanes_1_--staged_0_--debug-mode_2" "l2:--lanes_2_--staged_0" "g2:--staged_2"}; do
+            name=${v%%:*}; flags=${v#*:}; flags=${flags//_/ }
             run pmcclk_$name 240 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_WAVES SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY \
                 --kernel-trace --output-format csv -d gpurun_out/pmcclk_$name -o p -- python3 bench.py --workload $W $flags --steps 5 --warmup 2 --cpu-seconds 0 --no-graph
-        done ;;
+        done
+        python3 tools/pmc_clock.py gpurun_out/pmcclk_* ;;
     pmc_sq)
         W=${RG_PMC_WORKLOAD:-cfg2}
         run pmcsq_$W 240 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_WAVES SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY \

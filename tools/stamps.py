@@ -56,6 +56,26 @@ for op in ("seal", "open"):
     os.makedirs("gpurun_out", exist_ok=True)
     np.save(f"gpurun_out/stamps_raw_{args.workload}_{op}.npy", d)
     d = d[d[:, 6] == 1]
+    if args.staged == 3:
+        # row kernel: prologue, load issue (incl. waits), compute, barrier; kind 1 = ChaCha wave, 2 = Poly1305 wave
+        res = {}
+        for kind, kname in ((1, "chacha"), (2, "poly")):
+            x = d[d[:, 5] == kind]
+            if not len(x):
+                continue
+            tot = x[:, :4].sum(axis=1)
+            rt = x[:, 7].astype(np.float64) / 100e6
+            res[kname] = {"waves": int(len(x)), "cycles_per_wave_mean": float(tot.mean()),
+                          "wave_us_mean": round(float(rt.mean()) * 1e6, 2),
+                          "shader_clock_ghz": round(float(tot.sum() / rt.sum()) / 1e9, 3),
+                          "start_us_pct_0_50_90_100": [round(float(v), 2) for v in np.percentile(
+                              (x[:, 4] - d[:, 4].min()) / 100.0, [0, 50, 90, 100])],
+                          "end_us_pct_0_50_90_100": [round(float(v), 2) for v in np.percentile(
+                              (x[:, 4] + x[:, 7] - d[:, 4].min()) / 100.0, [0, 50, 90, 100])],
+                          "share": {n: round(float(x[:, k].sum() / tot.sum()), 4)
+                                    for k, n in enumerate(["prologue", "issue", "compute", "barrier"])}}
+        out[op] = res
+        continue
     names = ["setup", "store", "dma_issue", "dma_wait", "chunk", "tail"]
     tot = d[:, :6].sum(axis=1)
     rt = d[:, 7].astype(np.float64) / 100e6  # s_memrealtime ticks at 100 MHz
