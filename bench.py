@@ -55,6 +55,19 @@ def parse():
     return ap.parse_args()
 
 
+def kernel_label(args, eng, w) -> str:
+    if args.staged == 0:
+        return f"lane-pass, {eng.lanes_per_packet(w.n)} lanes/packet"
+    if args.staged == 3:
+        return f"rows (wave-specialised), planner {({0: 'off', 1: 'on'}).get(args.plan, 'auto')}"
+    if args.staged == 4:
+        return "pipelined lanes (1 packet/lane, 2-deep chunk prefetch, Poly1305 in keystream rounds)"
+    if args.staged == 5:
+        return "wave tiles (1 packet/lane, coalesced chunk I/O through a wave-private LDS transpose)"
+    return (f"lds-staged tiles, {args.staged if args.staged > 0 else 2} chunks/window, "
+            f"planner {({0: 'off', 1: 'on'}).get(args.plan, 'auto')}, segments {args.segments or 'auto'}")
+
+
 def cpu_baseline(w, seconds: float, threads: int, impl: str = "port"):
     """A CPU implementation timed on this host's cores over a bounded sample of the workload.
 
@@ -259,9 +272,7 @@ def main():
                    "payload_bytes_per_packet": int(w.desc["len"][0]) if w.n else 0,
                    "mean_payload_bytes": round(payload / max(w.n, 1), 2), "wire_bytes_per_gpu": w.wire_bytes,
                    "sessions": int(w.meta.get("sessions", 1)), "parallelism": f"split{world} (no collective)",
-                   "kernel": (f"lane-pass, {eng.lanes_per_packet(w.n)} lanes/packet" if args.staged == 0 else
-                              f"lds-staged tiles, {args.staged if args.staged > 0 else 2} chunks/window, "
-                              f"planner {({0: 'off', 1: 'on'}).get(args.plan, 'auto')}, segments {args.segments or 'auto'}"),
+                   "kernel": kernel_label(args, eng, w),
                    "wg_per_cu": args.wg_per_cu or "auto"},
         "mpkt_s": round(total_pkts / tmax / 1e6, 3),
         "seal_ms": round(seal_ms, 5),

@@ -151,6 +151,8 @@ struct rg_ctx {
     PlanBuf plan_dev; // planner lists of the device API (calls on one ctx are stream-ordered)
     uint64_t *dbg = nullptr; // diagnostics buffer (device), stamp builds only
     int max_wg[2][3] = {{0, 0, 0}, {0, 0, 0}}; // [seal, open][K = 1, 2, 4]
+    int pipe_max_wg[2] = {0, 0};                // [seal, open] pipelined lane kernel
+    int wave_max_wg[2] = {0, 0};                // [seal, open] wave-tile kernel
     std::mutex mu;
     Slot slots[2];
     DevBuf d_keys, d_recv;
@@ -190,6 +192,8 @@ int rg_create(int device, rg_ctx **out) {
         if (e == hipSuccess) e = rg::prepare_kernels(c->max_wg);
         if (e == hipSuccess) e = rg::prepare_tile_kernels();
         if (e == hipSuccess) e = rg::prepare_row_kernels();
+        if (e == hipSuccess) e = rg::prepare_pipe_kernels(c->pipe_max_wg);
+        if (e == hipSuccess) e = rg::prepare_wave_kernels(c->wave_max_wg);
         if (e != hipSuccess) {
             delete c;
             return set_err(RG_EDEVICE, "kernel setup", e);
@@ -253,7 +257,9 @@ int rg_set_wg_per_cu(rg_ctx *ctx, int wg) {
 
 int rg_set_staged(rg_ctx *ctx, int g) {
     if (!ctx) return set_err(RG_EINVAL, "null context");
-    if (g < 0 || g > 3) return set_err(RG_EINVAL, "kernel must be 0 (lane-pass), 1/2 (tile windows) or 3 (rows)");
+    if (g < 0 || g > 5)
+        return set_err(RG_EINVAL,
+                       "kernel must be 0 (lane-pass), 1/2 (tile windows), 3 (rows), 4 (pipelined lanes) or 5 (wave tiles)");
     ctx->staged_g = g;
     return RG_OK;
 }
@@ -280,7 +286,7 @@ int rg_set_debug_buffer(rg_ctx *ctx, void *dev_ptr) {
 
 int rg_set_debug_mode(rg_ctx *ctx, int mode) {
     if (!ctx) return set_err(RG_EINVAL, "null context");
-    if (mode < 0 || mode > 3) return set_err(RG_EINVAL, "debug mode must be 0..3");
+    if (mode < 0 || mode > 6) return set_err(RG_EINVAL, "debug mode must be 0..6");
     ctx->debug_mode = mode;
     return RG_OK;
 }
@@ -292,8 +298,11 @@ static rg::Launch launch_cfg(rg_ctx *ctx, size_t n, bool open) {
     L.debug_mode = open ? 0 : ctx->debug_mode;
     if (L.debug_mode == 3 && ctx->staged_g == 0) L.debug_mode = 0;
     L.staged_g = ctx->staged_g;
+    if (L.staged_g >= 4) L.lanes = 1;
     const int k = L.lanes == 1 ? 0 : L.lanes == 2 ? 1 : 2;
-    const int cap = std::max(1, ctx->max_wg[open ? 1 : 0][k]);
+    const int cap = std::max(1, L.staged_g == 4   ? ctx->pipe_max_wg[open ? 1 : 0]
+                                : L.staged_g == 5 ? ctx->wave_max_wg[open ? 1 : 0]
+                                                  : ctx->max_wg[open ? 1 : 0][k]);
     if (ctx->wg_per_cu < 0) {
         L.wg_per_cu = 0;
     } else if (ctx->wg_per_cu > 0) {
@@ -361,8 +370,11 @@ static hipError_t launch_tiles_any(rg_ctx *ctx, const rg::SealArgs *sa, const rg
 
 static hipError_t launch_seal_any(rg_ctx *ctx, const rg::SealArgs &a0, PlanBuf &pb, hipStream_t st) {
     rg::SealArgs a = a0;
-    a.dbg = ctx->debug_mode == 3 ? ctx->dbg : nullptr;
+    // stamps: debug mode 3, or any diagnostic mode of the pipelined kernel
+    a.dbg = ctx->debug_mode == 3 || (ctx->staged_g >= 4 && ctx->debug_mode != 0) ? ctx->dbg : nullptr;
     rg::Launch L = launch_cfg(ctx, a.n, false);
+    if (L.staged_g == 4) return rg::launch_pipe(&a, nullptr, L, st);
+    if (L.staged_g == 5) return rg::launch_wave(&a, nullptr, L, st);
     if (L.staged_g > 0 && (L.debug_mode == 0 || L.debug_mode == 3)) return launch_tiles_any(ctx, &a, nullptr, pb, L, st);
     return rg::launch_seal(a, L, st);
 }
@@ -372,6 +384,8 @@ static hipError_t launch_open_any(rg_ctx *ctx, const rg::OpenArgs &a0, PlanBuf &
     a.dbg = ctx->debug_mode == 3 ? ctx->dbg : nullptr;
     rg::Launch L = launch_cfg(ctx, a.n, true);
     L.debug_mode = ctx->debug_mode == 3 ? 3 : 0;
+    if (L.staged_g == 4) return rg::launch_pipe(nullptr, &a, L, st);
+    if (L.staged_g == 5) return rg::launch_wave(nullptr, &a, L, st);
     if (L.staged_g > 0) return launch_tiles_any(ctx, nullptr, &a, pb, L, st);
     return rg::launch_open(a, L, st);
 }

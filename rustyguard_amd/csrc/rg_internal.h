@@ -57,7 +57,7 @@ struct Launch {
     int cus;
     int wg_per_cu;
     int debug_mode; // diagnostics: 0 normal, 1/2 seal compute/memory only, 3 staged stamps
-    int staged_g;   // > 0: use the LDS-staged tile kernel with windows of this many chunks
+    int staged_g;   // kernel family: 0 lane-pass, 1/2 LDS-staged tiles (window chunks), 3 rows, 4 pipelined lanes, 5 wave tiles
 };
 constexpr uint32_t kLdsPerCu = 160u * 1024u;
 
@@ -85,6 +85,14 @@ hipError_t prepare_tile_kernels();
 constexpr uint32_t kRowMaxTilesWG = 2048; // tiles per workgroup (LDS row table)
 hipError_t launch_rows(const SealArgs *sa, const OpenArgs *oa, const TilePlan &tp, const Launch &L, hipStream_t s);
 hipError_t prepare_row_kernels();
+// Pipelined lane kernel (rg_pipe.hip): one packet per lane, double-buffered
+// chunk loads, Poly1305 absorbed inside the next chunk's keystream rounds.
+hipError_t launch_pipe(const SealArgs *sa, const OpenArgs *oa, const Launch &L, hipStream_t s);
+hipError_t prepare_pipe_kernels(int max_wg[2]); // [seal, open] resident 256-thread workgroups per CU
+// Wave-tile kernel (rg_wave.hip): one packet per lane, tiles of 64 packets moved
+// with coalesced loads / stores through a wave-private LDS transpose.
+hipError_t launch_wave(const SealArgs *sa, const OpenArgs *oa, const Launch &L, hipStream_t s);
+hipError_t prepare_wave_kernels(int max_wg[2]);
 // sets the dynamic-LDS attribute and returns max resident workgroups per CU
 // for [seal, open][K = 1, 2, 4]
 hipError_t prepare_kernels(int max_wg[2][3]);

@@ -1,0 +1,334 @@
+// rg_pipe.hip -- the pipelined lane kernel: batched WireGuard transport seal /
+// open, one packet per lane.  Replaces N x Core::chacha20poly1305_{enc,dec}
+// (rustyguard-crypto/src/prim.rs:179-201) as driven by EncryptionKey::encrypt
+// / DecryptionKey::decrypt (prim.rs:386-437), with the frame layout of
+// EncryptedMetadata::frame_in_place (rustyguard-core/src/lib.rs:450-470).
+//
+// Why this shape (measured, tools/microbench.hip): a ChaCha20 block costs
+// ~3800 cycles per wave at 1 wave/SIMD and ~3560 at 8 waves/SIMD, so one
+// packet per lane already runs the keystream near the VALU ceiling.  What the
+// plain lane kernel loses is (a) HBM latency -- its prefetch register copy at
+// the loop head makes the wave wait for chunk t+1 one keystream period after
+// issuing it -- and (b) the serial Poly1305 chain, whose multiply-carry
+// dependencies leave issue slots empty.  Here
+//  * two chunk buffers alternate (the loop is unrolled twice, nothing in flight
+//    is ever copied): chunk t+2 is requested as soon as chunk t is written, so
+//    a load has two keystream periods (~3 us) to arrive;
+//  * chunk t-1's four Poly1305 blocks are absorbed inside chunk t's keystream
+//    rounds (after double rounds 1, 3, 5, 7), where the ARX chains leave the
+//    multiply chain's latency covered;
+//  * payload loads of a packet are issued before its one-time-key block, so
+//    that block hides the first chunks' latency.
+// A partial last chunk (P % 64 != 0) runs after the loop with per-block
+// predicates; the last chunk's Poly1305 blocks are absorbed after it.
+#include "rg_device.h"
+#include "rg_internal.h"
+
+namespace rg {
+
+struct Chunk {
+    uint4 q0, q1, q2, q3;
+};
+
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+template <int NT> __device__ __forceinline__ uint4 ld16(const uint4 *p) {
+    if constexpr (NT & 1) {
+        const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(p));
+        return make_uint4(v.x, v.y, v.z, v.w);
+    } else return *p;
+}
+template <int NT> __device__ __forceinline__ void st16(uint4 *p, const uint4 &x) {
+    if constexpr (NT & 2) {
+        const v4u v = {x.x, x.y, x.z, x.w};
+        __builtin_nontemporal_store(v, reinterpret_cast<v4u *>(p));
+    } else *p = x;
+}
+
+// blocks of chunk t (of nb Poly1305 blocks), 0..4
+__device__ __forceinline__ uint32_t chunk_blocks(uint32_t nb, uint32_t t) {
+    const uint32_t b0 = 4 * t;
+    return nb > b0 ? (nb - b0 < 4 ? nb - b0 : 4) : 0;
+}
+
+// Branch-free chunk load: piece indices are clamped to the packet's last
+// 16-byte block (block 0 of an empty payload is the tag slot, also inside the
+// frame), so every lane issues the same four loads and the waitcnt pass can
+// count them exactly.
+template <int NT = 0>
+__device__ __forceinline__ void load_chunk(Chunk &c, const uint4 *pl, uint32_t t, uint32_t last) {
+    const uint32_t b = 4 * t;
+    c.q0 = ld16<NT>(pl + min(b + 0, last));
+    c.q1 = ld16<NT>(pl + min(b + 1, last));
+    c.q2 = ld16<NT>(pl + min(b + 2, last));
+    c.q3 = ld16<NT>(pl + min(b + 3, last));
+}
+
+__device__ __forceinline__ void absorb_chunk(Acc &h, const Chunk &c, const Mul &r, uint32_t cnt) {
+    acc_block_pred(h, c.q0, r, cnt > 0);
+    acc_block_pred(h, c.q1, r, cnt > 1);
+    acc_block_pred(h, c.q2, r, cnt > 2);
+    acc_block_pred(h, c.q3, r, cnt > 3);
+}
+
+// One step: keystream block t+1 -- with the previous chunk's four Poly1305
+// blocks (pi, always a full chunk) absorbed in its rounds when ABSORB -- XORed
+// into chunk t (buf) and stored; then chunk t+2 is requested into buf.  Full
+// steps store unconditionally: a store under a branch leaves the waitcnt pass
+// a path with fewer memory operations, and since vmcnt counts stores as well
+// as loads it would then also wait for the last step's stores to be acked.
+// TAIL: the partial last chunk (cnt < 4 blocks), predicated, no prefetch.
+// MODE (seal diagnostics, rg_set_debug_mode): 0 normal; 1 compute only (no
+// payload loads or stores, loop-carried fake data); 2 memory only (no
+// keystream and no Poly1305); 4/5/6 non-temporal loads / stores / both.
+template <bool OPEN, bool ABSORB, bool TAIL, int MODE = 0>
+__device__ __forceinline__ void pipe_step(uint4 *pl, const Stream &st, const Mul &r, Acc &h, Chunk &pi, Chunk &buf,
+                                          uint32_t t, uint32_t nb) {
+    uint32_t ks[16];
+    if constexpr (MODE == 2) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) ks[i] = t * 16 + i;
+        h.h0 ^= pi.q0.x ^ pi.q1.y ^ pi.q2.z ^ pi.q3.w;
+    } else stream_block_hooked(st, t + 1, ks, [&](int dr) {
+        if constexpr (ABSORB) {
+            if (dr == 1) acc_block(h, pi.q0, r);
+            if (dr == 3) acc_block(h, pi.q1, r);
+            if (dr == 5) acc_block(h, pi.q2, r);
+            if (dr == 7) acc_block(h, pi.q3, r);
+            if (dr % 2 == 1) pin_acc(h);
+        }
+    });
+    const Chunk x = {xor4(buf.q0, ks + 0), xor4(buf.q1, ks + 4), xor4(buf.q2, ks + 8), xor4(buf.q3, ks + 12)};
+    uint4 *dst = pl + 4 * t;
+    if constexpr (MODE == 1) {
+        pi = x;
+        buf.q0.x += t; buf.q1.y ^= t; buf.q2.z += h.h0; buf.q3.w ^= t; // fake next chunk, loop-carried
+        return;
+    }
+    constexpr int NT = MODE >= 4 ? MODE - 3 : 0;
+    if constexpr (TAIL) {
+        const uint32_t cnt = nb & 3u;
+        st16<NT>(dst + 0, x.q0); // cnt >= 1
+        if (cnt > 1) st16<NT>(dst + 1, x.q1);
+        if (cnt > 2) st16<NT>(dst + 2, x.q2);
+    } else {
+        st16<NT>(dst + 0, x.q0);
+        st16<NT>(dst + 1, x.q1);
+        st16<NT>(dst + 2, x.q2);
+        st16<NT>(dst + 3, x.q3);
+    }
+    pi = OPEN ? buf : x;
+    if constexpr (!TAIL) load_chunk<NT>(buf, pl, t + 2, nb - 1);
+}
+
+// Keystream XOR in place + Poly1305 over the ciphertext for one packet's nb
+// 16-byte blocks; b0 / b1 hold chunks 0 / 1 (loads already issued).  The
+// first step is peeled (nothing to absorb yet), so that every absorb inside
+// the loop is unconditional; chunk c always lives in buffer c % 2.
+template <bool OPEN, int MODE = 0>
+__device__ __forceinline__ Acc pipe_pass(uint4 *pl, const Stream &st, const Mul &r, uint32_t nb, Chunk &b0,
+                                         Chunk &b1) {
+    const uint32_t F = nb >> 2, bl = nb & 3u; // full chunks, blocks in the partial last chunk
+    Acc h = {0, 0, 0, 0, 0};
+    Chunk pi = {};
+    uint32_t pending = 0; // blocks of pi not yet absorbed
+    if (F > 0) {
+        pipe_step<OPEN, false, false, MODE>(pl, st, r, h, pi, b0, 0, nb);
+        uint32_t t = 1;
+        // whole pairs only: a step that may be skipped would leave the waitcnt
+        // pass a path without its memory operations (vmcnt(0) at the next one)
+        for (; t + 1 < F; t += 2) {
+            pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b1, t, nb);
+            pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b0, t + 1, nb);
+        }
+        if (t < F) pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b1, t, nb);
+        pending = 4;
+    }
+    if (bl > 0) {
+        Chunk &bp = (F & 1u) ? b1 : b0;
+        if (F > 0) pipe_step<OPEN, true, true, MODE>(pl, st, r, h, pi, bp, F, nb);
+        else pipe_step<OPEN, false, true, MODE>(pl, st, r, h, pi, bp, F, nb);
+        pending = bl;
+    }
+    absorb_chunk(h, pi, r, pending); // the last chunk's blocks
+    return h;
+}
+
+// tag = ((h + lenblock) r mod p) + s; length block le64(aad_len = 0) || le64(P) (RFC 8439 §2.8)
+__device__ __forceinline__ void pipe_tag(Acc h, const Mul &r, uint32_t P, const uint32_t *s, uint32_t tag[4]) {
+    acc_add(h, 0, 0, P, 0, 1);
+    acc_mul(h, r);
+    acc_finish(h, s[0], s[1], s[2], s[3], tag);
+}
+
+// ------------------------------------------------------------------ seal
+// Frame: [hdr 16][payload P][tag 16]; desc.len = P.  Checks as seal_packet
+// (rg_kernels.hip): descriptor and force_encrypt's padding assert
+// (rustyguard-core/src/lib.rs:273-277).
+template <int MODE> __device__ __forceinline__ void pipe_seal_packet(const SealArgs &a, uint32_t i) {
+    const rg_pkt_desc d = a.desc[i];
+    const uint32_t P = d.len;
+    const bool valid = d.key_idx < a.nkeys && (P & 15u) == 0 && (d.offset & 15u) == 0 && P <= kMaxPayload &&
+                       d.offset <= a.buf_len && P + 32 <= a.buf_len - d.offset;
+    if (!valid) {
+        if (a.status) a.status[i] = d.key_idx == RG_KEY_SKIP ? RG_PKT_REJECTED : RG_PKT_INVALID;
+        return;
+    }
+    uint8_t *frame = a.buf + d.offset;
+    uint4 *pl = reinterpret_cast<uint4 *>(frame + 16);
+    const uint32_t nb = P >> 4;
+    Chunk b0, b1;
+    if constexpr (MODE == 1) {
+        b0 = {make_uint4(i, 1, 2, 3), make_uint4(4, i, 6, 7), make_uint4(8, 9, i, 11), make_uint4(12, 13, 14, i)};
+        b1 = b0;
+    } else {
+        constexpr int NT = MODE >= 4 ? MODE - 3 : 0;
+        load_chunk<NT>(b0, pl, 0, nb ? nb - 1 : 0);
+        load_chunk<NT>(b1, pl, 1, nb ? nb - 1 : 0);
+    }
+    const Key8 key = load_key(a.keys, d.key_idx);
+    const uint64_t ctr = a.counters[i];
+    const uint32_t n1 = (uint32_t)ctr, n2 = (uint32_t)(ctr >> 32); // nonce = 0 || le64(ctr) (prim.rs:32-36)
+    const Stream stm = make_stream(key, 0u, n1, n2);
+    uint32_t ks[16];
+    stream_block(stm, 0, ks); // RFC 8439 §2.6 one-time key
+    const Mul r = make_mul(ks[0], ks[1], ks[2], ks[3]);
+    const Acc h = pipe_pass<false, MODE>(pl, stm, r, nb, b0, b1);
+    uint32_t tag[4];
+    pipe_tag(h, r, P, ks + 4, tag);
+    if (a.receivers) // DataHeader {4, receiver, counter} (rustyguard-core/src/lib.rs:286-290)
+        *reinterpret_cast<uint4 *>(frame) = make_uint4(4u, a.receivers[d.key_idx], n1, n2);
+    *reinterpret_cast<uint4 *>(frame + 16 + P) = make_uint4(tag[0], tag[1], tag[2], tag[3]);
+    if (a.status) a.status[i] = RG_PKT_OK;
+}
+
+// ------------------------------------------------------------------ open
+// desc.len = W.  Checks mirror rustyguard-core/src/lib.rs:613-629,
+// rustyguard-types/src/lib.rs:181-196 and rustyguard-crypto/src/prim.rs:
+// 427-429.  Decrypts speculatively while MACing the ciphertext; a failed tag
+// (constant-time compare) re-applies the keystream, so the frame is left
+// unchanged.
+__device__ __forceinline__ void pipe_open_packet(const OpenArgs &a, uint32_t i) {
+    const rg_pkt_desc d = a.desc[i];
+    const uint32_t W = d.len;
+    uint32_t st;
+    if (d.key_idx == RG_KEY_SKIP) st = RG_PKT_REJECTED;
+    else if ((d.offset & 15u) != 0) st = RG_PKT_UNALIGNED;
+    else if (d.key_idx >= a.nkeys || W > kMaxPayload + 32 || d.offset > a.buf_len || W > a.buf_len - d.offset ||
+             W < 4)
+        st = RG_PKT_INVALID;
+    else st = 0xFF;
+    uint8_t *frame = a.buf + d.offset;
+    uint64_t ctr = 0;
+    if (st == 0xFF) {
+        const uint4 hdr = *reinterpret_cast<const uint4 *>(frame);
+        if (hdr.x != 4u) st = RG_PKT_NOT_DATA;
+        else if ((W & 15u) != 0 || W < 16) st = RG_PKT_INVALID;
+        else {
+            ctr = ((uint64_t)hdr.w << 32) | hdr.z;
+            if (W < 32) st = RG_PKT_DECRYPT_ERR;
+        }
+    }
+    if (st != 0xFF) {
+        a.status[i] = (uint8_t)st;
+        if (a.counters_out) a.counters_out[i] = ctr;
+        return;
+    }
+    const uint32_t P = W - 32;
+    uint4 *pl = reinterpret_cast<uint4 *>(frame + 16);
+    const uint32_t nb = P >> 4;
+    Chunk b0, b1;
+    load_chunk(b0, pl, 0, nb ? nb - 1 : 0);
+    load_chunk(b1, pl, 1, nb ? nb - 1 : 0);
+    const uint4 want = *reinterpret_cast<const uint4 *>(frame + 16 + P);
+    const Key8 key = load_key(a.keys, d.key_idx);
+    const uint32_t n1 = (uint32_t)ctr, n2 = (uint32_t)(ctr >> 32);
+    const Stream stm = make_stream(key, 0u, n1, n2);
+    uint32_t ks[16];
+    stream_block(stm, 0, ks);
+    const Mul r = make_mul(ks[0], ks[1], ks[2], ks[3]);
+    const Acc h = pipe_pass<true>(pl, stm, r, nb, b0, b1);
+    uint32_t tag[4];
+    pipe_tag(h, r, P, ks + 4, tag);
+    const uint32_t diff = (tag[0] ^ want.x) | (tag[1] ^ want.y) | (tag[2] ^ want.z) | (tag[3] ^ want.w);
+    if (diff != 0) {
+        // restore: plaintext ^ keystream = ciphertext (callers never read the
+        // buffer on Err, but the frame is left as it came)
+        for (uint32_t c = 0; 4 * c < nb; ++c) {
+            stream_block(stm, c + 1, ks);
+            const uint32_t cnt = chunk_blocks(nb, c);
+            for (uint32_t q = 0; q < cnt; ++q) pl[4 * c + q] = xor4(pl[4 * c + q], ks + 4 * q);
+        }
+    }
+    a.status[i] = diff == 0 ? RG_PKT_OK : RG_PKT_DECRYPT_ERR;
+    if (a.counters_out) a.counters_out[i] = ctr;
+}
+
+// ------------------------------------------------------------- kernels
+// Persistent grid as seal_kernel<1> (rg_kernels.hip): the host launches at most
+// CUs x wg_per_cu workgroups with an LDS reservation that fixes residency.
+// With a diagnostics buffer (debug mode 3) lane 0 of every wave records
+// [s_memtime delta, 0, 0, 0, start s_memrealtime, 4, 1, s_memrealtime delta]
+// (tools/stamps.py; s_memrealtime ticks at 100 MHz).
+__device__ __forceinline__ void pipe_stamp(uint64_t *dbg, uint64_t t0, uint64_t r0) {
+    const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    if ((threadIdx.x & 63) == 0) {
+        uint64_t *o = dbg + 8ull * (blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64);
+        o[0] = t1 - t0; o[1] = 0; o[2] = 0; o[3] = 0;
+        o[4] = r0; o[5] = 4; o[6] = 1; o[7] = r1 - r0;
+    }
+}
+
+template <int MODE> __global__ __launch_bounds__(256) void pipe_seal_kernel(SealArgs a) {
+    const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+    const uint32_t stride = gridDim.x * 256;
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < a.n; i += stride) pipe_seal_packet<MODE>(a, i);
+    if (a.dbg) pipe_stamp(a.dbg, t0, r0);
+}
+
+__global__ __launch_bounds__(256) void pipe_open_kernel(OpenArgs a) {
+    const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+    const uint32_t stride = gridDim.x * 256;
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < a.n; i += stride) pipe_open_packet(a, i);
+    if (a.dbg) pipe_stamp(a.dbg, t0, r0);
+}
+
+static void pipe_grid(uint32_t n, const Launch &L, uint32_t &blocks, uint32_t &lds) {
+    const uint64_t want = ((uint64_t)n + 255) / 256;
+    const uint64_t cap = (uint64_t)L.cus * (uint64_t)L.wg_per_cu;
+    blocks = (uint32_t)(want < cap || cap == 0 ? want : cap);
+    lds = L.wg_per_cu > 0 ? (kLdsPerCu / L.wg_per_cu) & ~255u : 0;
+}
+
+hipError_t launch_pipe(const SealArgs *sa, const OpenArgs *oa, const Launch &L, hipStream_t s) {
+    const uint32_t n = sa ? sa->n : oa->n;
+    if (n == 0) return hipSuccess;
+    uint32_t blocks, lds;
+    pipe_grid(n, L, blocks, lds);
+    if (sa && L.debug_mode == 1) hipLaunchKernelGGL(pipe_seal_kernel<1>, dim3(blocks), dim3(256), lds, s, *sa);
+    else if (sa && L.debug_mode == 2) hipLaunchKernelGGL(pipe_seal_kernel<2>, dim3(blocks), dim3(256), lds, s, *sa);
+    else if (sa && L.debug_mode == 4) hipLaunchKernelGGL(pipe_seal_kernel<4>, dim3(blocks), dim3(256), lds, s, *sa);
+    else if (sa && L.debug_mode == 5) hipLaunchKernelGGL(pipe_seal_kernel<5>, dim3(blocks), dim3(256), lds, s, *sa);
+    else if (sa && L.debug_mode == 6) hipLaunchKernelGGL(pipe_seal_kernel<6>, dim3(blocks), dim3(256), lds, s, *sa);
+    else if (sa) hipLaunchKernelGGL(pipe_seal_kernel<0>, dim3(blocks), dim3(256), lds, s, *sa);
+    else hipLaunchKernelGGL(pipe_open_kernel, dim3(blocks), dim3(256), lds, s, *oa);
+    return hipGetLastError();
+}
+
+hipError_t prepare_pipe_kernels(int max_wg[2]) {
+    const void *f[7] = {(const void *)pipe_seal_kernel<0>, (const void *)pipe_open_kernel,
+                        (const void *)pipe_seal_kernel<1>, (const void *)pipe_seal_kernel<2>,
+                        (const void *)pipe_seal_kernel<4>, (const void *)pipe_seal_kernel<5>,
+                        (const void *)pipe_seal_kernel<6>};
+    for (int w = 0; w < 7; ++w) {
+        hipError_t e = hipFuncSetAttribute(f[w], hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsPerCu);
+        if (e != hipSuccess) return e;
+        int nb = 0;
+        if (w >= 2) continue;
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f[w], 256, 0);
+        if (e != hipSuccess) return e;
+        max_wg[w] = nb;
+    }
+    return hipSuccess;
+}
+
+} // namespace rg

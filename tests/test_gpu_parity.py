@@ -70,14 +70,18 @@ def _gpu_open(engine, keys, desc_open, buf):
 # kernel configurations every parity test runs under: lane-pass kernels with
 # K lanes per packet, and the LDS-staged tile kernel with G-chunk windows,
 # the size-class planner on/off and 1/2/4 segments per packet (0 = automatic)
-MODES = [("rows",), ("lane", 1), ("lane", 2), ("lane", 4),
+MODES = [("wave",), ("pipe",), ("rows",), ("lane", 1), ("lane", 2), ("lane", 4),
          ("tile", 2, 2, 0), ("tile", 2, 1, 0), ("tile", 1, 1, 1), ("tile", 2, 1, 2), ("tile", 2, 1, 4),
          ("tile", 2, 0, 1), ("tile", 2, 0, 2), ("tile", 1, 0, 4), ("tile", 1, 1, 0)]
 
 
 def _configure(engine, mode):
     _reset(engine)
-    if mode[0] == "rows":
+    if mode[0] == "wave":
+        engine.set_staged(5)
+    elif mode[0] == "pipe":
+        engine.set_staged(4)
+    elif mode[0] == "rows":
         engine.set_staged(3)
     elif mode[0] == "lane":
         engine.set_staged(0)
@@ -98,8 +102,8 @@ def _reset(engine):
 
 
 def _mode_id(m):
-    if m[0] == "rows":
-        return "rows"
+    if m[0] in ("rows", "pipe", "wave"):
+        return m[0]
     return f"lane{m[1]}" if m[0] == "lane" else f"tile_g{m[1]}_p{m[2]}_k{m[3]}"
 
 

@@ -26,6 +26,7 @@ run() { # name timeout cmd...
 for s in "$@"; do
     case $s in
     micro) run micro 120 tools/build/microbench ;;
+    mempat) run mempat 120 tools/build/mempattern ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     test) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
     testall) run pytest_gpu 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread ;;

@@ -160,6 +160,97 @@ __global__ void k_chacha2(uint32_t *out, uint32_t seed) {
     out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
 }
 
+// ChaCha variants with different rotate lowerings (same arithmetic):
+//  P: rot16 / rot8 as v_perm_b32 byte shuffles (rot12 / rot7 stay v_alignbit_b32)
+//  S: xor + rot16 as two SDWA word-select xors, rot8 as v_perm_b32
+__device__ __forceinline__ uint32_t perm_rot16(uint32_t v) { return __builtin_amdgcn_perm(v, v, 0x01000302u); }
+__device__ __forceinline__ uint32_t perm_rot8(uint32_t v) { return __builtin_amdgcn_perm(v, v, 0x02010003u); }
+__device__ __forceinline__ uint32_t xor_rot16_sdwa(uint32_t d, uint32_t a) {
+    uint32_t t;
+    asm volatile("v_xor_b32_sdwa %0, %1, %2 dst_sel:WORD_1 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_0\n\t"
+                 "v_xor_b32_sdwa %0, %1, %2 dst_sel:WORD_0 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 src1_sel:WORD_1"
+                 : "=&v"(t) : "v"(d), "v"(a));
+    return t;
+}
+#define QR_P(a, b, c, d)                                   \
+    a += b; d ^= a; d = perm_rot16(d);                      \
+    c += d; b ^= c; b = rg::rotl(b, 12);                    \
+    a += b; d ^= a; d = perm_rot8(d);                       \
+    c += d; b ^= c; b = rg::rotl(b, 7);
+#define QR_S(a, b, c, d)                                   \
+    a += b; d = xor_rot16_sdwa(d, a);                       \
+    c += d; b ^= c; b = rg::rotl(b, 12);                    \
+    a += b; d ^= a; d = perm_rot8(d);                       \
+    c += d; b ^= c; b = rg::rotl(b, 7);
+#define CHACHA_VARIANT(NAME, QR)                                                       \
+    __global__ void NAME(uint32_t *out, uint32_t seed) {                               \
+        uint32_t k[8];                                                                 \
+        for (int i = 0; i < 8; ++i) k[i] = seed * (i + 1) + threadIdx.x;              \
+        uint32_t acc = 0;                                                              \
+        for (int blk = 0; blk < CHACHA_BLOCKS; ++blk) {                                \
+            uint32_t x0 = 0x61707865u, x1 = 0x3320646eu, x2 = 0x79622d32u, x3 = 0x6b206574u; \
+            uint32_t x4 = k[0], x5 = k[1], x6 = k[2], x7 = k[3], x8 = k[4], x9 = k[5], x10 = k[6], x11 = k[7]; \
+            uint32_t x12 = blk + 1, x13 = 0, x14 = threadIdx.x, x15 = blockIdx.x;       \
+            _Pragma("unroll") for (int i = 0; i < 10; i++) {                           \
+                QR(x0, x4, x8, x12) QR(x1, x5, x9, x13) QR(x2, x6, x10, x14) QR(x3, x7, x11, x15) \
+                QR(x0, x5, x10, x15) QR(x1, x6, x11, x12) QR(x2, x7, x8, x13) QR(x3, x4, x9, x14) \
+            }                                                                          \
+            acc ^= (x0 + 0x61707865u) ^ (x1 + 0x3320646eu) ^ (x2 + 0x79622d32u) ^ (x3 + 0x6b206574u) ^ \
+                   (x4 + k[0]) ^ (x5 + k[1]) ^ (x6 + k[2]) ^ (x7 + k[3]) ^ (x8 + k[4]) ^ (x9 + k[5]) ^ \
+                   (x10 + k[6]) ^ (x11 + k[7]) ^ (x12 + blk + 1) ^ x13 ^ (x14 + threadIdx.x) ^ (x15 + blockIdx.x); \
+        }                                                                              \
+        out[blockIdx.x * blockDim.x + threadIdx.x] = acc;                              \
+    }
+CHACHA_VARIANT(k_chacha_perm, QR_P)
+CHACHA_VARIANT(k_chacha_sdwa, QR_S)
+
+// Quad ChaCha: 4 lanes per block, lane j holds column j (rows a, b, c, d =
+// words j, 4+j, 8+j, 12+j); diagonal rounds rotate rows b, c, d across the
+// quad with DPP quad_perm.  CHACHA_BLOCKS blocks per quad (so 4x the lanes of
+// k_chacha for the same number of blocks).
+template <int CTRL> __device__ __forceinline__ uint32_t qrot(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
+}
+#define QCTRL_L1 0x39 // lane j <- j+1
+#define QCTRL_L2 0x4E // lane j <- j+2
+#define QCTRL_L3 0x93 // lane j <- j+3
+#define QQR(a, b, c, d)                                   \
+    a += b; d ^= a; d = rg::rotl(d, 16);                   \
+    c += d; b ^= c; b = rg::rotl(b, 12);                   \
+    a += b; d ^= a; d = rg::rotl(d, 8);                    \
+    c += d; b ^= c; b = rg::rotl(b, 7);
+template <int ILP> __global__ void k_chacha_quad(uint32_t *out, uint32_t seed) {
+    const uint32_t j = threadIdx.x & 3;
+    const uint32_t k0 = seed * (j + 1) + threadIdx.x, k1 = seed * (j + 5) + threadIdx.x;
+    const uint32_t a0 = 0x61707865u + j * 0x01010101u;
+    uint32_t acc = 0;
+    for (int blk = 0; blk < CHACHA_BLOCKS; blk += ILP) {
+        uint32_t a[ILP], b[ILP], c[ILP], d[ILP];
+#pragma unroll
+        for (int u = 0; u < ILP; ++u) {
+            a[u] = a0; b[u] = k0; c[u] = k1; d[u] = j == 0 ? (uint32_t)(blk + u + 1) : (j == 1 ? 0u : blockIdx.x + j);
+        }
+#pragma unroll
+        for (int i = 0; i < 10; i++) {
+#pragma unroll
+            for (int u = 0; u < ILP; ++u) { QQR(a[u], b[u], c[u], d[u]) }
+#pragma unroll
+            for (int u = 0; u < ILP; ++u) {
+                b[u] = qrot<QCTRL_L1>(b[u]); c[u] = qrot<QCTRL_L2>(c[u]); d[u] = qrot<QCTRL_L3>(d[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < ILP; ++u) { QQR(a[u], b[u], c[u], d[u]) }
+#pragma unroll
+            for (int u = 0; u < ILP; ++u) {
+                b[u] = qrot<QCTRL_L3>(b[u]); c[u] = qrot<QCTRL_L2>(c[u]); d[u] = qrot<QCTRL_L1>(d[u]);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < ILP; ++u) acc ^= (a[u] + a0) ^ (b[u] + k0) ^ (c[u] + k1) ^ d[u];
+    }
+    out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
+}
+
 // ChaCha with an in-kernel clock stamp: lane 0 of each wave records
 // (s_memtime delta, s_memrealtime delta) into clk[wave] (100 MHz real-time).
 __global__ void k_chacha_clk(uint32_t *out, uint32_t seed, unsigned long long *clk) {
@@ -313,6 +404,8 @@ int main() {
         kfn f;
         double units;
     } ku[] = {{"chacha_block", k_chacha, CHACHA_BLOCKS}, {"chacha_block_x2", k_chacha2, CHACHA_BLOCKS},
+              {"chacha_perm_rot", k_chacha_perm, CHACHA_BLOCKS},
+              {"chacha_quad_ilp1", k_chacha_quad<1>, CHACHA_BLOCKS / 4.0}, {"chacha_quad_ilp2", k_chacha_quad<2>, CHACHA_BLOCKS / 4.0}, {"chacha_sdwa_rot16", k_chacha_sdwa, CHACHA_BLOCKS},
               {"poly_clamped_block", k_poly, POLY_BLOCKS},
               {"poly_general_block", k_polygen, POLY_BLOCKS}};
     for (auto &k : ku) {
@@ -320,7 +413,7 @@ int main() {
             double r = run_units(k.f, w, d, k.units);
             printf("%s{\"kernel\": \"%s\", \"waves_per_simd\": %d, \"per_ns_per_cu\": %.4f, "
                    "\"chip_GB_s\": %.1f}\n", first ? "" : ",", k.name, w, r,
-                   r * 256 * ((k.f == k_chacha || k.f == k_chacha2) ? 64 : 16));
+                   r * 256 * ((k.f == k_chacha || k.f == k_chacha2 || k.f == k_chacha_perm || k.f == k_chacha_sdwa || k.f == k_chacha_quad<1> || k.f == k_chacha_quad<2>) ? 64 : 16));
             first = false;
         }
     }

@@ -20,6 +20,7 @@ ap.add_argument("--staged", type=int, default=2)
 ap.add_argument("--wg-per-cu", type=int, default=0)
 ap.add_argument("--plan", type=int, default=-1)
 ap.add_argument("--segments", type=int, default=0)
+ap.add_argument("--mode", type=int, default=3, help="seal debug mode while stamping (pipelined kernel: 1/2/4/5/6 too)")
 args = ap.parse_args()
 eng = Engine(0)
 eng.set_staged(args.staged)
@@ -33,7 +34,7 @@ b = DeviceBatch(eng, w)
 b.fill()
 dbg = torch.zeros(8 * 256 * 32, dtype=torch.int64, device="cuda")
 eng.set_debug_buffer(dbg)
-eng.set_debug_mode(3)
+eng.set_debug_mode(args.mode)
 out = {}
 for op in ("seal", "open"):
     for rep in range(3):
@@ -43,7 +44,7 @@ for op in ("seal", "open"):
             eng.set_debug_mode(0)
             b.seal()
             torch.cuda.synchronize()
-            eng.set_debug_mode(3)
+            eng.set_debug_mode(args.mode)
         dbg.zero_()
         b.seal() if op == "seal" else b.open()
         torch.cuda.synchronize()
@@ -51,11 +52,24 @@ for op in ("seal", "open"):
             eng.set_debug_mode(0)
             b.open()  # restore plaintext so each seal starts from the same state
             torch.cuda.synchronize()
-            eng.set_debug_mode(3)
+            eng.set_debug_mode(args.mode)
     d = dbg.cpu().numpy().reshape(-1, 8)
     os.makedirs("gpurun_out", exist_ok=True)
     np.save(f"gpurun_out/stamps_raw_{args.workload}_{op}.npy", d)
     d = d[d[:, 6] == 1]
+    if not len(d):  # no stamps for this op in this mode
+        continue
+    if args.staged == 4:
+        # pipelined lane kernel: whole-wave cycles and wall time, start / end spread
+        tot = d[:, 0].astype(np.float64)
+        rt = d[:, 7].astype(np.float64) / 100e6
+        t0 = d[:, 4].min()
+        out[op] = {"waves": int(len(d)), "cycles_per_wave_mean": float(tot.mean()),
+                   "wave_us_pct_0_10_50_90_100": [round(float(v), 2) for v in np.percentile(rt * 1e6, [0, 10, 50, 90, 100])],
+                   "shader_clock_ghz": round(float(tot.sum() / rt.sum()) / 1e9, 3),
+                   "start_us_pct_0_50_90_100": [round(float(v), 2) for v in np.percentile((d[:, 4] - t0) / 100.0, [0, 50, 90, 100])],
+                   "end_us_pct_0_50_90_100": [round(float(v), 2) for v in np.percentile((d[:, 4] + d[:, 7] - t0) / 100.0, [0, 50, 90, 100])]}
+        continue
     if args.staged == 3:
         # row kernel: prologue, load issue (incl. waits), compute, barrier; kind 1 = ChaCha wave, 2 = Poly1305 wave
         res = {}
