@@ -42,7 +42,8 @@ def parse():
     ap.add_argument("--workload", default="cfg2", choices=["cfg2", "cfg3", "cfg4", "cfg5"])
     ap.add_argument("--lanes", type=int, default=0, help="lanes per packet (0 = auto)")
     ap.add_argument("--wg-per-cu", type=int, default=0, help="resident workgroups per CU (0 = auto, -1 = plain grid)")
-    ap.add_argument("--staged", type=int, default=-1, help="LDS-staged window chunks (0 = lane-pass kernels, -1 = default)")
+    ap.add_argument("--staged", type=int, default=-1,
+                    help="kernel: -1 automatic (default), 0 pipelined lanes, 1/2 LDS-staged tiles with that window")
     ap.add_argument("--plan", type=int, default=-1, help="size-class planner: 0 off, 1 on, 2 auto, -1 library default (auto)")
     ap.add_argument("--segments", type=int, default=0, help="segments per packet for the tile kernels (0 = auto)")
     ap.add_argument("--debug-mode", type=int, default=0, help="seal diagnostics (invalid output): 1 compute-only, 2 memory-only")
@@ -56,16 +57,12 @@ def parse():
 
 
 def kernel_label(args, eng, w) -> str:
-    if args.staged == 0:
-        return f"lane-pass, {eng.lanes_per_packet(w.n)} lanes/packet"
-    if args.staged == 3:
-        return f"rows (wave-specialised), planner {({0: 'off', 1: 'on'}).get(args.plan, 'auto')}"
-    if args.staged == 4:
-        return "pipelined lanes (1 packet/lane, 2-deep chunk prefetch, Poly1305 in keystream rounds)"
-    if args.staged == 5:
-        return "wave tiles (1 packet/lane, coalesced chunk I/O through a wave-private LDS transpose)"
-    return (f"lds-staged tiles, {args.staged if args.staged > 0 else 2} chunks/window, "
-            f"planner {({0: 'off', 1: 'on'}).get(args.plan, 'auto')}, segments {args.segments or 'auto'}")
+    k = eng.kernel_for(w.n)
+    plan = ({0: "off", 1: "on"}).get(args.plan, "auto")
+    if k == 0:
+        return (f"pipelined lanes ({eng.lanes_per_packet(w.n)} lane(s)/packet without plan, 2-deep chunk prefetch, "
+                f"Poly1305 in keystream rounds), planner {plan}")
+    return f"lds-staged tiles, {k} chunks/window, planner {plan}, segments {args.segments or 'auto'}"
 
 
 def cpu_baseline(w, seconds: float, threads: int, impl: str = "port"):
@@ -149,7 +146,7 @@ def main():
         eng.set_wg_per_cu(args.wg_per_cu)
     if args.debug_mode:
         eng.set_debug_mode(args.debug_mode)
-    if args.staged >= 0:
+    if args.staged != -1:
         eng.set_staged(args.staged)
     if args.plan >= 0:
         eng.set_plan(args.plan)

@@ -111,12 +111,18 @@ int rg_open_batch_dev(rg_ctx *ctx, const uint8_t *keys, uint32_t nkeys, const rg
 int rg_set_lanes_per_packet(rg_ctx *ctx, int lanes);
 int rg_get_lanes_per_packet(rg_ctx *ctx, size_t n);
 int rg_set_wg_per_cu(rg_ctx *ctx, int wg_per_cu);
-/* Kernel choice: 0 = lane-pass kernels (K lanes per packet, direct loads),
- * 1/2 = LDS-staged tiles (one packet (segment) per lane, coalesced LDS-DMA
- * windows of that many 64-byte chunks; default 2). */
-int rg_set_staged(rg_ctx *ctx, int window_chunks);
-/* Tile kernels: a device-side planner can first sort the batch into size
- * classes so that every 64-packet tile holds packets of similar length.
+/* Kernel choice: -1 (default) = automatic by batch size (rg_get_kernel);
+ * 0 = pipelined lane kernel (one packet -- or one of lanes_per_packet
+ * contiguous segments -- per lane, 2-deep register prefetch, Poly1305 folded
+ * into the keystream rounds); 1/2 = LDS-staged tiles (one packet (segment) per
+ * lane, coalesced LDS-DMA windows of that many 64-byte chunks). */
+int rg_set_staged(rg_ctx *ctx, int kernel);
+/* The kernel family a batch of n packets runs on (0, 1 or 2; see above). */
+int rg_get_kernel(rg_ctx *ctx, size_t n);
+/* A device-side planner can first sort the batch into size classes so that
+ * every 64-lane tile holds packets of similar length (both kernel families;
+ * the pipelined kernel then also picks segments per class from the batch's
+ * mean work and deals tiles longest first).
  * 0 = off (tiles take packets in array order), 1 = always, 2 (default) =
  * auto: plan unless the last planned batch of this context held a single size
  * class (re-checked every 32nd call).  Results are identical in every mode.
@@ -129,12 +135,15 @@ int rg_set_plan(rg_ctx *ctx, int on);
  * many contiguous segments on separate waves (Poly1305 partial sums combined
  * as sum_j A_j r^{N_j}). */
 int rg_set_segments(rg_ctx *ctx, int segments);
-/* Diagnostics only (profiling the seal kernel, output is NOT a valid seal):
- * 0 = normal, 1 = compute only (no payload loads/stores), 2 = memory only. */
+/* Diagnostics only (profiling the seal kernel, output is NOT a valid seal in
+ * modes 1, 2, 4-6): 0 = normal, 1 = compute only (no payload loads/stores),
+ * 2 = memory only, 3 = stamps, 4/5/6 = non-temporal loads / stores / both
+ * (pipelined kernel). */
 int rg_set_debug_mode(rg_ctx *ctx, int mode);
-/* mode 3 (staged kernels): per-wave s_memtime section totals are written to
- * this device buffer, 8 x u64 per wave (setup, store, dma-issue, dma-wait,
- * chunk, tail, valid, real-time ticks at 100 MHz). */
+/* Per-wave s_memtime stamps are written to this device buffer, 8 x u64 per
+ * wave: mode 3 on the tile kernels (setup, store, dma-issue, dma-wait, chunk,
+ * tail, valid, real-time ticks at 100 MHz); any non-zero mode on the
+ * pipelined kernel (cycles, 0, 0, 0, start tick, 4, valid, real-time ticks). */
 int rg_set_debug_buffer(rg_ctx *ctx, void *dev_ptr);
 
 /* ----------------------------------------- host-memory batch (blocking) */

@@ -33,6 +33,7 @@ SIGNATURES = {
     "rg_set_wg_per_cu": (c_int, [c_vp, c_int]),
     "rg_set_debug_mode": (c_int, [c_vp, c_int]),
     "rg_set_staged": (c_int, [c_vp, c_int]),
+    "rg_get_kernel": (c_int, [c_vp, c_size]),
     "rg_set_plan": (c_int, [c_vp, c_int]),
     "rg_set_segments": (c_int, [c_vp, c_int]),
     "rg_set_debug_buffer": (c_int, [c_vp, c_vp]),

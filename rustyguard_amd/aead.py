@@ -107,13 +107,17 @@ class Engine:
     def set_lanes_per_packet(self, lanes: int):
         check(self._L.rg_set_lanes_per_packet(self._h, lanes), "rg_set_lanes_per_packet")
 
-    def set_staged(self, window_chunks: int):
-        """Kernel family: 0 = lane-pass kernels; 1/2 = LDS-staged tile kernel with that window;
-        3 = row kernel (wave-specialised ChaCha20 / Poly1305 waves)."""
-        check(self._L.rg_set_staged(self._h, window_chunks), "rg_set_staged")
+    def set_staged(self, kernel: int):
+        """Kernel family: -1 = automatic by batch size (default), 0 = pipelined lane kernel,
+        1/2 = LDS-staged tile kernel with that many 64-byte chunks per window."""
+        check(self._L.rg_set_staged(self._h, kernel), "rg_set_staged")
+
+    def kernel_for(self, n: int) -> int:
+        """The kernel family a batch of n packets runs on (rg_get_kernel)."""
+        return check(self._L.rg_get_kernel(self._h, n), "rg_get_kernel")
 
     def set_plan(self, mode):
-        """Size-class planner before the tile kernels: 0/False off, 1/True on, 2 auto (default)."""
+        """Size-class planner before the batched kernels: 0/False off, 1/True on, 2 auto (default)."""
         check(self._L.rg_set_plan(self._h, int(mode)), "rg_set_plan")
 
     def set_segments(self, k: int):
@@ -121,11 +125,12 @@ class Engine:
         check(self._L.rg_set_segments(self._h, k), "rg_set_segments")
 
     def set_debug_mode(self, mode: int):
-        """Diagnostics: 1 = compute-only seal, 2 = memory-only seal (outputs invalid)."""
+        """Diagnostics: 1 = compute-only seal, 2 = memory-only seal, 3 = stamps, 4/5/6 = non-temporal
+        loads / stores / both on the pipelined kernel (outputs invalid except in mode 3)."""
         check(self._L.rg_set_debug_mode(self._h, mode), "rg_set_debug_mode")
 
     def set_debug_buffer(self, tensor):
-        """Diagnostics: device buffer receiving per-wave stamp totals (debug mode 3)."""
+        """Diagnostics: device buffer receiving per-wave stamps (include/rg_aead.h)."""
         check(self._L.rg_set_debug_buffer(self._h, _vp(tensor) if tensor is not None else None),
               "rg_set_debug_buffer")
 

@@ -80,6 +80,7 @@ struct HostBuf {
 // planner work lists (rg_tile.hip): class counts + [kClasses][cap] indices
 struct PlanBuf {
     DevBuf counts, lists;
+    DevBuf sched; // pipelined kernel's tile queue and per-class schedule (rg_pipe.hip), zero between launches
     uint32_t cap = 0;
     // auto planning: the tile kernel reports the number of size classes of the
     // last planned batch into host-mapped memory (read without synchronising;
@@ -91,6 +92,11 @@ struct PlanBuf {
         if (!counts.p) { // counters + done count; the tile kernels leave them zeroed
             hipError_t e = counts.reserve((rg::kClasses + 1) * sizeof(uint32_t));
             if (e == hipSuccess) e = hipMemset(counts.p, 0, (rg::kClasses + 1) * sizeof(uint32_t));
+            if (e != hipSuccess) return e;
+        }
+        if (!sched.p) {
+            hipError_t e = sched.reserve(rg::kSchedWords * sizeof(uint32_t));
+            if (e == hipSuccess) e = hipMemset(sched.p, 0, rg::kSchedWords * sizeof(uint32_t));
             if (e != hipSuccess) return e;
         }
         if (!h_classes) {
@@ -113,6 +119,7 @@ struct PlanBuf {
     void release() {
         counts.release();
         lists.release();
+        sched.release();
         cap = 0;
         if (h_classes) (void)hipHostFree(const_cast<uint32_t *>(h_classes));
         h_classes = nullptr;
@@ -145,14 +152,12 @@ struct rg_ctx {
     int wg_per_cu = 0;  // 0 = auto, -1 = plain one-shot grid (no LDS reservation)
     int cus = 0;
     int debug_mode = 0;
-    int staged_g = 2; // 0 = lane-pass kernels, else LDS-staged windows of G chunks (default: 2)
+    int staged_g = -1; // -1 auto, 0 pipelined lane kernel, 1/2 LDS-staged tile windows of G chunks
     int plan = 2;     // size-class planner: 0 off (array order), 1 always, 2 auto (skip for single-class batches)
     int segments = 0; // segments per packet: 0 = automatic, else 1 / 2 / 4
     PlanBuf plan_dev; // planner lists of the device API (calls on one ctx are stream-ordered)
     uint64_t *dbg = nullptr; // diagnostics buffer (device), stamp builds only
-    int max_wg[2][3] = {{0, 0, 0}, {0, 0, 0}}; // [seal, open][K = 1, 2, 4]
-    int pipe_max_wg[2] = {0, 0};                // [seal, open] pipelined lane kernel
-    int wave_max_wg[2] = {0, 0};                // [seal, open] wave-tile kernel
+    int pipe_max_wg[2] = {0, 0}; // [seal, open] resident workgroups per CU of the pipelined kernel
     std::mutex mu;
     Slot slots[2];
     DevBuf d_keys, d_recv;
@@ -189,11 +194,8 @@ int rg_create(int device, rg_ctx **out) {
     c->device = device;
     {
         hipError_t e = hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device);
-        if (e == hipSuccess) e = rg::prepare_kernels(c->max_wg);
         if (e == hipSuccess) e = rg::prepare_tile_kernels();
-        if (e == hipSuccess) e = rg::prepare_row_kernels();
         if (e == hipSuccess) e = rg::prepare_pipe_kernels(c->pipe_max_wg);
-        if (e == hipSuccess) e = rg::prepare_wave_kernels(c->wave_max_wg);
         if (e != hipSuccess) {
             delete c;
             return set_err(RG_EDEVICE, "kernel setup", e);
@@ -240,9 +242,10 @@ int rg_set_lanes_per_packet(rg_ctx *ctx, int lanes) {
 int rg_get_lanes_per_packet(rg_ctx *ctx, size_t n) {
     if (!ctx) return set_err(RG_EINVAL, "null context");
     if (ctx->lanes) return ctx->lanes;
-    // fewest lanes per packet that still gives every SIMD >= 2 waves
-    // (n * K lanes >= CUs * 2 workgroups * 256 lanes)
-    const size_t want = (size_t)(ctx->cus > 0 ? ctx->cus : 256) * 512;
+    // fewest lanes per packet that still gives every SIMD one wave (n * K
+    // lanes >= CUs * 256): a single wave of the pipelined kernel already keeps
+    // a SIMD's VALU busy, so more segments only add combine work
+    const size_t want = (size_t)(ctx->cus > 0 ? ctx->cus : 256) * 256;
     if (n >= want) return 1;
     if (2 * n >= want) return 2;
     return 4;
@@ -257,9 +260,7 @@ int rg_set_wg_per_cu(rg_ctx *ctx, int wg) {
 
 int rg_set_staged(rg_ctx *ctx, int g) {
     if (!ctx) return set_err(RG_EINVAL, "null context");
-    if (g < 0 || g > 5)
-        return set_err(RG_EINVAL,
-                       "kernel must be 0 (lane-pass), 1/2 (tile windows), 3 (rows), 4 (pipelined lanes) or 5 (wave tiles)");
+    if (g < -1 || g > 2) return set_err(RG_EINVAL, "kernel must be -1 (auto), 0 (pipelined lanes) or 1/2 (tile windows)");
     ctx->staged_g = g;
     return RG_OK;
 }
@@ -291,24 +292,30 @@ int rg_set_debug_mode(rg_ctx *ctx, int mode) {
     return RG_OK;
 }
 
+// Kernel choice: batches that fill at most about one wave per SIMD go to the
+// pipelined lane kernel (it saturates a SIMD with one wave and, with the
+// planner, balances mixed sizes); larger batches go to the LDS-staged tile
+// kernel, whose coalesced LDS-DMA windows win once two waves per SIMD are
+// resident (measured).
+int rg_get_kernel(rg_ctx *ctx, size_t n) {
+    if (!ctx) return set_err(RG_EINVAL, "null context");
+    if (ctx->staged_g >= 0) return ctx->staged_g;
+    return n < (size_t)(ctx->cus > 0 ? ctx->cus : 256) * 512 ? 0 : 2;
+}
+
 static rg::Launch launch_cfg(rg_ctx *ctx, size_t n, bool open) {
     rg::Launch L;
     L.lanes = rg_get_lanes_per_packet(ctx, n);
     L.cus = ctx->cus;
-    L.debug_mode = open ? 0 : ctx->debug_mode;
-    if (L.debug_mode == 3 && ctx->staged_g == 0) L.debug_mode = 0;
-    L.staged_g = ctx->staged_g;
-    if (L.staged_g >= 4) L.lanes = 1;
-    const int k = L.lanes == 1 ? 0 : L.lanes == 2 ? 1 : 2;
-    const int cap = std::max(1, L.staged_g == 4   ? ctx->pipe_max_wg[open ? 1 : 0]
-                                : L.staged_g == 5 ? ctx->wave_max_wg[open ? 1 : 0]
-                                                  : ctx->max_wg[open ? 1 : 0][k]);
+    L.staged_g = rg_get_kernel(ctx, n);
+    L.debug_mode = open ? (ctx->debug_mode == 3 ? 3 : 0) : ctx->debug_mode;
+    const int cap = std::max(1, ctx->pipe_max_wg[open ? 1 : 0]);
     if (ctx->wg_per_cu < 0) {
         L.wg_per_cu = 0;
     } else if (ctx->wg_per_cu > 0) {
         L.wg_per_cu = std::min(ctx->wg_per_cu, cap);
     } else {
-        // enough resident workgroups for one packet per lane group, capped by occupancy
+        // enough resident workgroups for one lane per packet segment, capped by occupancy
         const size_t need = ((size_t)n * L.lanes + 255) / 256;
         const size_t per_cu = (need + L.cus - 1) / std::max(1, L.cus);
         L.wg_per_cu = (int)std::max<size_t>(1, std::min<size_t>(per_cu, (size_t)cap));
@@ -325,26 +332,6 @@ static hipError_t launch_tiles_any(rg_ctx *ctx, const rg::SealArgs *sa, const rg
     const uint32_t n = sa ? sa->n : oa->n;
     rg::Launch L = L0;
     rg::TilePlan tp{};
-    if (L.staged_g == 3) { // row kernel: identity tiles, or the planner's lists for mixed sizes
-        bool plan = ctx->plan == 1;
-        if (ctx->plan == 2) {
-            hipError_t e = pb.reserve(n);
-            if (e != hipSuccess) return e;
-            plan = pb.want_plan();
-        }
-        if (plan) {
-            hipError_t e = pb.reserve(n);
-            if (e != hipSuccess) return e;
-            tp.counts = static_cast<uint32_t *>(pb.counts.p);
-            tp.lists = static_cast<uint32_t *>(pb.lists.p);
-            tp.cap = pb.cap;
-            tp.classes_out = pb.d_classes;
-            e = rg::launch_plan(sa ? sa->desc : oa->desc, n, oa != nullptr, tp, st);
-            if (e != hipSuccess) return e;
-        }
-        L.wg_per_cu = ctx->wg_per_cu > 0 ? ctx->wg_per_cu : 2;
-        return rg::launch_rows(sa, oa, tp, L, st);
-    }
     tp.target_lanes = (uint32_t)std::max(1, ctx->cus) * 256u; // one wave per SIMD
     tp.fixed_k = (uint32_t)ctx->segments;
     bool plan = ctx->plan == 1;
@@ -368,26 +355,48 @@ static hipError_t launch_tiles_any(rg_ctx *ctx, const rg::SealArgs *sa, const rg
     return rg::launch_tiles(sa, oa, L.staged_g, tp, L, st);
 }
 
+// Pipelined kernel: planned (size classes, per-class segments, tile queue) or
+// in array order with lanes_per_packet segments.
+static hipError_t launch_pipe_any(rg_ctx *ctx, const rg::SealArgs *sa, const rg::OpenArgs *oa, PlanBuf &pb,
+                                  const rg::Launch &L, hipStream_t st) {
+    const uint32_t n = sa ? sa->n : oa->n;
+    bool plan = ctx->plan == 1;
+    if (ctx->plan == 2) {
+        hipError_t e = pb.reserve(n);
+        if (e != hipSuccess) return e;
+        plan = pb.want_plan();
+    }
+    if (!plan) return rg::launch_pipe(sa, oa, L, nullptr, st);
+    rg::Launch Lp = L;
+    Lp.wg_per_cu = ctx->wg_per_cu > 0 ? std::min(ctx->wg_per_cu, std::max(1, ctx->pipe_max_wg[oa ? 1 : 0])) : 1;
+    hipError_t e = pb.reserve(n);
+    if (e != hipSuccess) return e;
+    rg::TilePlan tp{};
+    tp.counts = static_cast<uint32_t *>(pb.counts.p);
+    tp.lists = static_cast<uint32_t *>(pb.lists.p);
+    tp.cap = pb.cap;
+    e = rg::launch_plan(sa ? sa->desc : oa->desc, n, oa != nullptr, tp, st);
+    if (e != hipSuccess) return e;
+    rg::PipePlan pp{static_cast<uint32_t *>(pb.counts.p), static_cast<const uint32_t *>(pb.lists.p), pb.cap,
+                    static_cast<uint32_t *>(pb.sched.p), pb.d_classes};
+    return rg::launch_pipe(sa, oa, Lp, &pp, st);
+}
+
 static hipError_t launch_seal_any(rg_ctx *ctx, const rg::SealArgs &a0, PlanBuf &pb, hipStream_t st) {
     rg::SealArgs a = a0;
+    const rg::Launch L = launch_cfg(ctx, a.n, false);
     // stamps: debug mode 3, or any diagnostic mode of the pipelined kernel
-    a.dbg = ctx->debug_mode == 3 || (ctx->staged_g >= 4 && ctx->debug_mode != 0) ? ctx->dbg : nullptr;
-    rg::Launch L = launch_cfg(ctx, a.n, false);
-    if (L.staged_g == 4) return rg::launch_pipe(&a, nullptr, L, st);
-    if (L.staged_g == 5) return rg::launch_wave(&a, nullptr, L, st);
-    if (L.staged_g > 0 && (L.debug_mode == 0 || L.debug_mode == 3)) return launch_tiles_any(ctx, &a, nullptr, pb, L, st);
-    return rg::launch_seal(a, L, st);
+    a.dbg = L.debug_mode == 3 || (L.staged_g == 0 && L.debug_mode != 0) ? ctx->dbg : nullptr;
+    if (L.staged_g == 0) return launch_pipe_any(ctx, &a, nullptr, pb, L, st);
+    return launch_tiles_any(ctx, &a, nullptr, pb, L, st);
 }
 
 static hipError_t launch_open_any(rg_ctx *ctx, const rg::OpenArgs &a0, PlanBuf &pb, hipStream_t st) {
     rg::OpenArgs a = a0;
-    a.dbg = ctx->debug_mode == 3 ? ctx->dbg : nullptr;
-    rg::Launch L = launch_cfg(ctx, a.n, true);
-    L.debug_mode = ctx->debug_mode == 3 ? 3 : 0;
-    if (L.staged_g == 4) return rg::launch_pipe(nullptr, &a, L, st);
-    if (L.staged_g == 5) return rg::launch_wave(nullptr, &a, L, st);
-    if (L.staged_g > 0) return launch_tiles_any(ctx, nullptr, &a, pb, L, st);
-    return rg::launch_open(a, L, st);
+    const rg::Launch L = launch_cfg(ctx, a.n, true);
+    a.dbg = L.debug_mode == 3 ? ctx->dbg : nullptr;
+    if (L.staged_g == 0) return launch_pipe_any(ctx, nullptr, &a, pb, L, st);
+    return launch_tiles_any(ctx, nullptr, &a, pb, L, st);
 }
 
 // --------------------------------------------------------------- device API

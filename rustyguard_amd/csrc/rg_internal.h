@@ -57,13 +57,19 @@ struct Launch {
     int cus;
     int wg_per_cu;
     int debug_mode; // diagnostics: 0 normal, 1/2 seal compute/memory only, 3 staged stamps
-    int staged_g;   // kernel family: 0 lane-pass, 1/2 LDS-staged tiles (window chunks), 3 rows, 4 pipelined lanes, 5 wave tiles
+    int staged_g;   // kernel family: 0 pipelined lanes (rg_pipe.hip), 1/2 LDS-staged tiles of that window (rg_tile.hip)
 };
 constexpr uint32_t kLdsPerCu = 160u * 1024u;
 
 // Size-class work lists built by the planner (rg_tile.hip).  counts == nullptr:
 // identity order (packet i in tile i / 64), one segment count fixed_k for all.
 constexpr uint32_t kClasses = 37;
+// class c: c chunks for c <= 16; above, upper bounds 24, 32, 48, 64, ..., 16384
+__host__ __device__ __forceinline__ uint32_t class_hi(uint32_t c) {
+    if (c <= 16) return c;
+    const uint32_t j = c - 17;
+    return (j & 1u) ? (1u << (j / 2 + 5)) : (3u << (j / 2 + 3));
+}
 struct TilePlan {
     const uint32_t *counts; // [kClasses] packets per class, then [kClasses] = finished-workgroup count
     const uint32_t *lists;  // [kClasses][cap] packet indices
@@ -73,29 +79,29 @@ struct TilePlan {
     uint32_t *classes_out; // host-mapped: number of non-empty classes of the batch (or nullptr)
 };
 
-hipError_t launch_seal(const SealArgs &a, const Launch &L, hipStream_t s);
-hipError_t launch_open(const OpenArgs &a, const Launch &L, hipStream_t s);
 // Planner + LDS-staged tile kernel (rg_tile.hip); exactly one of sa / oa is non-null.
 hipError_t launch_plan(const rg_pkt_desc *desc, uint32_t n, bool open, const TilePlan &tp, hipStream_t s);
 hipError_t launch_tiles(const SealArgs *sa, const OpenArgs *oa, int G, const TilePlan &tp, const Launch &L,
                         hipStream_t s);
 hipError_t prepare_tile_kernels();
-// Row kernel (rg_rows.hip): wave-specialised workgroups over identity tiles
-// (tp.counts == nullptr) or the planner's size-class lists.
-constexpr uint32_t kRowMaxTilesWG = 2048; // tiles per workgroup (LDS row table)
-hipError_t launch_rows(const SealArgs *sa, const OpenArgs *oa, const TilePlan &tp, const Launch &L, hipStream_t s);
-hipError_t prepare_row_kernels();
 // Pipelined lane kernel (rg_pipe.hip): one packet per lane, double-buffered
 // chunk loads, Poly1305 absorbed inside the next chunk's keystream rounds.
-hipError_t launch_pipe(const SealArgs *sa, const OpenArgs *oa, const Launch &L, hipStream_t s);
+// With a plan (planner lists, rg_tile.hip): a schedule kernel picks segments per
+// size class from the batch's mean work, then one wave per SIMD walks tiles of
+// 64 lanes, largest class first, round robin (sched[] holds the schedule; the
+// schedule kernel zeroes the planner's counts).  Without one: lane units in
+// array order, grid-stride.
+constexpr uint32_t kSchedWords = 128;
+struct PipePlan {
+    uint32_t *counts;      // [kClasses] packets per class (zeroed again by the schedule kernel)
+    const uint32_t *lists; // [kClasses][cap] packet indices
+    uint32_t cap;
+    uint32_t *sched;       // [kSchedWords] per-batch schedule
+    uint32_t *classes_out; // host-mapped: non-empty classes of the batch (or nullptr)
+};
+hipError_t launch_pipe(const SealArgs *sa, const OpenArgs *oa, const Launch &L, const PipePlan *plan,
+                       hipStream_t s);
 hipError_t prepare_pipe_kernels(int max_wg[2]); // [seal, open] resident 256-thread workgroups per CU
-// Wave-tile kernel (rg_wave.hip): one packet per lane, tiles of 64 packets moved
-// with coalesced loads / stores through a wave-private LDS transpose.
-hipError_t launch_wave(const SealArgs *sa, const OpenArgs *oa, const Launch &L, hipStream_t s);
-hipError_t prepare_wave_kernels(int max_wg[2]);
-// sets the dynamic-LDS attribute and returns max resident workgroups per CU
-// for [seal, open][K = 1, 2, 4]
-hipError_t prepare_kernels(int max_wg[2][3]);
 hipError_t launch_general(GeneralJob *jobs, uint32_t njobs, uint8_t *arena, hipStream_t s);
 hipError_t launch_synth_fill(const rg_pkt_desc *desc, const uint32_t *inner_len, uint32_t n, uint8_t *buf,
                              uint64_t buf_len, uint64_t seed, hipStream_t s);

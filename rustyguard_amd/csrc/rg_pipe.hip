@@ -82,13 +82,13 @@ __device__ __forceinline__ void absorb_chunk(Acc &h, const Chunk &c, const Mul &
 // keystream and no Poly1305); 4/5/6 non-temporal loads / stores / both.
 template <bool OPEN, bool ABSORB, bool TAIL, int MODE = 0>
 __device__ __forceinline__ void pipe_step(uint4 *pl, const Stream &st, const Mul &r, Acc &h, Chunk &pi, Chunk &buf,
-                                          uint32_t t, uint32_t nb) {
+                                          uint32_t t, uint32_t nb, uint32_t c0) {
     uint32_t ks[16];
     if constexpr (MODE == 2) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) ks[i] = t * 16 + i;
         h.h0 ^= pi.q0.x ^ pi.q1.y ^ pi.q2.z ^ pi.q3.w;
-    } else stream_block_hooked(st, t + 1, ks, [&](int dr) {
+    } else stream_block_hooked(st, c0 + t + 1, ks, [&](int dr) {
         if constexpr (ABSORB) {
             if (dr == 1) acc_block(h, pi.q0, r);
             if (dr == 3) acc_block(h, pi.q1, r);
@@ -120,33 +120,34 @@ __device__ __forceinline__ void pipe_step(uint4 *pl, const Stream &st, const Mul
     if constexpr (!TAIL) load_chunk<NT>(buf, pl, t + 2, nb - 1);
 }
 
-// Keystream XOR in place + Poly1305 over the ciphertext for one packet's nb
-// 16-byte blocks; b0 / b1 hold chunks 0 / 1 (loads already issued).  The
+// Keystream XOR in place + Poly1305 over the ciphertext of nb 16-byte blocks
+// starting at chunk c0 of the payload (pl points there; keystream blocks from
+// c0 + 1); b0 / b1 hold its chunks 0 / 1 (loads already issued).  The
 // first step is peeled (nothing to absorb yet), so that every absorb inside
 // the loop is unconditional; chunk c always lives in buffer c % 2.
 template <bool OPEN, int MODE = 0>
-__device__ __forceinline__ Acc pipe_pass(uint4 *pl, const Stream &st, const Mul &r, uint32_t nb, Chunk &b0,
-                                         Chunk &b1) {
+__device__ __forceinline__ Acc pipe_pass(uint4 *pl, const Stream &st, const Mul &r, uint32_t nb, uint32_t c0,
+                                         Chunk &b0, Chunk &b1) {
     const uint32_t F = nb >> 2, bl = nb & 3u; // full chunks, blocks in the partial last chunk
     Acc h = {0, 0, 0, 0, 0};
     Chunk pi = {};
     uint32_t pending = 0; // blocks of pi not yet absorbed
     if (F > 0) {
-        pipe_step<OPEN, false, false, MODE>(pl, st, r, h, pi, b0, 0, nb);
+        pipe_step<OPEN, false, false, MODE>(pl, st, r, h, pi, b0, 0, nb, c0);
         uint32_t t = 1;
         // whole pairs only: a step that may be skipped would leave the waitcnt
         // pass a path without its memory operations (vmcnt(0) at the next one)
         for (; t + 1 < F; t += 2) {
-            pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b1, t, nb);
-            pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b0, t + 1, nb);
+            pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b1, t, nb, c0);
+            pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b0, t + 1, nb, c0);
         }
-        if (t < F) pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b1, t, nb);
+        if (t < F) pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b1, t, nb, c0);
         pending = 4;
     }
     if (bl > 0) {
         Chunk &bp = (F & 1u) ? b1 : b0;
-        if (F > 0) pipe_step<OPEN, true, true, MODE>(pl, st, r, h, pi, bp, F, nb);
-        else pipe_step<OPEN, false, true, MODE>(pl, st, r, h, pi, bp, F, nb);
+        if (F > 0) pipe_step<OPEN, true, true, MODE>(pl, st, r, h, pi, bp, F, nb, c0);
+        else pipe_step<OPEN, false, true, MODE>(pl, st, r, h, pi, bp, F, nb, c0);
         pending = bl;
     }
     absorb_chunk(h, pi, r, pending); // the last chunk's blocks
@@ -160,30 +161,92 @@ __device__ __forceinline__ void pipe_tag(Acc h, const Mul &r, uint32_t P, const 
     acc_finish(h, s[0], s[1], s[2], s[3], tag);
 }
 
+// ------------------------------------------------------------- segments
+// G lanes (consecutive, G | 64) may share a packet: segment j covers chunks
+// [jL, min(C, (j+1)L)), L = ceil(C / G), with its own Horner chain h_j over
+// its blocks (clamped r).  With N_j = blocks after segment j,
+//   Poly1305 accumulator = sum_j h_j r^{N_j},
+// each lane raises r to its own N_j (left-to-right square-and-multiply: the
+// squarings are general multiplies, the "times r" steps the cheap clamped
+// one) and the group sums by butterfly; every lane of the group then holds
+// the packet's accumulator.  Each lane also computes the one-time-key block
+// itself (no cross-lane dependency before the combine).
+struct Seg {
+    uint32_t c0, nb, after; // first chunk, blocks in the segment, blocks after it
+};
+
+__device__ __forceinline__ Seg make_seg(uint32_t nb, uint32_t j, uint32_t G) {
+    const uint32_t C = (nb + 3) >> 2, L = (C + G - 1) / G;
+    const uint32_t c0 = min(j * L, C), c1 = min(c0 + L, C);
+    const uint32_t b0 = min(4 * c0, nb), b1 = min(4 * c1, nb);
+    return {c0, b1 - b0, nb - b1};
+}
+
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
+    return v;
+}
+
+__device__ __forceinline__ Acc combine_segments(Acc h, const Mul &r, uint32_t after, uint32_t G) {
+    if (G == 1) return h;
+    const uint32_t bits = 32 - __clz((int)wave_max_u32(after));
+    if (bits > 0) {
+        // r^after, left to right over the wave's bit count; every lane starts
+        // from 1, so leading zero bits of a shorter exponent are harmless
+        Acc x = {1, 0, 0, 0, 0};
+        for (int b = (int)bits - 1; b >= 0; --b) {
+            Acc sq = x;
+            acc_mul_gen(sq, make_gen(x));
+            Acc xr = sq;
+            acc_mul(xr, r);
+            const bool bit = (after >> b) & 1u;
+            x.h0 = bit ? xr.h0 : sq.h0; x.h1 = bit ? xr.h1 : sq.h1; x.h2 = bit ? xr.h2 : sq.h2;
+            x.h3 = bit ? xr.h3 : sq.h3; x.h4 = bit ? xr.h4 : sq.h4;
+        }
+        acc_mul_gen(h, make_gen(x));
+    }
+    for (uint32_t o = 1; o < G; o <<= 1) {
+        Acc other;
+        other.h0 = (uint32_t)__shfl_xor((int)h.h0, (int)o);
+        other.h1 = (uint32_t)__shfl_xor((int)h.h1, (int)o);
+        other.h2 = (uint32_t)__shfl_xor((int)h.h2, (int)o);
+        other.h3 = (uint32_t)__shfl_xor((int)h.h3, (int)o);
+        other.h4 = (uint32_t)__shfl_xor((int)h.h4, (int)o);
+        acc_add_acc(h, other);
+        acc_fold(h);
+    }
+    return h;
+}
+
 // ------------------------------------------------------------------ seal
 // Frame: [hdr 16][payload P][tag 16]; desc.len = P.  Checks as seal_packet
 // (rg_kernels.hip): descriptor and force_encrypt's padding assert
-// (rustyguard-core/src/lib.rs:273-277).
-template <int MODE> __device__ __forceinline__ void pipe_seal_packet(const SealArgs &a, uint32_t i) {
+// (rustyguard-core/src/lib.rs:273-277).  Lane j of a G-lane group runs
+// segment j; lane 0 writes header, tag and status.
+template <int MODE>
+__device__ __forceinline__ void pipe_seal_packet(const SealArgs &a, uint32_t i, uint32_t j, uint32_t G) {
     const rg_pkt_desc d = a.desc[i];
     const uint32_t P = d.len;
     const bool valid = d.key_idx < a.nkeys && (P & 15u) == 0 && (d.offset & 15u) == 0 && P <= kMaxPayload &&
                        d.offset <= a.buf_len && P + 32 <= a.buf_len - d.offset;
     if (!valid) {
-        if (a.status) a.status[i] = d.key_idx == RG_KEY_SKIP ? RG_PKT_REJECTED : RG_PKT_INVALID;
+        if (a.status && j == 0) a.status[i] = d.key_idx == RG_KEY_SKIP ? RG_PKT_REJECTED : RG_PKT_INVALID;
         return;
     }
     uint8_t *frame = a.buf + d.offset;
-    uint4 *pl = reinterpret_cast<uint4 *>(frame + 16);
     const uint32_t nb = P >> 4;
+    const Seg sg = make_seg(nb, j, G);
+    // an empty segment reads (never writes) the payload start, which is in the frame
+    uint4 *pl = reinterpret_cast<uint4 *>(frame + 16) + (sg.nb ? 4 * sg.c0 : 0);
     Chunk b0, b1;
     if constexpr (MODE == 1) {
         b0 = {make_uint4(i, 1, 2, 3), make_uint4(4, i, 6, 7), make_uint4(8, 9, i, 11), make_uint4(12, 13, 14, i)};
         b1 = b0;
     } else {
         constexpr int NT = MODE >= 4 ? MODE - 3 : 0;
-        load_chunk<NT>(b0, pl, 0, nb ? nb - 1 : 0);
-        load_chunk<NT>(b1, pl, 1, nb ? nb - 1 : 0);
+        load_chunk<NT>(b0, pl, 0, sg.nb ? sg.nb - 1 : 0);
+        load_chunk<NT>(b1, pl, 1, sg.nb ? sg.nb - 1 : 0);
     }
     const Key8 key = load_key(a.keys, d.key_idx);
     const uint64_t ctr = a.counters[i];
@@ -192,7 +255,9 @@ template <int MODE> __device__ __forceinline__ void pipe_seal_packet(const SealA
     uint32_t ks[16];
     stream_block(stm, 0, ks); // RFC 8439 §2.6 one-time key
     const Mul r = make_mul(ks[0], ks[1], ks[2], ks[3]);
-    const Acc h = pipe_pass<false, MODE>(pl, stm, r, nb, b0, b1);
+    Acc h = pipe_pass<false, MODE>(pl, stm, r, sg.nb, sg.c0, b0, b1);
+    h = combine_segments(h, r, sg.after, G);
+    if (j != 0) return;
     uint32_t tag[4];
     pipe_tag(h, r, P, ks + 4, tag);
     if (a.receivers) // DataHeader {4, receiver, counter} (rustyguard-core/src/lib.rs:286-290)
@@ -205,9 +270,9 @@ template <int MODE> __device__ __forceinline__ void pipe_seal_packet(const SealA
 // desc.len = W.  Checks mirror rustyguard-core/src/lib.rs:613-629,
 // rustyguard-types/src/lib.rs:181-196 and rustyguard-crypto/src/prim.rs:
 // 427-429.  Decrypts speculatively while MACing the ciphertext; a failed tag
-// (constant-time compare) re-applies the keystream, so the frame is left
-// unchanged.
-__device__ __forceinline__ void pipe_open_packet(const OpenArgs &a, uint32_t i) {
+// (constant-time compare, identical on every lane of the group) makes each
+// lane re-apply its segment's keystream, so the frame is left unchanged.
+__device__ __forceinline__ void pipe_open_packet(const OpenArgs &a, uint32_t i, uint32_t j, uint32_t G) {
     const rg_pkt_desc d = a.desc[i];
     const uint32_t W = d.len;
     uint32_t st;
@@ -229,16 +294,19 @@ __device__ __forceinline__ void pipe_open_packet(const OpenArgs &a, uint32_t i) 
         }
     }
     if (st != 0xFF) {
-        a.status[i] = (uint8_t)st;
-        if (a.counters_out) a.counters_out[i] = ctr;
+        if (j == 0) {
+            a.status[i] = (uint8_t)st;
+            if (a.counters_out) a.counters_out[i] = ctr;
+        }
         return;
     }
     const uint32_t P = W - 32;
-    uint4 *pl = reinterpret_cast<uint4 *>(frame + 16);
     const uint32_t nb = P >> 4;
+    const Seg sg = make_seg(nb, j, G);
+    uint4 *pl = reinterpret_cast<uint4 *>(frame + 16) + (sg.nb ? 4 * sg.c0 : 0);
     Chunk b0, b1;
-    load_chunk(b0, pl, 0, nb ? nb - 1 : 0);
-    load_chunk(b1, pl, 1, nb ? nb - 1 : 0);
+    load_chunk(b0, pl, 0, sg.nb ? sg.nb - 1 : 0);
+    load_chunk(b1, pl, 1, sg.nb ? sg.nb - 1 : 0);
     const uint4 want = *reinterpret_cast<const uint4 *>(frame + 16 + P);
     const Key8 key = load_key(a.keys, d.key_idx);
     const uint32_t n1 = (uint32_t)ctr, n2 = (uint32_t)(ctr >> 32);
@@ -246,21 +314,24 @@ __device__ __forceinline__ void pipe_open_packet(const OpenArgs &a, uint32_t i) 
     uint32_t ks[16];
     stream_block(stm, 0, ks);
     const Mul r = make_mul(ks[0], ks[1], ks[2], ks[3]);
-    const Acc h = pipe_pass<true>(pl, stm, r, nb, b0, b1);
+    Acc h = pipe_pass<true>(pl, stm, r, sg.nb, sg.c0, b0, b1);
+    h = combine_segments(h, r, sg.after, G);
     uint32_t tag[4];
     pipe_tag(h, r, P, ks + 4, tag);
     const uint32_t diff = (tag[0] ^ want.x) | (tag[1] ^ want.y) | (tag[2] ^ want.z) | (tag[3] ^ want.w);
     if (diff != 0) {
-        // restore: plaintext ^ keystream = ciphertext (callers never read the
-        // buffer on Err, but the frame is left as it came)
-        for (uint32_t c = 0; 4 * c < nb; ++c) {
-            stream_block(stm, c + 1, ks);
-            const uint32_t cnt = chunk_blocks(nb, c);
+        // restore this lane's segment: plaintext ^ keystream = ciphertext
+        // (callers never read the buffer on Err, but the frame is left as it came)
+        for (uint32_t c = 0; 4 * c < sg.nb; ++c) {
+            stream_block(stm, sg.c0 + c + 1, ks);
+            const uint32_t cnt = chunk_blocks(sg.nb, c);
             for (uint32_t q = 0; q < cnt; ++q) pl[4 * c + q] = xor4(pl[4 * c + q], ks + 4 * q);
         }
     }
-    a.status[i] = diff == 0 ? RG_PKT_OK : RG_PKT_DECRYPT_ERR;
-    if (a.counters_out) a.counters_out[i] = ctr;
+    if (j == 0) {
+        a.status[i] = diff == 0 ? RG_PKT_OK : RG_PKT_DECRYPT_ERR;
+        if (a.counters_out) a.counters_out[i] = ctr;
+    }
 }
 
 // ------------------------------------------------------------- kernels
@@ -278,39 +349,132 @@ __device__ __forceinline__ void pipe_stamp(uint64_t *dbg, uint64_t t0, uint64_t 
     }
 }
 
-template <int MODE> __global__ __launch_bounds__(256) void pipe_seal_kernel(SealArgs a) {
+// ------------------------------------------------------------- schedule
+// sched[] words: 2 total tiles, 4 + c: first tile of class c, 44 + c: log2
+// segments of class c, 84 + c: packets of class c.
+constexpr uint32_t kSchedStart = 4, kSchedLg = 44, kSchedCnt = 84;
+static_assert(kSchedCnt + kClasses <= kSchedWords, "schedule words");
+
+// One wave: lane c owns size class c.  Segments per class: the fewest (power
+// of two) that keep a lane's slots (1 one-time-key block + its chunks) within
+// the batch's mean work per SIMD, so that no tile outlasts the balanced
+// schedule; tiles are numbered largest class first (the round robin then
+// deals long tiles before short ones).
+// It also takes the planner's class counts over into sched[] and zeroes them
+// for the next batch (no atomics in the transport kernel).
+__global__ __launch_bounds__(64) void pipe_schedule_kernel(uint32_t *counts, uint32_t *sched, uint32_t simds,
+                                                           uint32_t *classes_out) {
+    const uint32_t c = threadIdx.x;
+    const uint32_t cnt = c < kClasses ? counts[c] : 0;
+    if (c < kClasses) counts[c] = 0;
+    const uint32_t chunks = c < kClasses ? class_hi(c) : 0;
+    uint64_t work = (uint64_t)cnt * (1 + chunks); // lane slots with one lane per packet
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) work += (uint64_t)__shfl_xor((long long)work, o);
+    const uint64_t per_simd = (work + 64ull * simds - 1) / (64ull * simds);
+    const uint32_t target = (uint32_t)(per_simd < 2 ? 2 : per_simd > 0xFFFF ? 0xFFFF : per_simd);
+    uint32_t lg = 0;
+    while (lg < 6 && 1 + (chunks + (1u << lg) - 1) / (1u << lg) > target) ++lg;
+    const uint32_t tiles = (uint32_t)((((uint64_t)cnt << lg) + 63) / 64);
+    // first tile of class c = tiles of all larger classes (suffix sum)
+    uint32_t suffix = tiles;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t v = (uint32_t)__shfl_down((int)suffix, o);
+        if (c + o < 64) suffix += v;
+    }
+    if (c < kClasses) {
+        sched[kSchedStart + c] = suffix - tiles;
+        sched[kSchedLg + c] = lg;
+        sched[kSchedCnt + c] = cnt;
+    }
+    const uint64_t used = __ballot(cnt > 0);
+    if (c == 0) {
+        sched[2] = suffix; // lane 0: all tiles
+        if (classes_out) *reinterpret_cast<volatile uint32_t *>(classes_out) = (uint32_t)__popcll(used);
+    }
+}
+
+// ------------------------------------------------------------- kernels
+// Identity order: lane units u = G * packet + segment, grid-stride (the stride
+// is a multiple of 256, so a packet's G lanes stay together in one wave);
+// lg = log2(G).
+// Planned order: wave w takes tiles w, w + W, ... of the size-ordered tile
+// list; lane l of a tile of class c is unit (tile - first tile of c) * 64 + l
+// of that class.
+template <typename Body>
+__device__ __forceinline__ void pipe_walk(uint32_t n, uint32_t lg, const PipePlan &pp, Body &&body) {
+    if (!pp.counts) {
+        const uint64_t units = (uint64_t)n << lg, stride = (uint64_t)gridDim.x * 256;
+        for (uint64_t u = blockIdx.x * 256 + threadIdx.x; u < units; u += stride)
+            body((uint32_t)(u >> lg), (uint32_t)u & ((1u << lg) - 1), 1u << lg);
+        return;
+    }
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t my_cnt = lane < kClasses ? pp.sched[kSchedCnt + lane] : 0;
+    const uint32_t my_start = lane < kClasses ? pp.sched[kSchedStart + lane] : 0;
+    const uint32_t my_lg = lane < kClasses ? pp.sched[kSchedLg + lane] : 0;
+    const uint32_t my_tiles = (uint32_t)((((uint64_t)my_cnt << my_lg) + 63) / 64);
+    const uint32_t total = pp.sched[2];
+    const uint32_t waves = gridDim.x * (blockDim.x / 64);
+    // static round robin over the size-ordered tiles (longest first): a single
+    // shared queue counter would serialise every wave's start on one atomic
+    for (uint32_t tile = uniform_u32(blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64); tile < total; tile += waves) {
+        const uint64_t hit = __ballot(lane < kClasses && my_start <= tile && tile < my_start + my_tiles);
+        const uint32_t c = uniform_u32((uint32_t)(__ffsll((unsigned long long)hit) - 1));
+        const uint32_t lgc = uniform_u32((uint32_t)__shfl((int)my_lg, (int)c));
+        const uint32_t cnt = uniform_u32((uint32_t)__shfl((int)my_cnt, (int)c));
+        const uint32_t u = (tile - uniform_u32((uint32_t)__shfl((int)my_start, (int)c))) * 64 + lane;
+        const uint32_t p = u >> lgc;
+        if (p < cnt) body(pp.lists[(uint64_t)c * pp.cap + p], u & ((1u << lgc) - 1), 1u << lgc);
+    }
+}
+
+template <int MODE> __global__ __launch_bounds__(256) void pipe_seal_kernel(SealArgs a, uint32_t lg, PipePlan pp) {
     const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
-    const uint32_t stride = gridDim.x * 256;
-    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < a.n; i += stride) pipe_seal_packet<MODE>(a, i);
+    pipe_walk(a.n, lg, pp, [&](uint32_t i, uint32_t j, uint32_t G) { pipe_seal_packet<MODE>(a, i, j, G); });
     if (a.dbg) pipe_stamp(a.dbg, t0, r0);
 }
 
-__global__ __launch_bounds__(256) void pipe_open_kernel(OpenArgs a) {
+__global__ __launch_bounds__(256) void pipe_open_kernel(OpenArgs a, uint32_t lg, PipePlan pp) {
     const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
-    const uint32_t stride = gridDim.x * 256;
-    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < a.n; i += stride) pipe_open_packet(a, i);
+    pipe_walk(a.n, lg, pp, [&](uint32_t i, uint32_t j, uint32_t G) { pipe_open_packet(a, i, j, G); });
     if (a.dbg) pipe_stamp(a.dbg, t0, r0);
 }
 
-static void pipe_grid(uint32_t n, const Launch &L, uint32_t &blocks, uint32_t &lds) {
-    const uint64_t want = ((uint64_t)n + 255) / 256;
+static void pipe_grid(uint64_t units, const Launch &L, uint32_t &blocks, uint32_t &lds) {
+    const uint64_t want = (units + 255) / 256;
     const uint64_t cap = (uint64_t)L.cus * (uint64_t)L.wg_per_cu;
     blocks = (uint32_t)(want < cap || cap == 0 ? want : cap);
     lds = L.wg_per_cu > 0 ? (kLdsPerCu / L.wg_per_cu) & ~255u : 0;
 }
 
-hipError_t launch_pipe(const SealArgs *sa, const OpenArgs *oa, const Launch &L, hipStream_t s) {
+hipError_t launch_pipe(const SealArgs *sa, const OpenArgs *oa, const Launch &L, const PipePlan *plan,
+                       hipStream_t s) {
     const uint32_t n = sa ? sa->n : oa->n;
     if (n == 0) return hipSuccess;
+    const uint32_t lg = L.lanes >= 4 ? 2 : L.lanes == 2 ? 1 : 0; // segments per packet without a plan: 1, 2, 4
+    PipePlan pp{};
     uint32_t blocks, lds;
-    pipe_grid(n, L, blocks, lds);
-    if (sa && L.debug_mode == 1) hipLaunchKernelGGL(pipe_seal_kernel<1>, dim3(blocks), dim3(256), lds, s, *sa);
-    else if (sa && L.debug_mode == 2) hipLaunchKernelGGL(pipe_seal_kernel<2>, dim3(blocks), dim3(256), lds, s, *sa);
-    else if (sa && L.debug_mode == 4) hipLaunchKernelGGL(pipe_seal_kernel<4>, dim3(blocks), dim3(256), lds, s, *sa);
-    else if (sa && L.debug_mode == 5) hipLaunchKernelGGL(pipe_seal_kernel<5>, dim3(blocks), dim3(256), lds, s, *sa);
-    else if (sa && L.debug_mode == 6) hipLaunchKernelGGL(pipe_seal_kernel<6>, dim3(blocks), dim3(256), lds, s, *sa);
-    else if (sa) hipLaunchKernelGGL(pipe_seal_kernel<0>, dim3(blocks), dim3(256), lds, s, *sa);
-    else hipLaunchKernelGGL(pipe_open_kernel, dim3(blocks), dim3(256), lds, s, *oa);
+    if (plan) {
+        // L.wg_per_cu 4-wave workgroups per CU, held there by the LDS reservation
+        pp = *plan;
+        const uint32_t wg = (uint32_t)(L.wg_per_cu > 0 ? L.wg_per_cu : 1);
+        blocks = (uint32_t)(L.cus > 0 ? L.cus : 1) * wg;
+        lds = (kLdsPerCu / wg) & ~255u;
+        // balance per SIMD: co-resident waves share one SIMD's issue slots
+        hipLaunchKernelGGL(pipe_schedule_kernel, dim3(1), dim3(64), 0, s, pp.counts, pp.sched, blocks / wg * 4,
+                           pp.classes_out);
+    } else {
+        pipe_grid((uint64_t)n << lg, L, blocks, lds);
+    }
+    if (sa && L.debug_mode == 1) hipLaunchKernelGGL(pipe_seal_kernel<1>, dim3(blocks), dim3(256), lds, s, *sa, lg, pp);
+    else if (sa && L.debug_mode == 2) hipLaunchKernelGGL(pipe_seal_kernel<2>, dim3(blocks), dim3(256), lds, s, *sa, lg, pp);
+    else if (sa && L.debug_mode == 4) hipLaunchKernelGGL(pipe_seal_kernel<4>, dim3(blocks), dim3(256), lds, s, *sa, lg, pp);
+    else if (sa && L.debug_mode == 5) hipLaunchKernelGGL(pipe_seal_kernel<5>, dim3(blocks), dim3(256), lds, s, *sa, lg, pp);
+    else if (sa && L.debug_mode == 6) hipLaunchKernelGGL(pipe_seal_kernel<6>, dim3(blocks), dim3(256), lds, s, *sa, lg, pp);
+    else if (sa) hipLaunchKernelGGL(pipe_seal_kernel<0>, dim3(blocks), dim3(256), lds, s, *sa, lg, pp);
+    else hipLaunchKernelGGL(pipe_open_kernel, dim3(blocks), dim3(256), lds, s, *oa, lg, pp);
     return hipGetLastError();
 }
 

@@ -34,12 +34,6 @@
 namespace rg {
 
 // ------------------------------------------------------------ size classes
-// class c: c chunks for c <= 16; above, upper bounds 24, 32, 48, 64, ..., 16384
-__host__ __device__ __forceinline__ uint32_t class_hi(uint32_t c) {
-    if (c <= 16) return c;
-    const uint32_t j = c - 17;
-    return (j & 1u) ? (1u << (j / 2 + 5)) : (3u << (j / 2 + 3));
-}
 
 __device__ __forceinline__ uint32_t class_of(uint32_t chunks) {
     if (chunks <= 16) return chunks;

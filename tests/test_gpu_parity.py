@@ -67,26 +67,24 @@ def _gpu_open(engine, keys, desc_open, buf):
     return b.cpu().numpy(), st.cpu().numpy(), co.cpu().numpy().view(np.uint64)
 
 
-# kernel configurations every parity test runs under: lane-pass kernels with
-# K lanes per packet, and the LDS-staged tile kernel with G-chunk windows,
-# the size-class planner on/off and 1/2/4 segments per packet (0 = automatic)
-MODES = [("wave",), ("pipe",), ("rows",), ("lane", 1), ("lane", 2), ("lane", 4),
+# kernel configurations every parity test runs under: the library default
+# (automatic kernel choice), the pipelined lane kernel with the size-class
+# plan or in array order with K segments per packet, and the LDS-staged tile
+# kernel with G-chunk windows, the planner on/off and 1/2/4 segments per
+# packet (0 = automatic)
+MODES = [("auto",), ("pipe", 0), ("pipe", 1), ("pipe", 2), ("pipe", 4),
          ("tile", 2, 2, 0), ("tile", 2, 1, 0), ("tile", 1, 1, 1), ("tile", 2, 1, 2), ("tile", 2, 1, 4),
          ("tile", 2, 0, 1), ("tile", 2, 0, 2), ("tile", 1, 0, 4), ("tile", 1, 1, 0)]
 
 
 def _configure(engine, mode):
     _reset(engine)
-    if mode[0] == "wave":
-        engine.set_staged(5)
-    elif mode[0] == "pipe":
-        engine.set_staged(4)
-    elif mode[0] == "rows":
-        engine.set_staged(3)
-    elif mode[0] == "lane":
+    if mode[0] == "pipe":  # ("pipe", 0): size-class plan; ("pipe", K): array order, K segments
         engine.set_staged(0)
-        engine.set_lanes_per_packet(mode[1])
-    else:
+        engine.set_plan(1 if mode[1] == 0 else 0)
+        if mode[1]:
+            engine.set_lanes_per_packet(mode[1])
+    elif mode[0] == "tile":
         _, g, plan, k = mode
         engine.set_staged(g)
         engine.set_plan(plan)
@@ -95,16 +93,18 @@ def _configure(engine, mode):
 
 def _reset(engine):
     """library defaults"""
-    engine.set_staged(2)
+    engine.set_staged(-1)
     engine.set_plan(2)
     engine.set_segments(0)
     engine.set_lanes_per_packet(0)
 
 
 def _mode_id(m):
-    if m[0] in ("rows", "pipe", "wave"):
-        return m[0]
-    return f"lane{m[1]}" if m[0] == "lane" else f"tile_g{m[1]}_p{m[2]}_k{m[3]}"
+    if m[0] == "auto":
+        return "auto"
+    if m[0] == "pipe":
+        return f"pipe{m[1]}" if m[1] else "pipe_plan"
+    return f"tile_g{m[1]}_p{m[2]}_k{m[3]}"
 
 
 # ------------------------------------------------------------ reference pins

@@ -16,7 +16,7 @@ for d in sys.argv[1:]:
         agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
         dur[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     for k, v in agg.items():
-        if not any(x in k for x in ("seal", "open", "staged", "tile", "row_kernel", "plan", "pipe")):
+        if not any(x in k for x in ("seal", "open", "tile", "plan", "pipe")):
             continue
         m = {c: sum(x) / len(x) for c, x in v.items()}
         us = sorted(dur[k])[len(dur[k]) // 2]

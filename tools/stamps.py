@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Section shares of the LDS-staged kernel from its s_memtime diagnostic build (debug mode 3)."""
+"""Per-wave s_memtime stamps of the batched kernels: section shares of the LDS-staged tile kernel
+(debug mode 3), whole-wave cycles / wall time / start-end spread of the pipelined kernel."""
 import argparse
 import json
 import os
@@ -16,10 +17,11 @@ from rustyguard_amd.device import DeviceBatch  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--workload", default="cfg2")
-ap.add_argument("--staged", type=int, default=2)
+ap.add_argument("--staged", type=int, default=-1)
 ap.add_argument("--wg-per-cu", type=int, default=0)
 ap.add_argument("--plan", type=int, default=-1)
 ap.add_argument("--segments", type=int, default=0)
+ap.add_argument("--lanes", type=int, default=0)
 ap.add_argument("--mode", type=int, default=3, help="seal debug mode while stamping (pipelined kernel: 1/2/4/5/6 too)")
 args = ap.parse_args()
 eng = Engine(0)
@@ -29,6 +31,8 @@ if args.wg_per_cu:
 if args.plan >= 0:
     eng.set_plan(args.plan)
 eng.set_segments(args.segments)
+if args.lanes:
+    eng.set_lanes_per_packet(args.lanes)
 w = workloads.build(args.workload)
 b = DeviceBatch(eng, w)
 b.fill()
@@ -59,7 +63,7 @@ for op in ("seal", "open"):
     d = d[d[:, 6] == 1]
     if not len(d):  # no stamps for this op in this mode
         continue
-    if args.staged == 4:
+    if eng.kernel_for(w.n) == 0:
         # pipelined lane kernel: whole-wave cycles and wall time, start / end spread
         tot = d[:, 0].astype(np.float64)
         rt = d[:, 7].astype(np.float64) / 100e6
@@ -69,26 +73,6 @@ for op in ("seal", "open"):
                    "shader_clock_ghz": round(float(tot.sum() / rt.sum()) / 1e9, 3),
                    "start_us_pct_0_50_90_100": [round(float(v), 2) for v in np.percentile((d[:, 4] - t0) / 100.0, [0, 50, 90, 100])],
                    "end_us_pct_0_50_90_100": [round(float(v), 2) for v in np.percentile((d[:, 4] + d[:, 7] - t0) / 100.0, [0, 50, 90, 100])]}
-        continue
-    if args.staged == 3:
-        # row kernel: prologue, load issue (incl. waits), compute, barrier; kind 1 = ChaCha wave, 2 = Poly1305 wave
-        res = {}
-        for kind, kname in ((1, "chacha"), (2, "poly")):
-            x = d[d[:, 5] == kind]
-            if not len(x):
-                continue
-            tot = x[:, :4].sum(axis=1)
-            rt = x[:, 7].astype(np.float64) / 100e6
-            res[kname] = {"waves": int(len(x)), "cycles_per_wave_mean": float(tot.mean()),
-                          "wave_us_mean": round(float(rt.mean()) * 1e6, 2),
-                          "shader_clock_ghz": round(float(tot.sum() / rt.sum()) / 1e9, 3),
-                          "start_us_pct_0_50_90_100": [round(float(v), 2) for v in np.percentile(
-                              (x[:, 4] - d[:, 4].min()) / 100.0, [0, 50, 90, 100])],
-                          "end_us_pct_0_50_90_100": [round(float(v), 2) for v in np.percentile(
-                              (x[:, 4] + x[:, 7] - d[:, 4].min()) / 100.0, [0, 50, 90, 100])],
-                          "share": {n: round(float(x[:, k].sum() / tot.sum()), 4)
-                                    for k, n in enumerate(["prologue", "issue", "compute", "barrier"])}}
-        out[op] = res
         continue
     names = ["setup", "store", "dma_issue", "dma_wait", "chunk", "tail"]
     tot = d[:, :6].sum(axis=1)
