@@ -247,7 +247,8 @@ def main():
     achieved = dom_alg / (dom_ms / 1e3) / 1e9
     pmc = load_traffic(args.workload)
     traffic = None
-    if pmc and pmc.get(dominant):
+    # only counters of the kernel family this run used (a kernel change makes them stale)
+    if pmc and pmc.get(dominant) and pmc[dominant].get("family") == eng.kernel_for(w.n):
         traffic = pmc[dominant].get("hbm_bytes_per_launch")
 
     out = {

@@ -30,11 +30,18 @@ def kind_of(name: str):
     if "staged_kernel<" in name or "tile_kernel<" in name:
         args = name.split("<", 1)[1].split(">", 1)[0].split(",")
         return "open" if args[1].strip() == "true" else "seal"
-    if "seal_kernel<" in name or "seal_tile" in name:
+    if "pipe_seal_kernel" in name:
         return "seal"
-    if "open_kernel<" in name or "open_tile" in name:
+    if "pipe_open_kernel" in name:
         return "open"
     return None
+
+
+def family_of(name: str) -> int:
+    """rg_get_kernel value of a transport kernel: 0 pipelined lanes, 1/2 tile window."""
+    if "pipe_" in name:
+        return 0
+    return int(name.split("<", 1)[1].split(",", 1)[0])
 
 
 def counter_means(d: str):
@@ -82,7 +89,7 @@ def main():
                 continue
             rd = fetch[k]["FETCH_SIZE"] * 1024 * 2
             wr = write[k]["WRITE_SIZE"] * 1024
-            res[k] = {"kernel": names[k], "fetch_size_kib_raw": round(fetch[k]["FETCH_SIZE"], 1),
+            res[k] = {"kernel": names[k], "family": family_of(names[k]), "fetch_size_kib_raw": round(fetch[k]["FETCH_SIZE"], 1),
                       "read_bytes": int(rd), "write_bytes": int(wr), "hbm_bytes_per_launch": int(rd + wr)}
             if k in alg:
                 res[k]["alg_bytes_per_launch"] = alg[k]
