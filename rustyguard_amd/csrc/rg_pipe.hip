@@ -77,12 +77,17 @@ __device__ __forceinline__ void absorb_chunk(Acc &h, const Chunk &c, const Mul &
 // a path with fewer memory operations, and since vmcnt counts stores as well
 // as loads it would then also wait for the last step's stores to be acked.
 // TAIL: the partial last chunk (cnt < 4 blocks), predicated, no prefetch.
+// Stores are shifted by one block so that each step writes one 64-byte
+// frame-aligned block (the payload starts 16 bytes into the frame): the
+// previous chunk's last block (prev; or the header, before the first chunk of
+// a sealed frame) and this chunk's first three.  Lines written piecewise across
+// steps were measured at 1.66x the algorithmic write bytes (profiles/).
 // MODE (seal diagnostics, rg_set_debug_mode): 0 normal; 1 compute only (no
 // payload loads or stores, loop-carried fake data); 2 memory only (no
 // keystream and no Poly1305); 4/5/6 non-temporal loads / stores / both.
 template <bool OPEN, bool ABSORB, bool TAIL, int MODE = 0>
 __device__ __forceinline__ void pipe_step(uint4 *pl, const Stream &st, const Mul &r, Acc &h, Chunk &pi, Chunk &buf,
-                                          uint32_t t, uint32_t nb, uint32_t c0) {
+                                          uint4 &prev, bool &have_prev, uint32_t t, uint32_t nb, uint32_t c0) {
     uint32_t ks[16];
     if constexpr (MODE == 2) {
 #pragma unroll
@@ -107,14 +112,19 @@ __device__ __forceinline__ void pipe_step(uint4 *pl, const Stream &st, const Mul
     constexpr int NT = MODE >= 4 ? MODE - 3 : 0;
     if constexpr (TAIL) {
         const uint32_t cnt = nb & 3u;
+        if (have_prev) st16<NT>(dst - 1, prev);
         st16<NT>(dst + 0, x.q0); // cnt >= 1
         if (cnt > 1) st16<NT>(dst + 1, x.q1);
         if (cnt > 2) st16<NT>(dst + 2, x.q2);
+        have_prev = false;
     } else {
+        if constexpr (ABSORB) st16<NT>(dst - 1, prev); // inside the loop there always is one
+        else if (have_prev) st16<NT>(dst - 1, prev);
         st16<NT>(dst + 0, x.q0);
         st16<NT>(dst + 1, x.q1);
         st16<NT>(dst + 2, x.q2);
-        st16<NT>(dst + 3, x.q3);
+        prev = x.q3;
+        have_prev = true;
     }
     pi = OPEN ? buf : x;
     if constexpr (!TAIL) load_chunk<NT>(buf, pl, t + 2, nb - 1);
@@ -125,31 +135,39 @@ __device__ __forceinline__ void pipe_step(uint4 *pl, const Stream &st, const Mul
 // c0 + 1); b0 / b1 hold its chunks 0 / 1 (loads already issued).  The
 // first step is peeled (nothing to absorb yet), so that every absorb inside
 // the loop is unconditional; chunk c always lives in buffer c % 2.
+// head / has_head: the DataHeader a seal writes in front of the payload (only
+// the lane whose segment starts the payload has one).
 template <bool OPEN, int MODE = 0>
 __device__ __forceinline__ Acc pipe_pass(uint4 *pl, const Stream &st, const Mul &r, uint32_t nb, uint32_t c0,
-                                         Chunk &b0, Chunk &b1) {
+                                         Chunk &b0, Chunk &b1, uint4 head, bool has_head) {
     const uint32_t F = nb >> 2, bl = nb & 3u; // full chunks, blocks in the partial last chunk
     Acc h = {0, 0, 0, 0, 0};
     Chunk pi = {};
+    uint4 prev = head; // block still to be stored just in front of the current chunk
+    bool have_prev = has_head;
     uint32_t pending = 0; // blocks of pi not yet absorbed
     if (F > 0) {
-        pipe_step<OPEN, false, false, MODE>(pl, st, r, h, pi, b0, 0, nb, c0);
+        pipe_step<OPEN, false, false, MODE>(pl, st, r, h, pi, b0, prev, have_prev, 0, nb, c0);
         uint32_t t = 1;
         // whole pairs only: a step that may be skipped would leave the waitcnt
         // pass a path without its memory operations (vmcnt(0) at the next one)
         for (; t + 1 < F; t += 2) {
-            pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b1, t, nb, c0);
-            pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b0, t + 1, nb, c0);
+            pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0);
+            pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b0, prev, have_prev, t + 1, nb, c0);
         }
-        if (t < F) pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b1, t, nb, c0);
+        if (t < F) pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0);
         pending = 4;
     }
     if (bl > 0) {
-        Chunk &bp = (F & 1u) ? b1 : b0;
-        if (F > 0) pipe_step<OPEN, true, true, MODE>(pl, st, r, h, pi, bp, F, nb, c0);
-        else pipe_step<OPEN, false, true, MODE>(pl, st, r, h, pi, bp, F, nb, c0);
+        // chunk F lives in b(F % 2); select by value (a reference select
+        // between the two buffers would move both to scratch memory)
+        const bool odd = F & 1u;
+        Chunk bp = {odd ? b1.q0 : b0.q0, odd ? b1.q1 : b0.q1, odd ? b1.q2 : b0.q2, odd ? b1.q3 : b0.q3};
+        if (F > 0) pipe_step<OPEN, true, true, MODE>(pl, st, r, h, pi, bp, prev, have_prev, F, nb, c0);
+        else pipe_step<OPEN, false, true, MODE>(pl, st, r, h, pi, bp, prev, have_prev, F, nb, c0);
         pending = bl;
     }
+    if (have_prev && MODE != 1) st16<(MODE >= 4 ? MODE - 3 : 0)>(pl + 4 * F - 1, prev);
     absorb_chunk(h, pi, r, pending); // the last chunk's blocks
     return h;
 }
@@ -255,13 +273,15 @@ __device__ __forceinline__ void pipe_seal_packet(const SealArgs &a, uint32_t i, 
     uint32_t ks[16];
     stream_block(stm, 0, ks); // RFC 8439 §2.6 one-time key
     const Mul r = make_mul(ks[0], ks[1], ks[2], ks[3]);
-    Acc h = pipe_pass<false, MODE>(pl, stm, r, sg.nb, sg.c0, b0, b1);
+    // DataHeader {4, receiver, counter} (rustyguard-core/src/lib.rs:286-290), stored by segment 0
+    // together with the first payload blocks
+    const bool head = a.receivers != nullptr && j == 0;
+    const uint4 hdr = make_uint4(4u, head ? a.receivers[d.key_idx] : 0u, n1, n2);
+    Acc h = pipe_pass<false, MODE>(pl, stm, r, sg.nb, sg.c0, b0, b1, hdr, head);
     h = combine_segments(h, r, sg.after, G);
     if (j != 0) return;
     uint32_t tag[4];
     pipe_tag(h, r, P, ks + 4, tag);
-    if (a.receivers) // DataHeader {4, receiver, counter} (rustyguard-core/src/lib.rs:286-290)
-        *reinterpret_cast<uint4 *>(frame) = make_uint4(4u, a.receivers[d.key_idx], n1, n2);
     *reinterpret_cast<uint4 *>(frame + 16 + P) = make_uint4(tag[0], tag[1], tag[2], tag[3]);
     if (a.status) a.status[i] = RG_PKT_OK;
 }
@@ -314,7 +334,7 @@ __device__ __forceinline__ void pipe_open_packet(const OpenArgs &a, uint32_t i, 
     uint32_t ks[16];
     stream_block(stm, 0, ks);
     const Mul r = make_mul(ks[0], ks[1], ks[2], ks[3]);
-    Acc h = pipe_pass<true>(pl, stm, r, sg.nb, sg.c0, b0, b1);
+    Acc h = pipe_pass<true>(pl, stm, r, sg.nb, sg.c0, b0, b1, make_uint4(0, 0, 0, 0), false);
     h = combine_segments(h, r, sg.after, G);
     uint32_t tag[4];
     pipe_tag(h, r, P, ks + 4, tag);
@@ -402,43 +422,61 @@ __global__ __launch_bounds__(64) void pipe_schedule_kernel(uint32_t *counts, uin
 // Planned order: wave w takes tiles w, w + W, ... of the size-ordered tile
 // list; lane l of a tile of class c is unit (tile - first tile of c) * 64 + l
 // of that class.
+//
+// Both orders share one loop, so the packet body has a single call site (two
+// would make the compiler emit it as a real function call: stack frame, kernel
+// arguments in scratch, ~250 VGPRs).
 template <typename Body>
-__device__ __forceinline__ void pipe_walk(uint32_t n, uint32_t lg, const PipePlan &pp, Body &&body) {
-    if (!pp.counts) {
-        const uint64_t units = (uint64_t)n << lg, stride = (uint64_t)gridDim.x * 256;
-        for (uint64_t u = blockIdx.x * 256 + threadIdx.x; u < units; u += stride)
-            body((uint32_t)(u >> lg), (uint32_t)u & ((1u << lg) - 1), 1u << lg);
-        return;
-    }
+__device__ __forceinline__ void pipe_walk(uint32_t n, uint32_t lg0, const PipePlan &pp, Body &&body) {
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t my_cnt = lane < kClasses ? pp.sched[kSchedCnt + lane] : 0;
-    const uint32_t my_start = lane < kClasses ? pp.sched[kSchedStart + lane] : 0;
-    const uint32_t my_lg = lane < kClasses ? pp.sched[kSchedLg + lane] : 0;
-    const uint32_t my_tiles = (uint32_t)((((uint64_t)my_cnt << my_lg) + 63) / 64);
-    const uint32_t total = pp.sched[2];
-    const uint32_t waves = gridDim.x * (blockDim.x / 64);
-    // static round robin over the size-ordered tiles (longest first): a single
-    // shared queue counter would serialise every wave's start on one atomic
-    for (uint32_t tile = uniform_u32(blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64); tile < total; tile += waves) {
-        const uint64_t hit = __ballot(lane < kClasses && my_start <= tile && tile < my_start + my_tiles);
-        const uint32_t c = uniform_u32((uint32_t)(__ffsll((unsigned long long)hit) - 1));
-        const uint32_t lgc = uniform_u32((uint32_t)__shfl((int)my_lg, (int)c));
-        const uint32_t cnt = uniform_u32((uint32_t)__shfl((int)my_cnt, (int)c));
-        const uint32_t u = (tile - uniform_u32((uint32_t)__shfl((int)my_start, (int)c))) * 64 + lane;
-        const uint32_t p = u >> lgc;
-        if (p < cnt) body(pp.lists[(uint64_t)c * pp.cap + p], u & ((1u << lgc) - 1), 1u << lgc);
+    const bool planned = pp.counts != nullptr;
+    uint32_t my_cnt = 0, my_start = 0, my_lg = 0, my_tiles = 0;
+    uint64_t total, first, stride;
+    if (planned) {
+        my_cnt = lane < kClasses ? pp.sched[kSchedCnt + lane] : 0;
+        my_start = lane < kClasses ? pp.sched[kSchedStart + lane] : 0;
+        my_lg = lane < kClasses ? pp.sched[kSchedLg + lane] : 0;
+        my_tiles = (uint32_t)((((uint64_t)my_cnt << my_lg) + 63) / 64);
+        // static round robin over the size-ordered tiles (longest first): a shared
+        // queue counter would serialise every wave on one atomic
+        total = pp.sched[2];
+        first = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+        stride = gridDim.x * (blockDim.x / 64);
+    } else { // lane units, grid-stride
+        total = (uint64_t)n << lg0;
+        first = blockIdx.x * 256 + threadIdx.x;
+        stride = (uint64_t)gridDim.x * 256;
+    }
+    for (uint64_t it = first; it < total; it += stride) {
+        uint32_t i, lg, u;
+        bool live = true;
+        if (planned) {
+            const uint32_t tile = (uint32_t)it;
+            const uint64_t hit = __ballot(lane < kClasses && my_start <= tile && tile < my_start + my_tiles);
+            const uint32_t c = uniform_u32((uint32_t)(__ffsll((unsigned long long)hit) - 1));
+            lg = uniform_u32((uint32_t)__shfl((int)my_lg, (int)c));
+            u = (tile - uniform_u32((uint32_t)__shfl((int)my_start, (int)c))) * 64 + lane;
+            const uint32_t p = u >> lg;
+            live = p < uniform_u32((uint32_t)__shfl((int)my_cnt, (int)c));
+            i = live ? pp.lists[(uint64_t)c * pp.cap + p] : 0;
+        } else {
+            lg = lg0;
+            u = (uint32_t)it;
+            i = (uint32_t)(it >> lg0);
+        }
+        if (live) body(i, u & ((1u << lg) - 1), 1u << lg);
     }
 }
 
 template <int MODE> __global__ __launch_bounds__(256) void pipe_seal_kernel(SealArgs a, uint32_t lg, PipePlan pp) {
     const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
-    pipe_walk(a.n, lg, pp, [&](uint32_t i, uint32_t j, uint32_t G) { pipe_seal_packet<MODE>(a, i, j, G); });
+    pipe_walk(a.n, lg, pp, [=](uint32_t i, uint32_t j, uint32_t G) { pipe_seal_packet<MODE>(a, i, j, G); });
     if (a.dbg) pipe_stamp(a.dbg, t0, r0);
 }
 
 __global__ __launch_bounds__(256) void pipe_open_kernel(OpenArgs a, uint32_t lg, PipePlan pp) {
     const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
-    pipe_walk(a.n, lg, pp, [&](uint32_t i, uint32_t j, uint32_t G) { pipe_open_packet(a, i, j, G); });
+    pipe_walk(a.n, lg, pp, [=](uint32_t i, uint32_t j, uint32_t G) { pipe_open_packet(a, i, j, G); });
     if (a.dbg) pipe_stamp(a.dbg, t0, r0);
 }
 
