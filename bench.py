@@ -31,6 +31,19 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, MI355X_MICROARCH.md "Chip-level parameters"
+# VALU ceilings measured on the MI355X by tools/microbench.hip (profiles/r1c_microbench.json, best
+# occupancy): ChaCha20 keystream bytes/s over the whole chip, and clamped Poly1305 bytes/s
+CHACHA_PEAK_GBS = 2610.0
+POLY_PEAK_GBS = 15765.0
+
+
+def valu_ceiling_gbs(desc_len, is_open: bool) -> float:
+    """Payload bytes/s the chip's VALU could seal (open) at the measured ChaCha20 / Poly1305 rates:
+    per packet ceil(P/64) + 1 keystream blocks (one-time key) and P/16 + 1 Poly1305 blocks."""
+    import numpy as np
+    P = np.asarray(desc_len, dtype=np.float64) - (32 if is_open else 0)
+    t = ((np.ceil(P / 64) + 1) * 64 / CHACHA_PEAK_GBS + (P / 16 + 1) * 16 / POLY_PEAK_GBS).sum()
+    return float(P.sum() / t) if t > 0 else 0.0
 METRIC = "GiB/s + Mpkt/s device-resident ChaCha20-Poly1305 seal/open, 1/2/4/8 MI355X"
 
 
@@ -287,6 +300,13 @@ def main():
     }
     if pmc:
         out["roofline"]["pmc_source"] = pmc.get("source")
+    # the bound that actually applies: integer VALU (ChaCha20 ARX + Poly1305 multiplies), see DESIGN.md §5
+    ceil_gbs = valu_ceiling_gbs(w.desc["len"], False)
+    pay_gbs = payload / (seal_ms / 1e3) / 1e9
+    out["valu_roofline"] = {"kernel": "seal", "achieved": round(pay_gbs, 2), "peak": round(ceil_gbs, 2),
+                            "unit": "GB/s of payload", "frac": round(pay_gbs / ceil_gbs, 4) if ceil_gbs else None,
+                            "basis": f"ChaCha20 {CHACHA_PEAK_GBS:.0f} GB/s + Poly1305 {POLY_PEAK_GBS:.0f} GB/s chip "
+                                     "rates measured by tools/microbench.hip; one-time-key block per packet"}
     if args.e2e and rank == 0:
         out["e2e"] = e2e_host(eng, w)
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
