@@ -105,6 +105,31 @@ int rg_seal_batch_dev(rg_ctx *ctx, const uint8_t *keys, const uint32_t *receiver
 int rg_open_batch_dev(rg_ctx *ctx, const uint8_t *keys, uint32_t nkeys, const rg_pkt_desc *desc, size_t n,
                       uint8_t *buf, size_t buf_len, uint8_t *status, uint64_t *counters_out, void *stream);
 
+/* ------------------------------------ device-side receiver resolution */
+/* The receiver-index -> session map of Sessions::decrypt_packet
+ * (rustyguard-core/src/lib.rs:646-650, `peers_by_session`) as an
+ * open-addressing table: slot = (receiver * 0x9E3779B1) >> (32 - log2 cap),
+ * linear probing, key_idx == RG_KEY_SKIP marks an empty slot.  Built on the
+ * host (cap a power of two >= 2 n; receivers unique), used on the device. */
+typedef struct rg_rx_entry {
+    uint32_t receiver;
+    uint32_t key_idx;
+} rg_rx_entry;
+int rg_rx_table_build(const uint32_t *receivers, const uint32_t *key_idx, size_t n, rg_rx_entry *table,
+                      uint32_t cap);
+/* host lookup: key index, or -1 when the receiver has no session */
+int64_t rg_rx_table_find(const rg_rx_entry *table, uint32_t cap, uint32_t receiver);
+/* rg_open_batch_dev for frames straight off the wire: desc[i].key_idx is
+ * ignored; each frame's session comes from its header's receiver index through
+ * rx_table (device memory), in the reference's check order -- alignment,
+ * message type and 16-byte framing first (their statuses as rg_open_batch_dev),
+ * then an unknown receiver is RG_PKT_REJECTED (`Error::Rejected`, lib.rs:
+ * 647-650), then the AEAD.  key_idx_out (device, may be NULL) receives the
+ * resolved key index (RG_KEY_SKIP when none) for the host's anti-replay pass. */
+int rg_open_batch_dev_rx(rg_ctx *ctx, const uint8_t *keys, uint32_t nkeys, const rg_rx_entry *rx_table,
+                         uint32_t rx_cap, const rg_pkt_desc *desc, size_t n, uint8_t *buf, size_t buf_len,
+                         uint8_t *status, uint64_t *counters_out, uint32_t *key_idx_out, void *stream);
+
 /* Tuning knobs.  lanes: lanes cooperating on one packet (0 = automatic, else
  * 1/2/4).  wg_per_cu: resident 256-thread workgroups per CU of the persistent
  * grid (0 = automatic, -1 = plain one-shot grid). */

@@ -44,6 +44,8 @@ def lib():
         L.rg_oracle_aead_open.restype = ctypes.c_int
         L.rg_oracle_seal_batch.argtypes = [u8p, u8p, u8p, u8p, ctypes.c_size_t, u8p, u8p, ctypes.c_int]
         L.rg_oracle_open_batch.argtypes = [u8p, u8p, ctypes.c_size_t, u8p, u8p, u8p, ctypes.c_int]
+        L.rg_oracle_open_batch_rx.argtypes = [u8p, u8p, u8p, ctypes.c_size_t, u8p, ctypes.c_size_t, u8p, u8p, u8p,
+                                              u8p]
         L.rg_oracle_mix64.argtypes = [ctypes.c_uint64]
         L.rg_oracle_mix64.restype = ctypes.c_uint64
         L.rg_oracle_synth_fill.argtypes = [u8p, u8p, u8p, ctypes.c_size_t, ctypes.c_uint64]
@@ -125,6 +127,22 @@ def open_batch(keys: np.ndarray, desc: np.ndarray, buf: np.ndarray, nthreads: in
     ctr = np.zeros(max(n, 1), np.uint64)
     lib().rg_oracle_open_batch(_ptr(keys), _ptr(desc), n, _ptr(buf), _ptr(status), _ptr(ctr), nthreads)
     return status[:n], ctr[:n]
+
+
+def open_batch_rx(keys: np.ndarray, receivers, desc: np.ndarray, buf: np.ndarray):
+    """In-place open resolving each frame's session from its header receiver (session s has receiver
+    receivers[s] and key row s); returns (status u8[n], counters u64[n], key_idx u32[n])."""
+    assert desc.dtype == DESC_DTYPE and buf.dtype == np.uint8
+    keys = np.ascontiguousarray(keys, dtype=np.uint8)
+    rec = np.ascontiguousarray(receivers, np.uint32)
+    idx = np.arange(len(rec), dtype=np.uint32)
+    n = len(desc)
+    status = np.zeros(max(n, 1), np.uint8)
+    ctr = np.zeros(max(n, 1), np.uint64)
+    kout = np.zeros(max(n, 1), np.uint32)
+    lib().rg_oracle_open_batch_rx(_ptr(keys), _ptr(rec), _ptr(idx), len(rec), _ptr(desc), n, _ptr(buf),
+                                  _ptr(status), _ptr(ctr), _ptr(kout))
+    return status[:n], ctr[:n], kout[:n]
 
 
 def mix64(x: int) -> int:

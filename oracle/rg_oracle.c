@@ -325,6 +325,41 @@ void rg_oracle_open_one(const uint8_t *keys, const rg_oracle_desc *d, uint8_t *b
     *status = rc == 0 ? RG_ORACLE_OK : RG_ORACLE_DECRYPT_ERR;
 }
 
+/* Open of a frame straight off the wire (rustyguard-core/src/lib.rs:605-681):
+ * the same checks as rg_oracle_open_one, with Sessions::decrypt_packet's
+ * receiver -> session lookup (`peers_by_session.get_mut`, lib.rs:646-650;
+ * unknown -> Error::Rejected) between the DataHeader framing check and the
+ * AEAD.  Sessions are a plain list (receiver rx_rec[s], key row rx_key[s]),
+ * searched linearly: deliberately not the product's hash table. */
+void rg_oracle_open_one_rx(const uint8_t *keys, const uint32_t *rx_rec, const uint32_t *rx_key, size_t nrx,
+                           const rg_oracle_desc *d, uint8_t *buf, uint8_t *status, uint64_t *counter_out,
+                           uint32_t *key_out) {
+    uint8_t *frame = buf + d->offset;
+    uint32_t w = d->len;
+    if (counter_out) *counter_out = 0;
+    if (key_out) *key_out = 0xFFFFFFFFu;
+    if ((d->offset & 15) != 0) { *status = RG_ORACLE_UNALIGNED; return; }      /* lib.rs:613-615 */
+    if (w < 4) { *status = RG_ORACLE_INVALID; return; }                          /* lib.rs:619-620 */
+    if (ld32(frame) != 4u) { *status = RG_ORACLE_NOT_DATA; return; }             /* lib.rs:621-628 */
+    if ((w & 15) != 0 || w < 16) { *status = RG_ORACLE_INVALID; return; }        /* types lib.rs:181-196 */
+    const uint32_t receiver = ld32(frame + 4);
+    size_t s = 0;
+    while (s < nrx && rx_rec[s] != receiver) s++;
+    if (s == nrx) { *status = RG_ORACLE_REJECTED; return; }                      /* lib.rs:647-650 */
+    if (key_out) *key_out = rx_key[s];
+    rg_oracle_desc dk = *d;
+    dk.key_idx = rx_key[s];
+    rg_oracle_open_one(keys, &dk, buf, status, counter_out);
+}
+
+void rg_oracle_open_batch_rx(const uint8_t *keys, const uint32_t *rx_rec, const uint32_t *rx_key, size_t nrx,
+                             const rg_oracle_desc *desc, size_t n, uint8_t *buf, uint8_t *status,
+                             uint64_t *counters_out, uint32_t *key_out) {
+    for (size_t i = 0; i < n; i++)
+        rg_oracle_open_one_rx(keys, rx_rec, rx_key, nrx, &desc[i], buf, &status[i],
+                              counters_out ? &counters_out[i] : NULL, key_out ? &key_out[i] : NULL);
+}
+
 typedef struct {
     int open;
     const uint8_t *keys;

@@ -44,6 +44,14 @@ void rg_oracle_seal_batch(const uint8_t *keys, const uint32_t *receivers, const 
                           const uint64_t *counters, size_t n, uint8_t *buf, uint8_t *status, int nthreads);
 void rg_oracle_open_batch(const uint8_t *keys, const rg_oracle_desc *desc, size_t n, uint8_t *buf,
                           uint8_t *status, uint64_t *counters_out, int nthreads);
+/* open with the receiver -> session lookup of Sessions::decrypt_packet
+ * (rustyguard-core/src/lib.rs:646-650); sessions as a plain list */
+void rg_oracle_open_one_rx(const uint8_t *keys, const uint32_t *rx_rec, const uint32_t *rx_key, size_t nrx,
+                           const rg_oracle_desc *d, uint8_t *buf, uint8_t *status, uint64_t *counter_out,
+                           uint32_t *key_out);
+void rg_oracle_open_batch_rx(const uint8_t *keys, const uint32_t *rx_rec, const uint32_t *rx_key, size_t nrx,
+                             const rg_oracle_desc *desc, size_t n, uint8_t *buf, uint8_t *status,
+                             uint64_t *counters_out, uint32_t *key_out);
 
 uint64_t rg_oracle_mix64(uint64_t x);
 void rg_oracle_synth_fill(uint8_t *buf, const rg_oracle_desc *desc, const uint32_t *inner_len, size_t n,

@@ -156,6 +156,16 @@ class Engine:
                                         _vp(status), _vp(counters_out), _stream_handle(stream)),
               "rg_open_batch_dev")
 
+    def open_dev_rx(self, keys, rx_table, desc, buf, status, counters_out=None, key_idx_out=None, stream=None):
+        """Open frames straight off the wire: sessions resolved on the device from each header's receiver
+        index through rx_table (an rx_table() array moved to this device)."""
+        n = _ndesc(desc)
+        nkeys = _nbytes(keys) // 32
+        cap = _nbytes(rx_table) // 8
+        check(self._L.rg_open_batch_dev_rx(self._h, _vp(keys), nkeys, _vp(rx_table), cap, _vp(desc), n, _vp(buf),
+                                           _nbytes(buf), _vp(status), _vp(counters_out), _vp(key_idx_out),
+                                           _stream_handle(stream)), "rg_open_batch_dev_rx")
+
     def synth_fill_dev(self, desc, inner_len, buf, seed: int, stream=None):
         n = _ndesc(desc)
         check(self._L.rg_synth_fill_dev(self._h, _vp(desc), _vp(inner_len), n, _vp(buf), _nbytes(buf), seed,
@@ -317,6 +327,23 @@ class Sessions:
         check(lib().rg_recv_batch(self._h, _vp(desc), n, _vp(buf), buf.nbytes, _vp(status), _vp(slots)),
               "rg_recv_batch")
         return status[:n], slots[:n]
+
+
+def rx_table(receivers, key_idx, cap: int | None = None) -> np.ndarray:
+    """Receiver-index table for open_dev_rx (rg_rx_table_build): uint32 [cap, 2] of (receiver, key_idx),
+    cap a power of two >= 2 n (default: the smallest)."""
+    rec = np.ascontiguousarray(receivers, np.uint32)
+    idx = np.ascontiguousarray(key_idx, np.uint32)
+    if cap is None:
+        cap = 1 << max(1, int(2 * len(rec) - 1).bit_length())
+    table = np.zeros((cap, 2), np.uint32)
+    check(lib().rg_rx_table_build(_vp(rec), _vp(idx), len(rec), _vp(table), cap), "rg_rx_table_build")
+    return table
+
+
+def rx_find(table: np.ndarray, receiver: int) -> int:
+    """Host lookup in an rx_table(): key index or -1."""
+    return int(lib().rg_rx_table_find(_vp(table), table.shape[0], receiver))
 
 
 def host_alloc(nbytes: int) -> np.ndarray:

@@ -162,6 +162,7 @@ struct rg_ctx {
     Slot slots[2];
     DevBuf d_keys, d_recv;
     DevBuf d_general;  // per-message drop-in arena
+    DevBuf d_rx_desc;  // rg_open_batch_dev_rx: resolved descriptors
     DevBuf d_jobs;
 };
 
@@ -228,6 +229,7 @@ void rg_destroy(rg_ctx *ctx) {
     ctx->d_keys.release();
     ctx->d_recv.release();
     ctx->d_general.release();
+    ctx->d_rx_desc.release();
     ctx->d_jobs.release();
     delete ctx;
 }
@@ -451,6 +453,51 @@ int rg_synth_fill_dev(rg_ctx *ctx, const rg_pkt_desc *desc, const uint32_t *inne
     RG_HIP(rg::launch_synth_fill(desc, inner_len, (uint32_t)n, buf, buf_len, seed, (hipStream_t)stream),
            "synth launch");
     return RG_OK;
+}
+
+int rg_rx_table_build(const uint32_t *receivers, const uint32_t *key_idx, size_t n, rg_rx_entry *table,
+                      uint32_t cap) {
+    if (!table || (n && (!receivers || !key_idx))) return set_err(RG_EINVAL, "rx table: null pointer");
+    if (cap == 0 || (cap & (cap - 1)) != 0 || (uint64_t)cap < 2ull * n)
+        return set_err(RG_EINVAL, "rx table: cap must be a power of two >= 2 n");
+    for (uint32_t s = 0; s < cap; ++s) table[s] = rg_rx_entry{0, RG_KEY_SKIP};
+    for (size_t i = 0; i < n; ++i) {
+        if (key_idx[i] == RG_KEY_SKIP) return set_err(RG_EINVAL, "rx table: key index RG_KEY_SKIP is reserved");
+        uint32_t s = rg::rx_slot(receivers[i], cap);
+        while (table[s].key_idx != RG_KEY_SKIP) {
+            if (table[s].receiver == receivers[i]) return set_err(RG_EINVAL, "rx table: duplicate receiver");
+            s = (s + 1) & (cap - 1);
+        }
+        table[s] = rg_rx_entry{receivers[i], key_idx[i]};
+    }
+    return RG_OK;
+}
+
+int64_t rg_rx_table_find(const rg_rx_entry *table, uint32_t cap, uint32_t receiver) {
+    if (!table || cap == 0 || (cap & (cap - 1)) != 0) return -1;
+    uint32_t s = rg::rx_slot(receiver, cap);
+    for (uint32_t probe = 0; probe < cap && table[s].key_idx != RG_KEY_SKIP; ++probe) {
+        if (table[s].receiver == receiver) return table[s].key_idx;
+        s = (s + 1) & (cap - 1);
+    }
+    return -1;
+}
+
+int rg_open_batch_dev_rx(rg_ctx *ctx, const uint8_t *keys, uint32_t nkeys, const rg_rx_entry *rx_table,
+                         uint32_t rx_cap, const rg_pkt_desc *desc, size_t n, uint8_t *buf, size_t buf_len,
+                         uint8_t *status, uint64_t *counters_out, uint32_t *key_idx_out, void *stream) {
+    int rc = check_ctx(ctx);
+    if (rc) return rc;
+    if (n == 0) return RG_OK;
+    if (!rx_table || rx_cap == 0 || (rx_cap & (rx_cap - 1)) != 0 || !desc || n > 0xFFFFFFFFull)
+        return set_err(RG_EINVAL, "open_rx: bad args");
+    // resolved descriptors live in the context: calls on one context are stream-ordered
+    RG_HIP(ctx->d_rx_desc.reserve(n * sizeof(rg_pkt_desc)), "rx descriptors");
+    auto *rd = static_cast<rg_pkt_desc *>(ctx->d_rx_desc.p);
+    RG_HIP(rg::launch_rx_resolve(desc, (uint32_t)n, buf, buf_len, rx_table, rx_cap, rd, key_idx_out,
+                                 (hipStream_t)stream),
+           "rx resolve launch");
+    return rg_open_batch_dev(ctx, keys, nkeys, rd, n, buf, buf_len, status, counters_out, stream);
 }
 
 void *rg_host_alloc(size_t bytes) {

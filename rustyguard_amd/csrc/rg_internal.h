@@ -102,6 +102,15 @@ struct PipePlan {
 hipError_t launch_pipe(const SealArgs *sa, const OpenArgs *oa, const Launch &L, const PipePlan *plan,
                        hipStream_t s);
 hipError_t prepare_pipe_kernels(int max_wg[2]); // [seal, open] resident 256-thread workgroups per CU
+// Receiver resolution pre-pass (rg_kernels.hip): out[i] = desc[i] with key_idx
+// taken from the frame header's receiver through the rx table (see
+// rg_open_batch_dev_rx); key_out may be nullptr.
+hipError_t launch_rx_resolve(const rg_pkt_desc *desc, uint32_t n, const uint8_t *buf, uint64_t buf_len,
+                             const rg_rx_entry *table, uint32_t cap, rg_pkt_desc *out, uint32_t *key_out,
+                             hipStream_t s);
+__host__ __device__ __forceinline__ uint32_t rx_slot(uint32_t receiver, uint32_t cap) {
+    return cap > 1 ? (receiver * 0x9E3779B1u) >> (32 - __builtin_ctz(cap)) : 0u;
+}
 hipError_t launch_general(GeneralJob *jobs, uint32_t njobs, uint8_t *arena, hipStream_t s);
 hipError_t launch_synth_fill(const rg_pkt_desc *desc, const uint32_t *inner_len, uint32_t n, uint8_t *buf,
                              uint64_t buf_len, uint64_t seed, hipStream_t s);

@@ -65,6 +65,51 @@ __global__ void general_kernel(GeneralJob *jobs, uint32_t njobs, uint8_t *arena)
     j.status = RG_PKT_OK;
 }
 
+// ------------------------------------------------------------ receivers
+// Device half of Sessions::decrypt_packet's lookup (rustyguard-core/src/lib.rs:
+// 605-650): only a frame that passes the checks the reference makes first
+// (16-byte alignment, in the buffer, message type 4, whole 16-byte segments of
+// at least one) is looked up; an unknown receiver becomes RG_KEY_SKIP, which
+// the open kernels report as RG_PKT_REJECTED.  Frames failing an earlier check
+// get key 0, so the open kernel reports that check's status.
+__global__ __launch_bounds__(256) void rx_resolve_kernel(const rg_pkt_desc *desc, uint32_t n, const uint8_t *buf,
+                                                         uint64_t buf_len, const rg_rx_entry *table, uint32_t cap,
+                                                         rg_pkt_desc *out, uint32_t *key_out) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    rg_pkt_desc d = desc[i];
+    const uint64_t W = d.len;
+    uint32_t k = 0, found = RG_KEY_SKIP;
+    if ((d.offset & 15u) == 0 && d.offset <= buf_len && W <= buf_len - d.offset && W >= 16 && (W & 15u) == 0) {
+        const uint4 hdr = *reinterpret_cast<const uint4 *>(buf + d.offset);
+        if (hdr.x == 4u) {
+            uint32_t s = rx_slot(hdr.y, cap);
+            for (uint32_t probe = 0; probe < cap; ++probe) {
+                const rg_rx_entry e = table[s];
+                if (e.key_idx == RG_KEY_SKIP) break;
+                if (e.receiver == hdr.y) {
+                    found = e.key_idx;
+                    break;
+                }
+                s = (s + 1) & (cap - 1);
+            }
+            k = found; // RG_KEY_SKIP when unknown: Error::Rejected
+        }
+    }
+    d.key_idx = k;
+    out[i] = d;
+    if (key_out) key_out[i] = found;
+}
+
+hipError_t launch_rx_resolve(const rg_pkt_desc *desc, uint32_t n, const uint8_t *buf, uint64_t buf_len,
+                             const rg_rx_entry *table, uint32_t cap, rg_pkt_desc *out, uint32_t *key_out,
+                             hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(rx_resolve_kernel, dim3((n + 255) / 256), dim3(256), 0, s, desc, n, buf, buf_len, table, cap,
+                       out, key_out);
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------------------- synth
 __global__ __launch_bounds__(256) void synth_fill_kernel(const rg_pkt_desc *desc, const uint32_t *inner_len,
                                                          uint32_t n, uint8_t *buf, uint64_t buf_len, uint64_t seed) {

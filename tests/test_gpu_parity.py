@@ -442,3 +442,78 @@ def test_frames_past_2_and_4_gib(engine, mode):
     del buf
     torch.cuda.empty_cache()
     _reset(engine)
+
+
+# ------------------------------------------------- device-side receiver lookup
+@pytest.mark.parametrize("mode", [("auto",), ("pipe", 0), ("tile", 2, 1, 0)], ids=_mode_id)
+def test_open_with_device_receiver_lookup(engine, mode):
+    _configure(engine, mode)
+    rng = np.random.default_rng(21)
+    nses, n = 6, 400
+    keys, rec, desc, ctr, buf = _random_batch(rng, n, nkeys=nses)
+    rec = np.unique(rng.integers(1, 2**32, 3 * nses, dtype=np.uint64).astype(np.uint32))[:nses]
+    sealed, st = _gpu_seal(engine, keys, rec, desc, ctr, buf)
+    assert (st == 0).all()
+    dopen = desc.copy()
+    dopen["len"] = desc["len"] + 32
+    dopen["key_idx"] = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)  # ignored by the rx path
+    wire = sealed.copy()
+    pick = rng.permutation(n)
+    unknown, data_type, forged = pick[:12], pick[12:20], pick[20:28]
+    for i in unknown:  # receiver without a session: header is not authenticated -> Error::Rejected
+        wire[desc["offset"][i] + 4:desc["offset"][i] + 8] = np.frombuffer(np.uint32(0xA5A5A5A5).tobytes(), np.uint8)
+    for i in data_type:
+        wire[desc["offset"][i]] = 1  # handshake initiation -> routed elsewhere
+    for i in forged:
+        wire[desc["offset"][i] + 16 + desc["len"][i]] ^= 0x80  # tag bit flip -> DecryptionError
+    table = aead.rx_table(rec, np.arange(nses, dtype=np.uint32))
+    want, wctr, wkey = oracle.open_batch_rx(keys, rec, dopen, wire.copy())
+    b = _dev(wire)
+    st = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    co = torch.zeros(n, dtype=torch.int64, device="cuda")
+    ko = torch.zeros(n, dtype=torch.int32, device="cuda")
+    engine.open_dev_rx(_dev(keys), _dev(table), _dev(dopen.view(np.uint8).reshape(-1, 16)), b, st, co, ko)
+    torch.cuda.synchronize()
+    st, back, ko = st.cpu().numpy(), b.cpu().numpy(), ko.cpu().numpy().view(np.uint32)
+    assert list(st) == list(want)
+    assert (co.cpu().numpy().view(np.uint64) == wctr).all()
+    resolved = (st == 0) | (st == 1)
+    assert (ko[resolved] == wkey[resolved]).all()
+    assert (st[unknown] == aead.PKT_REJECTED).all() and (st[data_type] == 5).all() and (st[forged] == 1).all()
+    ok = st == 0
+    assert ok.sum() == n - 28
+    assert (ko[ok] == desc["key_idx"][ok]).all() and (ko[unknown] == 0xFFFFFFFF).all()
+    for i in np.nonzero(ok)[0]:  # plaintext back in place, byte for byte
+        o, P = int(desc["offset"][i]), int(desc["len"][i])
+        assert (back[o + 16:o + 16 + P] == buf[o + 16:o + 16 + P]).all()
+    for i in np.nonzero(~ok)[0]:  # rejected frames are left as they came
+        o, W = int(dopen["offset"][i]), int(dopen["len"][i])
+        assert (back[o:o + W] == wire[o:o + W]).all()
+    _reset(engine)
+
+
+def test_receiver_lookup_check_order(engine):
+    """Crafted frames pin the reference's order: Unaligned / InvalidMessage / not-data before the
+    session lookup, Rejected (unknown receiver) before DecryptionError (too short for a tag)."""
+    _reset(engine)
+    keys = np.zeros((1, 32), np.uint8)
+    table = aead.rx_table([77], [0])
+    buf = np.zeros(1024, np.uint8)
+    cases = [  # (offset, W, type, receiver) -> status
+        (8, 48, 4, 77, aead.PKT_UNALIGNED),
+        (64, 40, 4, 99, aead.PKT_INVALID),        # not whole 16-byte segments: before the lookup
+        (128, 48, 1, 99, 5),                      # not a data message: before the lookup
+        (192, 16, 4, 99, aead.PKT_REJECTED),      # unknown session beats "no room for a tag"
+        (256, 16, 4, 77, 1),                      # known session, no tag -> DecryptionError
+        (320, 48, 4, 99, aead.PKT_REJECTED),
+        (384, 48, 4, 77, 1),                      # random tag
+    ]
+    desc = np.zeros(len(cases), DESC_DTYPE)
+    for i, (o, w, t, r, _) in enumerate(cases):
+        desc[i] = (o, w, 0)
+        buf[o:o + 4] = np.frombuffer(np.uint32(t).tobytes(), np.uint8)
+        buf[o + 4:o + 8] = np.frombuffer(np.uint32(r).tobytes(), np.uint8)
+    st = torch.zeros(len(cases), dtype=torch.uint8, device="cuda")
+    engine.open_dev_rx(_dev(keys), _dev(table), _dev(desc.view(np.uint8).reshape(-1, 16)), _dev(buf), st)
+    torch.cuda.synchronize()
+    assert list(st.cpu().numpy()) == [c[4] for c in cases]
