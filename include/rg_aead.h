@@ -5,6 +5,7 @@
  *   trait CryptoPrimatives (rustyguard-crypto/src/prim.rs:74-111)
  *     fn chacha20poly1305_enc(key, nonce, aad, payload, tag)      prim.rs:82-88
  *     fn chacha20poly1305_dec(key, nonce, aad, payload, tag)      prim.rs:89-95
+ *     fn xchacha20poly1305_enc / _dec (24-byte nonce)            prim.rs:97-110
  *   impl for Core (graviola 0.2.0 underneath)                     prim.rs:179-201
  *   EncryptionKey::encrypt  (counter++, nonce, seal)              prim.rs:376-399
  *   DecryptionKey::decrypt  (replay gate, open, mark_seen)        prim.rs:401-437
@@ -191,6 +192,15 @@ int rg_chacha20poly1305_enc(rg_ctx *ctx, const uint8_t key[32], const uint8_t no
                             size_t aad_len, uint8_t *payload, size_t len, uint8_t tag[16]);
 int rg_chacha20poly1305_dec(rg_ctx *ctx, const uint8_t key[32], const uint8_t nonce[12], const uint8_t *aad,
                             size_t aad_len, uint8_t *payload, size_t len, const uint8_t tag[16]);
+
+/* Core::xchacha20poly1305_enc / _dec (prim.rs:202-224; decl :97-110), the
+ * cookie-reply AEAD (encrypt_cookie / decrypt_cookie, rustyguard-crypto/src/
+ * lib.rs:50-70): HChaCha20(key, nonce[0..16]) subkey, then ChaCha20-Poly1305
+ * with nonce 0^4 || nonce[16..24].  Same contract as the pair above. */
+int rg_xchacha20poly1305_enc(rg_ctx *ctx, const uint8_t key[32], const uint8_t nonce[24], const uint8_t *aad,
+                             size_t aad_len, uint8_t *payload, size_t len, uint8_t tag[16]);
+int rg_xchacha20poly1305_dec(rg_ctx *ctx, const uint8_t key[32], const uint8_t nonce[24], const uint8_t *aad,
+                             size_t aad_len, uint8_t *payload, size_t len, const uint8_t tag[16]);
 
 /* ---------------------------------------------- host-side session layer */
 /* AntiReplay: RFC 6479 window, 2048-bit bitmap, WINDOW_SIZE = 1984

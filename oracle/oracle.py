@@ -44,6 +44,10 @@ def lib():
         L.rg_oracle_aead_open.restype = ctypes.c_int
         L.rg_oracle_seal_batch.argtypes = [u8p, u8p, u8p, u8p, ctypes.c_size_t, u8p, u8p, ctypes.c_int]
         L.rg_oracle_open_batch.argtypes = [u8p, u8p, ctypes.c_size_t, u8p, u8p, u8p, ctypes.c_int]
+        L.rg_oracle_hchacha20.argtypes = [u8p, u8p, u8p]
+        L.rg_oracle_xaead_seal.argtypes = [u8p, u8p, u8p, ctypes.c_size_t, u8p, ctypes.c_size_t, u8p]
+        L.rg_oracle_xaead_open.argtypes = [u8p, u8p, u8p, ctypes.c_size_t, u8p, ctypes.c_size_t, u8p]
+        L.rg_oracle_xaead_open.restype = ctypes.c_int
         L.rg_oracle_open_batch_rx.argtypes = [u8p, u8p, u8p, ctypes.c_size_t, u8p, ctypes.c_size_t, u8p, u8p, u8p,
                                               u8p]
         L.rg_oracle_mix64.argtypes = [ctypes.c_uint64]
@@ -105,6 +109,30 @@ def aead_open(key: bytes, nonce: bytes, aad: bytes, ct: bytes, tag: bytes):
     rc = lib().rg_oracle_aead_open(_ptr(_u8(key)), _ptr(_u8(nonce)), _ptr(a), len(aad), _ptr(buf), len(ct),
                                    _ptr(_u8(tag)))
     return None if rc != 0 else buf.tobytes()[: len(ct)]
+
+
+def hchacha20(key: bytes, nonce16: bytes) -> bytes:
+    out = np.zeros(32, np.uint8)
+    lib().rg_oracle_hchacha20(_ptr(_u8(key)), _ptr(_u8(nonce16)), _ptr(out))
+    return out.tobytes()
+
+
+def xaead_seal(key: bytes, nonce24: bytes, aad: bytes, pt: bytes) -> tuple[bytes, bytes]:
+    """XChaCha20-Poly1305 (Core::xchacha20poly1305_enc, prim.rs:202-212): (ciphertext, tag)."""
+    buf = _u8(pt).copy() if pt else np.zeros(1, np.uint8)
+    tag = np.zeros(16, np.uint8)
+    a = _u8(aad) if aad else np.zeros(1, np.uint8)
+    lib().rg_oracle_xaead_seal(_ptr(_u8(key)), _ptr(_u8(nonce24)), _ptr(a), len(aad), _ptr(buf), len(pt), _ptr(tag))
+    return buf[:len(pt)].tobytes(), tag.tobytes()
+
+
+def xaead_open(key: bytes, nonce24: bytes, aad: bytes, ct: bytes, tag: bytes):
+    """Plaintext, or None on a tag mismatch (CryptoError::DecryptionError)."""
+    buf = _u8(ct).copy() if ct else np.zeros(1, np.uint8)
+    a = _u8(aad) if aad else np.zeros(1, np.uint8)
+    rc = lib().rg_oracle_xaead_open(_ptr(_u8(key)), _ptr(_u8(nonce24)), _ptr(a), len(aad), _ptr(buf), len(ct),
+                                    _ptr(_u8(tag)))
+    return None if rc != 0 else buf[:len(ct)].tobytes()
 
 
 def seal_batch(keys: np.ndarray, receivers, desc: np.ndarray, counters: np.ndarray, buf: np.ndarray,

@@ -278,6 +278,52 @@ int rg_oracle_aead_open(const uint8_t key[32], const uint8_t nonce[12], const ui
     return 0;
 }
 
+/* XChaCha20-Poly1305 (draft-irtf-cfrg-xchacha-03 §2.2-2.3), the cookie AEAD of
+ * Core::xchacha20poly1305_{enc,dec} (rustyguard-crypto/src/prim.rs:202-224):
+ * subkey = HChaCha20(key, nonce[0..16]) -- the 20 rounds with no feed-forward,
+ * words 0-3 and 12-15 -- then ChaCha20-Poly1305 with nonce 0^4 || nonce[16..24]. */
+void rg_oracle_hchacha20(const uint8_t key[32], const uint8_t nonce16[16], uint8_t out[32]) {
+    uint32_t x[16];
+    x[0] = 0x61707865u;
+    x[1] = 0x3320646eu;
+    x[2] = 0x79622d32u;
+    x[3] = 0x6b206574u;
+    for (int i = 0; i < 8; i++) x[4 + i] = ld32(key + 4 * i);
+    for (int i = 0; i < 4; i++) x[12 + i] = ld32(nonce16 + 4 * i);
+    for (int round = 0; round < 10; round++) {
+        QROUND(x, 0, 4, 8, 12);
+        QROUND(x, 1, 5, 9, 13);
+        QROUND(x, 2, 6, 10, 14);
+        QROUND(x, 3, 7, 11, 15);
+        QROUND(x, 0, 5, 10, 15);
+        QROUND(x, 1, 6, 11, 12);
+        QROUND(x, 2, 7, 8, 13);
+        QROUND(x, 3, 4, 9, 14);
+    }
+    for (int i = 0; i < 4; i++) st32(out + 4 * i, x[i]);
+    for (int i = 0; i < 4; i++) st32(out + 16 + 4 * i, x[12 + i]);
+}
+
+static void xchacha_subkey(const uint8_t key[32], const uint8_t nonce24[24], uint8_t sub[32], uint8_t n12[12]) {
+    rg_oracle_hchacha20(key, nonce24, sub);
+    memset(n12, 0, 4);
+    memcpy(n12 + 4, nonce24 + 16, 8);
+}
+
+void rg_oracle_xaead_seal(const uint8_t key[32], const uint8_t nonce24[24], const uint8_t *aad, size_t aad_len,
+                          uint8_t *payload, size_t len, uint8_t tag[16]) {
+    uint8_t sub[32], n12[12];
+    xchacha_subkey(key, nonce24, sub, n12);
+    rg_oracle_aead_seal(sub, n12, aad, aad_len, payload, len, tag);
+}
+
+int rg_oracle_xaead_open(const uint8_t key[32], const uint8_t nonce24[24], const uint8_t *aad, size_t aad_len,
+                         uint8_t *payload, size_t len, const uint8_t tag[16]) {
+    uint8_t sub[32], n12[12];
+    xchacha_subkey(key, nonce24, sub, n12);
+    return rg_oracle_aead_open(sub, n12, aad, aad_len, payload, len, tag);
+}
+
 /* prim.rs:32-36 */
 void rg_oracle_wg_nonce(uint64_t counter, uint8_t nonce[12]) {
     memset(nonce, 0, 4);

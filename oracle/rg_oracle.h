@@ -42,6 +42,12 @@ void rg_oracle_open_one(const uint8_t *keys, const rg_oracle_desc *d, uint8_t *b
                         uint64_t *counter_out);
 void rg_oracle_seal_batch(const uint8_t *keys, const uint32_t *receivers, const rg_oracle_desc *desc,
                           const uint64_t *counters, size_t n, uint8_t *buf, uint8_t *status, int nthreads);
+/* XChaCha20-Poly1305 cookie AEAD (rustyguard-crypto/src/prim.rs:202-224) */
+void rg_oracle_hchacha20(const uint8_t key[32], const uint8_t nonce16[16], uint8_t out[32]);
+void rg_oracle_xaead_seal(const uint8_t key[32], const uint8_t nonce24[24], const uint8_t *aad, size_t aad_len,
+                          uint8_t *payload, size_t len, uint8_t tag[16]);
+int rg_oracle_xaead_open(const uint8_t key[32], const uint8_t nonce24[24], const uint8_t *aad, size_t aad_len,
+                         uint8_t *payload, size_t len, const uint8_t tag[16]);
 void rg_oracle_open_batch(const uint8_t *keys, const rg_oracle_desc *desc, size_t n, uint8_t *buf,
                           uint8_t *status, uint64_t *counters_out, int nthreads);
 /* open with the receiver -> session lookup of Sessions::decrypt_packet

@@ -47,6 +47,8 @@ SIGNATURES = {
     "rg_host_free": (None, [c_vp]),
     "rg_chacha20poly1305_enc": (c_int, [c_vp, c_u8p, c_u8p, c_u8p, c_size, c_u8p, c_size, c_u8p]),
     "rg_chacha20poly1305_dec": (c_int, [c_vp, c_u8p, c_u8p, c_u8p, c_size, c_u8p, c_size, c_u8p]),
+    "rg_xchacha20poly1305_enc": (c_int, [c_vp, c_u8p, c_u8p, c_u8p, c_size, c_u8p, c_size, c_u8p]),
+    "rg_xchacha20poly1305_dec": (c_int, [c_vp, c_u8p, c_u8p, c_u8p, c_size, c_u8p, c_size, c_u8p]),
     "rg_antireplay_init": (None, [c_vp]),
     "rg_antireplay_would_accept": (c_int, [c_vp, c_u64]),
     "rg_antireplay_mark_seen": (None, [c_vp, c_u64]),

@@ -3,6 +3,8 @@
 Reference interface -> this module
   CryptoPrimatives::chacha20poly1305_enc/_dec (prim.rs:82-95, 179-201)
                                          -> Engine.chacha20poly1305_enc/_dec
+  CryptoPrimatives::xchacha20poly1305_enc/_dec (prim.rs:97-110, 202-224)
+                                         -> Engine.xchacha20poly1305_enc/_dec
   EncryptionKey {new, encrypt, counter}   (prim.rs:376-399) -> EncryptionKey
   DecryptionKey {new, decrypt}            (prim.rs:401-437) -> DecryptionKey
   AntiReplay {would_accept, mark_seen}    (anti_replay.rs:25-64) -> AntiReplay
@@ -201,6 +203,25 @@ class Engine:
         check(self._L.rg_chacha20poly1305_enc(self._h, _vp(k), _vp(nz), _vp(a), len(aad), _vp(payload) if payload
                                               else None, len(payload), _vp(tag)), "rg_chacha20poly1305_enc")
         return bytes(tag)
+
+    def xchacha20poly1305_enc(self, key: bytes, nonce: bytes, aad: bytes, payload: bytearray) -> bytes:
+        """Core::xchacha20poly1305_enc (prim.rs:202-212, the cookie AEAD): in place, returns the tag."""
+        assert len(key) == 32 and len(nonce) == 24
+        tag = bytearray(16)
+        k, nz, a = bytearray(key), bytearray(nonce), bytearray(aad or b"\0")
+        check(self._L.rg_xchacha20poly1305_enc(self._h, _vp(k), _vp(nz), _vp(a), len(aad), _vp(payload) if payload
+                                               else None, len(payload), _vp(tag)), "rg_xchacha20poly1305_enc")
+        return bytes(tag)
+
+    def xchacha20poly1305_dec(self, key: bytes, nonce: bytes, aad: bytes, payload: bytearray, tag: bytes) -> None:
+        """Core::xchacha20poly1305_dec (prim.rs:214-224): decrypts in place or raises DecryptionError."""
+        assert len(key) == 32 and len(nonce) == 24 and len(tag) == 16
+        k, nz, a, t = bytearray(key), bytearray(nonce), bytearray(aad or b"\0"), bytearray(tag)
+        rc = check(self._L.rg_xchacha20poly1305_dec(self._h, _vp(k), _vp(nz), _vp(a), len(aad), _vp(payload)
+                                                    if payload else None, len(payload), _vp(t)),
+                   "rg_xchacha20poly1305_dec")
+        if rc == PKT_DECRYPT_ERR:
+            raise DecryptionError()
 
     def chacha20poly1305_dec(self, key: bytes, nonce: bytes, aad: bytes, payload: bytearray, tag: bytes) -> None:
         """Core::chacha20poly1305_dec: decrypts in place or raises DecryptionError."""

@@ -672,8 +672,9 @@ int rg_open_batch_host(rg_ctx *ctx, const uint8_t *keys, uint32_t nkeys, const r
 }
 
 // ---------------------------------------------------- per-message drop-in
-static int general_one(rg_ctx *ctx, bool dec, const uint8_t key[32], const uint8_t nonce[12], const uint8_t *aad,
-                       size_t aad_len, uint8_t *payload, size_t len, uint8_t tag[16]) {
+// nonce: 12 bytes, or 24 for XChaCha20-Poly1305 (xchacha)
+static int general_one(rg_ctx *ctx, bool dec, const uint8_t key[32], const uint8_t *nonce, const uint8_t *aad,
+                       size_t aad_len, uint8_t *payload, size_t len, uint8_t tag[16], bool xchacha = false) {
     int rc = check_ctx(ctx);
     if (rc) return rc;
     if (!key || !nonce || !tag || (aad_len && !aad) || (len && !payload))
@@ -688,7 +689,13 @@ static int general_one(rg_ctx *ctx, bool dec, const uint8_t key[32], const uint8
     rg::GeneralJob job;
     memset(&job, 0, sizeof job);
     memcpy(job.key, key, 32);
-    memcpy(job.nonce, nonce, 12);
+    if (xchacha) { // HChaCha20 input nonce[0..16]; ChaCha20-Poly1305 nonce 0^4 || nonce[16..24]
+        job.xchacha = 1;
+        memcpy(job.hnonce, nonce, 16);
+        memcpy(reinterpret_cast<uint8_t *>(job.nonce) + 4, nonce + 16, 8);
+    } else {
+        memcpy(job.nonce, nonce, 12);
+    }
     job.decrypt = dec ? 1 : 0;
     job.aad_off = aad_off;
     job.aad_len = aad_len;
@@ -717,6 +724,16 @@ int rg_chacha20poly1305_enc(rg_ctx *ctx, const uint8_t key[32], const uint8_t no
 int rg_chacha20poly1305_dec(rg_ctx *ctx, const uint8_t key[32], const uint8_t nonce[12], const uint8_t *aad,
                             size_t aad_len, uint8_t *payload, size_t len, const uint8_t tag[16]) {
     return general_one(ctx, true, key, nonce, aad, aad_len, payload, len, const_cast<uint8_t *>(tag));
+}
+
+int rg_xchacha20poly1305_enc(rg_ctx *ctx, const uint8_t key[32], const uint8_t nonce[24], const uint8_t *aad,
+                             size_t aad_len, uint8_t *payload, size_t len, uint8_t tag[16]) {
+    return general_one(ctx, false, key, nonce, aad, aad_len, payload, len, tag, true);
+}
+
+int rg_xchacha20poly1305_dec(rg_ctx *ctx, const uint8_t key[32], const uint8_t nonce[24], const uint8_t *aad,
+                             size_t aad_len, uint8_t *payload, size_t len, const uint8_t tag[16]) {
+    return general_one(ctx, true, key, nonce, aad, aad_len, payload, len, const_cast<uint8_t *>(tag), true);
 }
 
 // ------------------------------------------------------------- AntiReplay

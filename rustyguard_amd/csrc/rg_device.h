@@ -74,6 +74,27 @@ __device__ __forceinline__ void chacha_block(const Key8 &key, uint32_t block, ui
     out[15] = x15 + n2;
 }
 
+// HChaCha20 (draft-irtf-cfrg-xchacha-03 §2.2): the ChaCha20 rounds over
+// consts | key | nonce16 with no feed-forward; the subkey is words 0-3, 12-15.
+__device__ __forceinline__ Key8 hchacha20(const Key8 &key, const uint32_t n[4]) {
+    uint32_t x0 = 0x61707865u, x1 = 0x3320646eu, x2 = 0x79622d32u, x3 = 0x6b206574u;
+    uint32_t x4 = key.k[0], x5 = key.k[1], x6 = key.k[2], x7 = key.k[3];
+    uint32_t x8 = key.k[4], x9 = key.k[5], x10 = key.k[6], x11 = key.k[7];
+    uint32_t x12 = n[0], x13 = n[1], x14 = n[2], x15 = n[3];
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+        RG_QR(x0, x4, x8, x12);
+        RG_QR(x1, x5, x9, x13);
+        RG_QR(x2, x6, x10, x14);
+        RG_QR(x3, x7, x11, x15);
+        RG_QR(x0, x5, x10, x15);
+        RG_QR(x1, x6, x11, x12);
+        RG_QR(x2, x7, x8, x13);
+        RG_QR(x3, x4, x9, x14);
+    }
+    return Key8{{x0, x1, x2, x3, x12, x13, x14, x15}};
+}
+
 // Per-packet ChaCha20 state with the block-counter-independent part of the
 // first column round hoisted: of QR(0,4,8,12) QR(1,5,9,13) QR(2,6,10,14)
 // QR(3,7,11,15) only the first reads word 12 (the block counter), so the other

@@ -41,6 +41,8 @@ struct GeneralJob {
     uint32_t key[8];
     uint32_t nonce[3];
     uint32_t decrypt; // 0 seal, 1 open
+    uint32_t xchacha; // 1: key is first replaced by HChaCha20(key, hnonce) (XChaCha20-Poly1305)
+    uint32_t hnonce[4];
     uint64_t aad_off; // offsets into the job arena
     uint64_t aad_len;
     uint64_t payload_off;

@@ -1,6 +1,7 @@
 // rg_kernels.hip -- the per-message CryptoPrimatives drop-in kernel (any
-// nonce, AAD and byte length: Core::chacha20poly1305_{enc,dec},
-// rustyguard-crypto/src/prim.rs:179-201) and the synthetic-payload generator
+// nonce, AAD and byte length: Core::chacha20poly1305_{enc,dec} and
+// Core::xchacha20poly1305_{enc,dec}, rustyguard-crypto/src/prim.rs:179-224),
+// the receiver-resolution pre-pass and the synthetic-payload generator
 // used by benches and tests.  The batched transport kernels live in
 // rg_pipe.hip (pipelined lanes) and rg_tile.hip (LDS-staged tiles).
 #include "rg_device.h"
@@ -27,6 +28,7 @@ __global__ void general_kernel(GeneralJob *jobs, uint32_t njobs, uint8_t *arena)
     GeneralJob &j = jobs[i];
     Key8 key;
     for (int t = 0; t < 8; ++t) key.k[t] = j.key[t];
+    if (j.xchacha) key = hchacha20(key, j.hnonce); // XChaCha20-Poly1305 subkey (prim.rs:202-224)
     uint32_t ks[16];
     chacha_block(key, 0, j.nonce[0], j.nonce[1], j.nonce[2], ks);
     const Mul r = make_mul(ks[0], ks[1], ks[2], ks[3]);

@@ -120,6 +120,22 @@ def test_reference_snapshots_per_message(engine):
         assert buf.hex() == v["plaintext"]
 
 
+def test_xchacha_per_message(engine):
+    """Core::xchacha20poly1305_{enc,dec} (cookie replies, rustyguard-crypto/src/lib.rs:50-70) on the GPU
+    against tests/golden/xchacha.json; a forged tag leaves the payload untouched."""
+    for v in load_golden("xchacha.json")["seals"]:
+        key, nonce, aad = bytes.fromhex(v["key"]), bytes.fromhex(v["nonce"]), bytes.fromhex(v["aad"])
+        buf = bytearray.fromhex(v["plaintext"])
+        tag = engine.xchacha20poly1305_enc(key, nonce, aad, buf)
+        assert buf.hex() == v["ciphertext"] and tag.hex() == v["tag"]
+        if buf:
+            with pytest.raises(aead.DecryptionError):
+                engine.xchacha20poly1305_dec(key, nonce, aad, buf, bytes([tag[0] ^ 0x40]) + tag[1:])
+            assert buf.hex() == v["ciphertext"]
+        engine.xchacha20poly1305_dec(key, nonce, aad, buf, tag)
+        assert buf.hex() == v["plaintext"]
+
+
 @pytest.mark.parametrize("mode", MODES, ids=_mode_id)
 def test_reference_framed_packet_batch(engine, mode):
     """rustyguard-core snapshot-3: the full 48-byte framed data packet."""

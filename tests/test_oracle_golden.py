@@ -118,3 +118,19 @@ def test_openssl_batch_baseline_matches_oracle():
     a[int(od["offset"][7]) + 20] ^= 1
     st = oracle.openssl_open_batch(w.keys, od, a, nthreads=1)
     assert st[7] == oracle.DECRYPT_ERR and (np.delete(st, 7) == 0).all()
+
+
+def test_xchacha_known_answer_and_vectors():
+    """XChaCha20-Poly1305 (the cookie AEAD, rustyguard-crypto/src/prim.rs:202-224): the oracle's
+    HChaCha20 reproduces draft-irtf-cfrg-xchacha-03 §2.2.1; the fixture seals open back and reject a
+    flipped tag."""
+    g = load_golden("xchacha.json")
+    k = g["hchacha20_kat"]
+    assert oracle.hchacha20(bytes.fromhex(k["key"]), bytes.fromhex(k["nonce"])).hex() == k["subkey"]
+    for v in g["seals"]:
+        key, nonce, aad = bytes.fromhex(v["key"]), bytes.fromhex(v["nonce"]), bytes.fromhex(v["aad"])
+        ct, tag = oracle.xaead_seal(key, nonce, aad, bytes.fromhex(v["plaintext"]))
+        assert ct.hex() == v["ciphertext"] and tag.hex() == v["tag"]
+        assert oracle.xaead_open(key, nonce, aad, ct, tag).hex() == v["plaintext"]
+        bad = bytes([tag[0] ^ 1]) + tag[1:]
+        assert oracle.xaead_open(key, nonce, aad, ct, bad) is None
