@@ -131,6 +131,21 @@ int rg_open_batch_dev_rx(rg_ctx *ctx, const uint8_t *keys, uint32_t nkeys, const
                          uint32_t rx_cap, const rg_pkt_desc *desc, size_t n, uint8_t *buf, size_t buf_len,
                          uint8_t *status, uint64_t *counters_out, uint32_t *key_idx_out, void *stream);
 
+/* ----------------------------------------- handshake MAC checks (batch) */
+/* HasMac::verify_mac1 / verify_mac2 (rustyguard-crypto/src/lib.rs:114-209)
+ * for n handshake messages (desc: offset, len = whole message incl. both
+ * macs): mac1 = BLAKE2s-128(keys[k], msg[..len-32]) against msg[len-32..
+ * len-16] (which = 1, 32-byte mac1 keys), mac2 = BLAKE2s-128(cookie,
+ * msg[..len-16]) against msg[len-16..] (which = 2, 16-byte cookies).
+ * status: RG_PKT_OK, RG_PKT_REJECTED (mismatch: CryptoError::Rejected),
+ * RG_PKT_UNALIGNED, RG_PKT_INVALID (len < 32 or outside buf).  key_idx
+ * RG_KEY_SCAN tries every key and reports the first match in key_idx_out
+ * (wg-proxy's peer scan, wg-proxy/src/main.rs:217-229).  Device pointers. */
+#define RG_KEY_SCAN 0xFFFFFFFEu
+int rg_mac_verify_batch_dev(rg_ctx *ctx, const uint8_t *keys, uint32_t key_len, uint32_t nkeys, int which,
+                            const rg_pkt_desc *desc, size_t n, const uint8_t *buf, size_t buf_len, uint8_t *status,
+                            uint32_t *key_idx_out, void *stream);
+
 /* Tuning knobs.  lanes: lanes cooperating on one packet (0 = automatic, else
  * 1/2/4).  wg_per_cu: resident 256-thread workgroups per CU of the persistent
  * grid (0 = automatic, -1 = plain one-shot grid). */

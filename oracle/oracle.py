@@ -45,6 +45,9 @@ def lib():
         L.rg_oracle_seal_batch.argtypes = [u8p, u8p, u8p, u8p, ctypes.c_size_t, u8p, u8p, ctypes.c_int]
         L.rg_oracle_open_batch.argtypes = [u8p, u8p, ctypes.c_size_t, u8p, u8p, u8p, ctypes.c_int]
         L.rg_oracle_hchacha20.argtypes = [u8p, u8p, u8p]
+        L.rg_oracle_blake2s.argtypes = [u8p, ctypes.c_size_t, u8p, ctypes.c_size_t, u8p, ctypes.c_size_t]
+        L.rg_oracle_mac_verify_batch.argtypes = [u8p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int, u8p,
+                                                 ctypes.c_size_t, u8p, u8p, u8p]
         L.rg_oracle_xaead_seal.argtypes = [u8p, u8p, u8p, ctypes.c_size_t, u8p, ctypes.c_size_t, u8p]
         L.rg_oracle_xaead_open.argtypes = [u8p, u8p, u8p, ctypes.c_size_t, u8p, ctypes.c_size_t, u8p]
         L.rg_oracle_xaead_open.restype = ctypes.c_int
@@ -109,6 +112,28 @@ def aead_open(key: bytes, nonce: bytes, aad: bytes, ct: bytes, tag: bytes):
     rc = lib().rg_oracle_aead_open(_ptr(_u8(key)), _ptr(_u8(nonce)), _ptr(a), len(aad), _ptr(buf), len(ct),
                                    _ptr(_u8(tag)))
     return None if rc != 0 else buf.tobytes()[: len(ct)]
+
+
+def blake2s(msg: bytes, key: bytes = b"", outlen: int = 32) -> bytes:
+    """RFC 7693 BLAKE2s (Core::blake2s_hash / blake2s_mac, rustyguard-crypto/src/prim.rs:118-131)."""
+    out = np.zeros(32, np.uint8)
+    m = _u8(msg) if msg else np.zeros(1, np.uint8)
+    k = _u8(key) if key else np.zeros(1, np.uint8)
+    lib().rg_oracle_blake2s(_ptr(out), outlen, _ptr(k), len(key), _ptr(m), len(msg))
+    return out[:outlen].tobytes()
+
+
+def mac_verify_batch(keys: np.ndarray, which: int, desc: np.ndarray, buf: np.ndarray):
+    """HasMac::verify_mac1 (which=1) / verify_mac2 (which=2) per handshake message; key_idx
+    0xFFFFFFFE scans every key (wg-proxy).  Returns (status u8[n], matched key u32[n])."""
+    assert desc.dtype == DESC_DTYPE and buf.dtype == np.uint8
+    keys = np.ascontiguousarray(keys, np.uint8)
+    n = len(desc)
+    status = np.zeros(max(n, 1), np.uint8)
+    kout = np.zeros(max(n, 1), np.uint32)
+    lib().rg_oracle_mac_verify_batch(_ptr(keys), keys.shape[1], keys.shape[0], which, _ptr(desc), n, _ptr(buf),
+                                     _ptr(status), _ptr(kout))
+    return status[:n], kout[:n]
 
 
 def hchacha20(key: bytes, nonce16: bytes) -> bytes:

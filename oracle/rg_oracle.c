@@ -324,6 +324,114 @@ int rg_oracle_xaead_open(const uint8_t key[32], const uint8_t nonce24[24], const
     return rg_oracle_aead_open(sub, n12, aad, aad_len, payload, len, tag);
 }
 
+/* ------------------------------------------------------------------------ */
+/* BLAKE2s (RFC 7693), keyed, any digest length 1..32: Core::blake2s_hash /    */
+/* Core::blake2s_mac (rustyguard-crypto/src/prim.rs:118-131, blake2s_simd).   */
+
+static const uint32_t B2S_IV[8] = {0x6A09E667u, 0xBB67AE85u, 0x3C6EF372u, 0xA54FF53Au,
+                                   0x510E527Fu, 0x9B05688Cu, 0x1F83D9ABu, 0x5BE0CD19u};
+static const uint8_t B2S_SIGMA[10][16] = {
+    {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15}, {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3},
+    {11, 8, 12, 0, 5, 2, 15, 13, 10, 14, 3, 6, 7, 1, 9, 4}, {7, 9, 3, 1, 13, 12, 11, 14, 2, 6, 5, 10, 4, 0, 15, 8},
+    {9, 0, 5, 7, 2, 4, 10, 15, 14, 1, 11, 12, 6, 8, 3, 13}, {2, 12, 6, 10, 0, 11, 8, 3, 4, 13, 7, 5, 15, 14, 1, 9},
+    {12, 5, 1, 15, 14, 13, 4, 10, 0, 7, 6, 3, 9, 2, 8, 11}, {13, 11, 7, 14, 12, 1, 3, 9, 5, 0, 15, 4, 8, 6, 2, 10},
+    {6, 15, 14, 9, 11, 3, 0, 8, 12, 2, 13, 7, 1, 4, 10, 5}, {10, 2, 8, 4, 7, 6, 1, 5, 15, 11, 9, 14, 3, 12, 13, 0}};
+
+static uint32_t rotr(uint32_t v, int n) { return (v >> n) | (v << (32 - n)); }
+
+static void b2s_compress(uint32_t h[8], const uint8_t block[64], uint64_t t, int last) {
+    uint32_t m[16], v[16];
+    for (int i = 0; i < 16; i++) m[i] = ld32(block + 4 * i);
+    for (int i = 0; i < 8; i++) { v[i] = h[i]; v[8 + i] = B2S_IV[i]; }
+    v[12] ^= (uint32_t)t;
+    v[13] ^= (uint32_t)(t >> 32);
+    if (last) v[14] = ~v[14];
+#define B2S_G(a, b, c, d, x, y)                                              \
+    do {                                                                     \
+        v[a] = v[a] + v[b] + x; v[d] = rotr(v[d] ^ v[a], 16);                \
+        v[c] = v[c] + v[d]; v[b] = rotr(v[b] ^ v[c], 12);                    \
+        v[a] = v[a] + v[b] + y; v[d] = rotr(v[d] ^ v[a], 8);                 \
+        v[c] = v[c] + v[d]; v[b] = rotr(v[b] ^ v[c], 7);                     \
+    } while (0)
+    for (int r = 0; r < 10; r++) {
+        const uint8_t *s = B2S_SIGMA[r];
+        B2S_G(0, 4, 8, 12, m[s[0]], m[s[1]]);
+        B2S_G(1, 5, 9, 13, m[s[2]], m[s[3]]);
+        B2S_G(2, 6, 10, 14, m[s[4]], m[s[5]]);
+        B2S_G(3, 7, 11, 15, m[s[6]], m[s[7]]);
+        B2S_G(0, 5, 10, 15, m[s[8]], m[s[9]]);
+        B2S_G(1, 6, 11, 12, m[s[10]], m[s[11]]);
+        B2S_G(2, 7, 8, 13, m[s[12]], m[s[13]]);
+        B2S_G(3, 4, 9, 14, m[s[14]], m[s[15]]);
+    }
+#undef B2S_G
+    for (int i = 0; i < 8; i++) h[i] ^= v[i] ^ v[8 + i];
+}
+
+/* RFC 7693 §3.3: parameter block word 0 = 0x01010000 ^ (kk << 8) ^ nn; a key
+ * is processed as a first, zero-padded block; the final block is flagged and
+ * zero-padded (an empty unkeyed message still compresses one empty block). */
+void rg_oracle_blake2s(uint8_t *out, size_t outlen, const uint8_t *key, size_t keylen, const uint8_t *msg,
+                       size_t len) {
+    uint32_t h[8];
+    for (int i = 0; i < 8; i++) h[i] = B2S_IV[i];
+    h[0] ^= 0x01010000u ^ ((uint32_t)keylen << 8) ^ (uint32_t)outlen;
+    uint8_t block[64];
+    uint64_t t = 0;
+    if (keylen) {
+        memset(block, 0, 64);
+        memcpy(block, key, keylen);
+        t = 64;
+        b2s_compress(h, block, t, len == 0);
+    }
+    size_t off = 0;
+    while (len - off > 64) {
+        t += 64;
+        b2s_compress(h, msg + off, t, 0);
+        off += 64;
+    }
+    if (len > off || !keylen) {
+        memset(block, 0, 64);
+        memcpy(block, msg + off, len - off);
+        t += len - off;
+        b2s_compress(h, block, t, 1);
+    }
+    uint8_t full[32];
+    for (int i = 0; i < 8; i++) st32(full + 4 * i, h[i]);
+    memcpy(out, full, outlen);
+}
+
+/* HasMac::verify_mac1 / verify_mac2 (rustyguard-crypto/src/lib.rs:114-209):
+ * mac1 = BLAKE2s-128(mac1_key, msg[..len-32]) must equal msg[len-32..len-16];
+ * mac2 = BLAKE2s-128(cookie, msg[..len-16]) must equal msg[len-16..]; a
+ * mismatch is CryptoError::Rejected.  key_idx RG_KEY_SCAN (0xFFFFFFFE) tries
+ * every key in order and keeps the first match, as wg-proxy's peer scan
+ * (wg-proxy/src/main.rs:217-229). */
+void rg_oracle_mac_verify_batch(const uint8_t *keys, size_t key_len, size_t nkeys, int which,
+                                const rg_oracle_desc *desc, size_t n, const uint8_t *buf, uint8_t *status,
+                                uint32_t *key_out) {
+    for (size_t i = 0; i < n; i++) {
+        const rg_oracle_desc *d = &desc[i];
+        key_out[i] = 0xFFFFFFFFu;
+        if ((d->offset & 15) != 0) { status[i] = RG_ORACLE_UNALIGNED; continue; }
+        if (d->len < 32) { status[i] = RG_ORACLE_INVALID; continue; }
+        const size_t covered = d->len - (which == 2 ? 16 : 32);
+        const uint8_t *msg = buf + d->offset;
+        size_t lo = d->key_idx, hi = d->key_idx + 1;
+        if (d->key_idx == 0xFFFFFFFEu) { lo = 0; hi = nkeys; }
+        status[i] = RG_ORACLE_REJECTED;
+        for (size_t k = lo; k < hi && k < nkeys; k++) {
+            uint8_t mac[16];
+            rg_oracle_blake2s(mac, 16, keys + key_len * k, key_len, msg, covered);
+            if (memcmp(mac, msg + covered, 16) == 0) {
+                status[i] = RG_ORACLE_OK;
+                key_out[i] = (uint32_t)k;
+                break;
+            }
+        }
+    }
+}
+
 /* prim.rs:32-36 */
 void rg_oracle_wg_nonce(uint64_t counter, uint8_t nonce[12]) {
     memset(nonce, 0, 4);

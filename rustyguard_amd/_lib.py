@@ -33,6 +33,8 @@ SIGNATURES = {
     "rg_set_wg_per_cu": (c_int, [c_vp, c_int]),
     "rg_set_debug_mode": (c_int, [c_vp, c_int]),
     "rg_set_staged": (c_int, [c_vp, c_int]),
+    "rg_mac_verify_batch_dev": (c_int, [c_vp, c_vp, ctypes.c_uint32, ctypes.c_uint32, c_int, c_vp, c_size, c_vp,
+                                        c_size, c_vp, c_vp, c_vp]),
     "rg_rx_table_build": (c_int, [c_vp, c_vp, c_size, c_vp, ctypes.c_uint32]),
     "rg_rx_table_find": (ctypes.c_int64, [c_vp, ctypes.c_uint32, ctypes.c_uint32]),
     "rg_open_batch_dev_rx": (c_int, [c_vp, c_vp, ctypes.c_uint32, c_vp, ctypes.c_uint32, c_vp, c_size, c_vp, c_size,

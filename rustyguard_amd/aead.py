@@ -27,6 +27,7 @@ from ._lib import check, lib
 from .workloads import DESC_DTYPE
 
 PKT_OK, PKT_DECRYPT_ERR, PKT_INVALID, PKT_REJECTED, PKT_UNALIGNED, PKT_NOT_DATA = range(6)
+KEY_SCAN = 0xFFFFFFFE  # rg_mac_verify_batch_dev: try every key
 KEY_SKIP = 0xFFFFFFFF
 REKEY_AFTER_MESSAGES = 1 << 60
 REJECT_AFTER_MESSAGES = (1 << 64) - 1 - (1 << 13)
@@ -167,6 +168,16 @@ class Engine:
         check(self._L.rg_open_batch_dev_rx(self._h, _vp(keys), nkeys, _vp(rx_table), cap, _vp(desc), n, _vp(buf),
                                            _nbytes(buf), _vp(status), _vp(counters_out), _vp(key_idx_out),
                                            _stream_handle(stream)), "rg_open_batch_dev_rx")
+
+    def mac_verify_dev(self, keys, which: int, desc, buf, status, key_idx_out=None, stream=None):
+        """HasMac::verify_mac1 (which=1, 32-byte keys) / verify_mac2 (which=2, 16-byte cookies) for a batch
+        of handshake messages; key_idx KEY_SCAN tries every key (wg-proxy)."""
+        n = _ndesc(desc)
+        key_len = 32 if which == 1 else 16
+        nkeys = _nbytes(keys) // key_len
+        check(self._L.rg_mac_verify_batch_dev(self._h, _vp(keys), key_len, nkeys, which, _vp(desc), n, _vp(buf),
+                                              _nbytes(buf), _vp(status), _vp(key_idx_out), _stream_handle(stream)),
+              "rg_mac_verify_batch_dev")
 
     def synth_fill_dev(self, desc, inner_len, buf, seed: int, stream=None):
         n = _ndesc(desc)

@@ -500,6 +500,30 @@ int rg_open_batch_dev_rx(rg_ctx *ctx, const uint8_t *keys, uint32_t nkeys, const
     return rg_open_batch_dev(ctx, keys, nkeys, rd, n, buf, buf_len, status, counters_out, stream);
 }
 
+int rg_mac_verify_batch_dev(rg_ctx *ctx, const uint8_t *keys, uint32_t key_len, uint32_t nkeys, int which,
+                            const rg_pkt_desc *desc, size_t n, const uint8_t *buf, size_t buf_len, uint8_t *status,
+                            uint32_t *key_idx_out, void *stream) {
+    int rc = check_ctx(ctx);
+    if (rc) return rc;
+    if (n == 0) return RG_OK;
+    if (!keys || nkeys == 0 || (key_len != 16 && key_len != 32) || (which != 1 && which != 2) || !desc || !buf ||
+        !status || n > 0xFFFFFFFFull)
+        return set_err(RG_EINVAL, "mac verify: bad args");
+    rg::MacArgs a{};
+    a.keys = reinterpret_cast<const uint32_t *>(keys);
+    a.key_len = key_len;
+    a.nkeys = nkeys;
+    a.which = (uint32_t)which;
+    a.n = (uint32_t)n;
+    a.desc = desc;
+    a.buf = buf;
+    a.buf_len = buf_len;
+    a.status = status;
+    a.key_out = key_idx_out;
+    RG_HIP(rg::launch_mac_verify(a, (hipStream_t)stream), "mac verify launch");
+    return RG_OK;
+}
+
 void *rg_host_alloc(size_t bytes) {
     void *p = nullptr;
     if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) return nullptr;

@@ -36,6 +36,21 @@ struct OpenArgs {
     uint32_t n;
 };
 
+// Handshake MAC checks (rg_mac.hip)
+struct MacArgs {
+    const uint32_t *keys; // [nkeys][key_len / 4] LE words
+    uint32_t key_len;     // 32 (mac1 key) or 16 (cookie, mac2)
+    uint32_t nkeys;
+    uint32_t which;       // 1 = mac1, 2 = mac2
+    uint32_t n;
+    const rg_pkt_desc *desc; // offset, len = whole message, key_idx or RG_KEY_SCAN
+    const uint8_t *buf;
+    uint64_t buf_len;
+    uint8_t *status;
+    uint32_t *key_out; // or nullptr
+};
+hipError_t launch_mac_verify(const MacArgs &a, hipStream_t s);
+
 // General AEAD job for the per-message drop-in (any nonce / AAD / length).
 struct GeneralJob {
     uint32_t key[8];

@@ -533,3 +533,65 @@ def test_receiver_lookup_check_order(engine):
     engine.open_dev_rx(_dev(keys), _dev(table), _dev(desc.view(np.uint8).reshape(-1, 16)), _dev(buf), st)
     torch.cuda.synchronize()
     assert list(st.cpu().numpy()) == [c[4] for c in cases]
+
+
+# ------------------------------------------------------ handshake MAC checks
+def _handshake_batch(rng, n, keys, key_len, which):
+    """n handshake messages (init 148 B / response 92 B, 16-byte aligned) whose mac field is valid for a
+    random key; returns desc (key_idx = the signing key), buf."""
+    sizes = rng.choice([148, 92], n)
+    off = np.concatenate([[0], np.cumsum((sizes + 15) // 16 * 16)[:-1]]).astype(np.uint64)
+    buf = rng.integers(0, 256, int(off[-1]) + 160, dtype=np.uint8)
+    desc = np.zeros(n, DESC_DTYPE)
+    desc["offset"], desc["len"] = off, sizes
+    desc["key_idx"] = rng.integers(0, len(keys), n)
+    for i in range(n):
+        o, L = int(off[i]), int(sizes[i])
+        cov = L - (32 if which == 1 else 16)
+        mac = oracle.blake2s(buf[o:o + cov].tobytes(), keys[desc["key_idx"][i]].tobytes(), 16)
+        buf[o + cov:o + cov + 16] = np.frombuffer(mac, np.uint8)
+    return desc, buf
+
+
+@pytest.mark.parametrize("which", [1, 2])
+def test_mac_verify_batch_vs_oracle(engine, which):
+    """HasMac::verify_mac1 / verify_mac2 (rustyguard-crypto/src/lib.rs:138-158) on the GPU against the
+    oracle: given keys, the wg-proxy peer scan (RG_KEY_SCAN), wrong keys and forged macs."""
+    rng = np.random.default_rng(30 + which)
+    key_len = 32 if which == 1 else 16
+    keys = rng.integers(0, 256, (24, key_len), dtype=np.uint8)
+    desc, buf = _handshake_batch(rng, 1500, keys, key_len, which)
+    pick = rng.permutation(len(desc))
+    desc["key_idx"][pick[:500]] = aead.KEY_SCAN
+    desc["key_idx"][pick[500:600]] = (desc["key_idx"][pick[500:600]] + 1) % len(keys)  # wrong peer
+    for i in pick[600:700]:  # forged mac byte
+        buf[int(desc["offset"][i]) + int(desc["len"][i]) - (32 if which == 1 else 16) + 3] ^= 0x10
+    want, wkey = oracle.mac_verify_batch(keys, which, desc, buf)
+    st = torch.zeros(len(desc), dtype=torch.uint8, device="cuda")
+    ko = torch.zeros(len(desc), dtype=torch.int32, device="cuda")
+    engine.mac_verify_dev(_dev(keys), which, _dev(desc.view(np.uint8).reshape(-1, 16)), _dev(buf), st, ko)
+    torch.cuda.synchronize()
+    st, ko = st.cpu().numpy(), ko.cpu().numpy().view(np.uint32)
+    assert list(st) == list(want) and list(ko) == list(wkey)
+    assert (st[pick[600:700]] == aead.PKT_REJECTED).all() and (st[pick[500:600]] == aead.PKT_REJECTED).all()
+    assert (st[pick[:500]] == 0).all()
+
+
+def test_mac_verify_reference_snapshot(engine):
+    """The reference's mac_snapshot (prim.rs:483-489) checked on the GPU in mac1 form: a message whose
+    bytes [len-32, len-16) are blake2s_mac(key, first len-32 bytes) verifies under the snapshot's key,
+    found by the peer scan, and is rejected under any other key."""
+    m = load_golden("blake2s.json")["reference_mac_snapshot"]
+    msg = bytes.fromhex(m["msg"]) + bytes.fromhex(m["mac"]) + bytes(16)  # the 16-byte mac2 slot follows
+    buf = np.zeros(80, np.uint8)
+    buf[:len(msg)] = np.frombuffer(msg, np.uint8)
+    key = np.frombuffer(bytes.fromhex(m["key"]), np.uint8)
+    keys = np.stack([key[::-1].copy(), key])  # row 1 is the snapshot's key
+    desc = np.zeros(2, DESC_DTYPE)
+    desc[0] = (0, len(msg), aead.KEY_SCAN)
+    desc[1] = (0, len(msg), 0)
+    st = torch.zeros(2, dtype=torch.uint8, device="cuda")
+    ko = torch.zeros(2, dtype=torch.int32, device="cuda")
+    engine.mac_verify_dev(_dev(keys), 1, _dev(desc.view(np.uint8).reshape(-1, 16)), _dev(buf), st, ko)
+    torch.cuda.synchronize()
+    assert list(st.cpu().numpy()) == [0, aead.PKT_REJECTED] and ko.cpu().numpy()[0] == 1

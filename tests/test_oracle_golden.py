@@ -134,3 +134,17 @@ def test_xchacha_known_answer_and_vectors():
         assert oracle.xaead_open(key, nonce, aad, ct, tag).hex() == v["plaintext"]
         bad = bytes([tag[0] ^ 1]) + tag[1:]
         assert oracle.xaead_open(key, nonce, aad, ct, bad) is None
+
+
+def test_blake2s_reference_snapshots_and_vectors():
+    """BLAKE2s behind HasMac (rustyguard-crypto/src/lib.rs:114-209): the oracle reproduces the
+    reference's own blake2s_mac / blake2s_hash insta snapshots (prim.rs:477-489), RFC 7693
+    Appendix B and hashlib-generated keyed MACs of handshake-message lengths."""
+    g = load_golden("blake2s.json")
+    m = g["reference_mac_snapshot"]
+    assert oracle.blake2s(bytes.fromhex(m["msg"]), bytes.fromhex(m["key"]), 16).hex() == m["mac"]
+    h = g["reference_hash_snapshot"]
+    assert oracle.blake2s(bytes.fromhex(h["msg"])).hex() == h["hash"]
+    assert oracle.blake2s(bytes.fromhex(g["rfc7693_abc"]["msg"])).hex() == g["rfc7693_abc"]["hash"]
+    for v in g["keyed_macs"]:
+        assert oracle.blake2s(bytes.fromhex(v["msg"]), bytes.fromhex(v["key"]), 16).hex() == v["mac"]
