@@ -52,6 +52,7 @@ for s in "$@"; do
     case $s in
     micro) run micro 120 tools/build/microbench ;;
     mempat) run mempat 120 tools/build/mempattern ;;
+    aux) run bench_aux 300 python tools/bench_aux.py ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     test) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
     testall) run pytest_gpu 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread ;;
