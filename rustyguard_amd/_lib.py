@@ -80,7 +80,7 @@ def lib(build_if_missing: bool = True):
     """Load librg_aead.so; raise loudly if it cannot be loaded."""
     global _lib
     if _lib is None:
-        path = _build.LIB
+        path = os.environ.get("RG_AEAD_LIB") or _build.LIB  # override: experimental builds only
         if not os.path.exists(path):
             if not build_if_missing:
                 raise RgError(f"librg_aead.so missing at {path}; run python -m rustyguard_amd.build")
