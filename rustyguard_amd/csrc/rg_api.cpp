@@ -370,13 +370,20 @@ static hipError_t launch_pipe_any(rg_ctx *ctx, const rg::SealArgs *sa, const rg:
     }
     if (!plan) return rg::launch_pipe(sa, oa, L, nullptr, st);
     rg::Launch Lp = L;
-    Lp.wg_per_cu = ctx->wg_per_cu > 0 ? std::min(ctx->wg_per_cu, std::max(1, ctx->pipe_max_wg[oa ? 1 : 0])) : 1;
+    // two waves per SIMD by default: one wave's tile prologue (descriptor -> key
+    // -> first chunks) and divergent tails overlap the other's keystream (config 3
+    // +8 % over one wave per SIMD; ChaCha alone gains nothing from a second wave)
+    const int want_wg = ctx->wg_per_cu > 0 ? ctx->wg_per_cu : 2;
+    Lp.wg_per_cu = std::min(want_wg, std::max(1, ctx->pipe_max_wg[oa ? 1 : 0]));
     hipError_t e = pb.reserve(n);
     if (e != hipSuccess) return e;
     rg::TilePlan tp{};
     tp.counts = static_cast<uint32_t *>(pb.counts.p);
     tp.lists = static_cast<uint32_t *>(pb.lists.p);
     tp.cap = pb.cap;
+    tp.sched = static_cast<uint32_t *>(pb.sched.p);
+    tp.simds = (uint32_t)std::max(1, ctx->cus) * 4u; // balance per SIMD: co-resident waves share its issue slots
+    tp.classes_out = pb.d_classes;
     e = rg::launch_plan(sa ? sa->desc : oa->desc, n, oa != nullptr, tp, st);
     if (e != hipSuccess) return e;
     rg::PipePlan pp{static_cast<uint32_t *>(pb.counts.p), static_cast<const uint32_t *>(pb.lists.p), pb.cap,

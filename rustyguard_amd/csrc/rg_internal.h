@@ -94,6 +94,8 @@ struct TilePlan {
     uint32_t target_lanes; // segment sizing: aim for this many busy lanes (0 = no splitting)
     uint32_t fixed_k;      // 0 = per class from the counts, else 1 / 2 / 4 segments for every packet
     uint32_t *classes_out; // host-mapped: number of non-empty classes of the batch (or nullptr)
+    uint32_t *sched;       // pipelined kernel: the planner also writes its schedule here (else nullptr)
+    uint32_t simds;        // SIMDs the pipelined kernel runs on (schedule balance)
 };
 
 // Planner + LDS-staged tile kernel (rg_tile.hip); exactly one of sa / oa is non-null.
@@ -103,14 +105,59 @@ hipError_t launch_tiles(const SealArgs *sa, const OpenArgs *oa, int G, const Til
 hipError_t prepare_tile_kernels();
 // Pipelined lane kernel (rg_pipe.hip): one packet per lane, double-buffered
 // chunk loads, Poly1305 absorbed inside the next chunk's keystream rounds.
-// With a plan (planner lists, rg_tile.hip): a schedule kernel picks segments per
-// size class from the batch's mean work, then one wave per SIMD walks tiles of
-// 64 lanes, largest class first, round robin (sched[] holds the schedule; the
-// schedule kernel zeroes the planner's counts).  Without one: lane units in
-// array order, grid-stride.
+// With a plan (planner lists, rg_tile.hip): the planner's last workgroup picks
+// segments per size class from the batch's mean work (schedule_classes), then
+// one wave per SIMD walks tiles of 64 lanes, largest class first, round robin
+// (sched[] holds the schedule; the planner zeroes its counts again).  Without
+// one: lane units in array order, grid-stride.
 constexpr uint32_t kSchedWords = 128;
+// sched[] words: 2 total tiles, 4 + c: first tile of class c, 44 + c: log2
+// segments of class c, 84 + c: packets of class c.
+constexpr uint32_t kSchedStart = 4, kSchedLg = 44, kSchedCnt = 84;
+static_assert(kSchedCnt + kClasses <= kSchedWords, "schedule words");
+
+// One wave (lanes 0-63), lane c owns size class c.  Segments per class: the
+// fewest (power of two) that keep a lane's slots (1 one-time-key block + its
+// chunks) within the batch's mean work per SIMD, so that no tile outlasts the
+// balanced schedule; tiles are numbered largest class first (the round robin
+// then deals long tiles before short ones).  Takes the planner's final class
+// counts over into sched[] and zeroes them for the next batch.
+__device__ __forceinline__ void schedule_classes(uint32_t *counts, uint32_t *sched, uint32_t simds,
+                                                 uint32_t *classes_out) {
+    const uint32_t c = threadIdx.x & 63;
+    const uint32_t cnt =
+        c < kClasses ? __hip_atomic_load(&counts[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+    if (c < kClasses) __hip_atomic_store(&counts[c], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t chunks = c < kClasses ? class_hi(c) : 0;
+    uint64_t work = (uint64_t)cnt * (1 + chunks); // lane slots with one lane per packet
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) work += (uint64_t)__shfl_xor((long long)work, o);
+    const uint64_t per_simd = (work + 64ull * simds - 1) / (64ull * simds);
+    const uint32_t target = (uint32_t)(per_simd < 2 ? 2 : per_simd > 0xFFFF ? 0xFFFF : per_simd);
+    uint32_t lg = 0;
+    while (lg < 6 && 1 + (chunks + (1u << lg) - 1) / (1u << lg) > target) ++lg;
+    const uint32_t tiles = (uint32_t)((((uint64_t)cnt << lg) + 63) / 64);
+    // first tile of class c = tiles of all larger classes (suffix sum)
+    uint32_t suffix = tiles;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t v = (uint32_t)__shfl_down((int)suffix, o);
+        if (c + o < 64) suffix += v;
+    }
+    if (c < kClasses) {
+        sched[kSchedStart + c] = suffix - tiles;
+        sched[kSchedLg + c] = lg;
+        sched[kSchedCnt + c] = cnt;
+    }
+    const uint64_t used = __ballot(cnt > 0);
+    if (c == 0) {
+        sched[2] = suffix; // lane 0: all tiles
+        if (classes_out) *reinterpret_cast<volatile uint32_t *>(classes_out) = (uint32_t)__popcll(used);
+    }
+}
+
 struct PipePlan {
-    uint32_t *counts;      // [kClasses] packets per class (zeroed again by the schedule kernel)
+    uint32_t *counts;      // [kClasses] packets per class (zeroed again by the planner's last workgroup)
     const uint32_t *lists; // [kClasses][cap] packet indices
     uint32_t cap;
     uint32_t *sched;       // [kSchedWords] per-batch schedule

@@ -237,14 +237,30 @@ __device__ __forceinline__ Acc combine_segments(Acc h, const Mul &r, uint32_t af
     return h;
 }
 
+#ifdef RG_TILE_MARKS
+// experiment builds only (tools/build_variant.sh): real-time marks inside a
+// seal unit, the data dependence pins each mark after the value it follows
+#define RG_MARK(slot, dep)                                                                  \
+    do {                                                                                    \
+        asm volatile("" ::"v"(dep));                                                        \
+        const uint64_t now_ = __builtin_amdgcn_s_memrealtime();                             \
+        if (a.dbg && (threadIdx.x & 63) == 0)                                               \
+            a.dbg[8ull * (blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64) + (slot)] = now_; \
+    } while (0)
+#else
+#define RG_MARK(slot, dep) \
+    do {                   \
+    } while (0)
+#endif
+
 // ------------------------------------------------------------------ seal
 // Frame: [hdr 16][payload P][tag 16]; desc.len = P.  Checks as seal_packet
 // (rg_kernels.hip): descriptor and force_encrypt's padding assert
 // (rustyguard-core/src/lib.rs:273-277).  Lane j of a G-lane group runs
 // segment j; lane 0 writes header, tag and status.
 template <int MODE>
-__device__ __forceinline__ void pipe_seal_packet(const SealArgs &a, uint32_t i, uint32_t j, uint32_t G) {
-    const rg_pkt_desc d = a.desc[i];
+__device__ __forceinline__ void pipe_seal_packet(const SealArgs &a, uint32_t i, const rg_pkt_desc &d, uint32_t j,
+                                                 uint32_t G) {
     const uint32_t P = d.len;
     const bool valid = d.key_idx < a.nkeys && (P & 15u) == 0 && (d.offset & 15u) == 0 && P <= kMaxPayload &&
                        d.offset <= a.buf_len && P + 32 <= a.buf_len - d.offset;
@@ -253,6 +269,7 @@ __device__ __forceinline__ void pipe_seal_packet(const SealArgs &a, uint32_t i, 
         return;
     }
     uint8_t *frame = a.buf + d.offset;
+    RG_MARK(1, P);
     const uint32_t nb = P >> 4;
     const Seg sg = make_seg(nb, j, G);
     // an empty segment reads (never writes) the payload start, which is in the frame
@@ -273,12 +290,15 @@ __device__ __forceinline__ void pipe_seal_packet(const SealArgs &a, uint32_t i, 
     uint32_t ks[16];
     stream_block(stm, 0, ks); // RFC 8439 §2.6 one-time key
     const Mul r = make_mul(ks[0], ks[1], ks[2], ks[3]);
+    RG_MARK(2, r.rr3);
     // DataHeader {4, receiver, counter} (rustyguard-core/src/lib.rs:286-290), stored by segment 0
     // together with the first payload blocks
     const bool head = a.receivers != nullptr && j == 0;
     const uint4 hdr = make_uint4(4u, head ? a.receivers[d.key_idx] : 0u, n1, n2);
     Acc h = pipe_pass<false, MODE>(pl, stm, r, sg.nb, sg.c0, b0, b1, hdr, head);
+    RG_MARK(3, h.h4);
     h = combine_segments(h, r, sg.after, G);
+    RG_MARK(5, h.h4);
     if (j != 0) return;
     uint32_t tag[4];
     pipe_tag(h, r, P, ks + 4, tag);
@@ -292,8 +312,8 @@ __device__ __forceinline__ void pipe_seal_packet(const SealArgs &a, uint32_t i, 
 // 427-429.  Decrypts speculatively while MACing the ciphertext; a failed tag
 // (constant-time compare, identical on every lane of the group) makes each
 // lane re-apply its segment's keystream, so the frame is left unchanged.
-__device__ __forceinline__ void pipe_open_packet(const OpenArgs &a, uint32_t i, uint32_t j, uint32_t G) {
-    const rg_pkt_desc d = a.desc[i];
+__device__ __forceinline__ void pipe_open_packet(const OpenArgs &a, uint32_t i, const rg_pkt_desc &d, uint32_t j,
+                                                 uint32_t G) {
     const uint32_t W = d.len;
     uint32_t st;
     if (d.key_idx == RG_KEY_SKIP) st = RG_PKT_REJECTED;
@@ -358,64 +378,24 @@ __device__ __forceinline__ void pipe_open_packet(const OpenArgs &a, uint32_t i, 
 // Persistent grid as seal_kernel<1> (rg_kernels.hip): the host launches at most
 // CUs x wg_per_cu workgroups with an LDS reservation that fixes residency.
 // With a diagnostics buffer (debug mode 3) lane 0 of every wave records
-// [s_memtime delta, 0, 0, 0, start s_memrealtime, 4, 1, s_memrealtime delta]
-// (tools/stamps.py; s_memrealtime ticks at 100 MHz).
-__device__ __forceinline__ void pipe_stamp(uint64_t *dbg, uint64_t t0, uint64_t r0) {
+// [s_memtime delta, real-time ticks to the end of the wave's first and second
+// unit, 0, start s_memrealtime, 4, 1, s_memrealtime delta] (tools/stamps.py;
+// s_memrealtime ticks at 100 MHz).
+__device__ __forceinline__ void pipe_stamp(uint64_t *dbg, uint64_t t0, uint64_t r0, const uint64_t marks[2]) {
     const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
     if ((threadIdx.x & 63) == 0) {
         uint64_t *o = dbg + 8ull * (blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64);
-        o[0] = t1 - t0; o[1] = 0; o[2] = 0; o[3] = 0;
-        o[4] = r0; o[5] = 4; o[6] = 1; o[7] = r1 - r0;
+#ifndef RG_TILE_MARKS
+        o[0] = t1 - t0; o[1] = marks[0] ? marks[0] - r0 : 0; o[2] = marks[1] ? marks[1] - r0 : 0; o[3] = 0;
+        o[5] = 4;
+#else
+        o[0] = marks[0];
+#endif
+        o[4] = r0; o[6] = 1; o[7] = r1 - r0;
     }
 }
 
-// ------------------------------------------------------------- schedule
-// sched[] words: 2 total tiles, 4 + c: first tile of class c, 44 + c: log2
-// segments of class c, 84 + c: packets of class c.
-constexpr uint32_t kSchedStart = 4, kSchedLg = 44, kSchedCnt = 84;
-static_assert(kSchedCnt + kClasses <= kSchedWords, "schedule words");
-
-// One wave: lane c owns size class c.  Segments per class: the fewest (power
-// of two) that keep a lane's slots (1 one-time-key block + its chunks) within
-// the batch's mean work per SIMD, so that no tile outlasts the balanced
-// schedule; tiles are numbered largest class first (the round robin then
-// deals long tiles before short ones).
-// It also takes the planner's class counts over into sched[] and zeroes them
-// for the next batch (no atomics in the transport kernel).
-__global__ __launch_bounds__(64) void pipe_schedule_kernel(uint32_t *counts, uint32_t *sched, uint32_t simds,
-                                                           uint32_t *classes_out) {
-    const uint32_t c = threadIdx.x;
-    const uint32_t cnt = c < kClasses ? counts[c] : 0;
-    if (c < kClasses) counts[c] = 0;
-    const uint32_t chunks = c < kClasses ? class_hi(c) : 0;
-    uint64_t work = (uint64_t)cnt * (1 + chunks); // lane slots with one lane per packet
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) work += (uint64_t)__shfl_xor((long long)work, o);
-    const uint64_t per_simd = (work + 64ull * simds - 1) / (64ull * simds);
-    const uint32_t target = (uint32_t)(per_simd < 2 ? 2 : per_simd > 0xFFFF ? 0xFFFF : per_simd);
-    uint32_t lg = 0;
-    while (lg < 6 && 1 + (chunks + (1u << lg) - 1) / (1u << lg) > target) ++lg;
-    const uint32_t tiles = (uint32_t)((((uint64_t)cnt << lg) + 63) / 64);
-    // first tile of class c = tiles of all larger classes (suffix sum)
-    uint32_t suffix = tiles;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t v = (uint32_t)__shfl_down((int)suffix, o);
-        if (c + o < 64) suffix += v;
-    }
-    if (c < kClasses) {
-        sched[kSchedStart + c] = suffix - tiles;
-        sched[kSchedLg + c] = lg;
-        sched[kSchedCnt + c] = cnt;
-    }
-    const uint64_t used = __ballot(cnt > 0);
-    if (c == 0) {
-        sched[2] = suffix; // lane 0: all tiles
-        if (classes_out) *reinterpret_cast<volatile uint32_t *>(classes_out) = (uint32_t)__popcll(used);
-    }
-}
-
-// ------------------------------------------------------------- kernels
+// ---------------------------------------------------------------- walk
 // Identity order: lane units u = G * packet + segment, grid-stride (the stride
 // is a multiple of 256, so a packet's G lanes stay together in one wave);
 // lg = log2(G).
@@ -426,8 +406,9 @@ __global__ __launch_bounds__(64) void pipe_schedule_kernel(uint32_t *counts, uin
 // Both orders share one loop, so the packet body has a single call site (two
 // would make the compiler emit it as a real function call: stack frame, kernel
 // arguments in scratch, ~250 VGPRs).
-template <typename Body>
-__device__ __forceinline__ void pipe_walk(uint32_t n, uint32_t lg0, const PipePlan &pp, Body &&body) {
+template <class Body>
+__device__ __forceinline__ void pipe_walk(uint32_t n, uint32_t lg0, const PipePlan &pp, const rg_pkt_desc *desc,
+                                          bool stamp, uint64_t marks[2], Body &&body) {
     const uint32_t lane = threadIdx.x & 63;
     const bool planned = pp.counts != nullptr;
     uint32_t my_cnt = 0, my_start = 0, my_lg = 0, my_tiles = 0;
@@ -447,37 +428,80 @@ __device__ __forceinline__ void pipe_walk(uint32_t n, uint32_t lg0, const PipePl
         first = blockIdx.x * 256 + threadIdx.x;
         stride = (uint64_t)gridDim.x * 256;
     }
-    for (uint64_t it = first; it < total; it += stride) {
-        uint32_t i, lg, u;
-        bool live = true;
+    // unit `it` -> packet slot; the packet index itself comes from the plan's
+    // list (a load) or is the unit's high bits
+    struct Unit {
+        uint32_t i, j, lg;
+        bool live;
+    };
+    auto locate = [&](uint64_t it, uint32_t &list_pos) -> Unit {
+        Unit o;
+        list_pos = 0;
         if (planned) {
             const uint32_t tile = (uint32_t)it;
             const uint64_t hit = __ballot(lane < kClasses && my_start <= tile && tile < my_start + my_tiles);
             const uint32_t c = uniform_u32((uint32_t)(__ffsll((unsigned long long)hit) - 1));
-            lg = uniform_u32((uint32_t)__shfl((int)my_lg, (int)c));
-            u = (tile - uniform_u32((uint32_t)__shfl((int)my_start, (int)c))) * 64 + lane;
-            const uint32_t p = u >> lg;
-            live = p < uniform_u32((uint32_t)__shfl((int)my_cnt, (int)c));
-            i = live ? pp.lists[(uint64_t)c * pp.cap + p] : 0;
+            o.lg = uniform_u32((uint32_t)__shfl((int)my_lg, (int)c));
+            const uint32_t u = (tile - uniform_u32((uint32_t)__shfl((int)my_start, (int)c))) * 64 + lane;
+            const uint32_t p = u >> o.lg;
+            o.live = it < total && p < uniform_u32((uint32_t)__shfl((int)my_cnt, (int)c));
+            o.j = u & ((1u << o.lg) - 1);
+            list_pos = o.live ? c * pp.cap + p : 0;
+            o.i = 0;
         } else {
-            lg = lg0;
-            u = (uint32_t)it;
-            i = (uint32_t)(it >> lg0);
+            o.lg = lg0;
+            o.live = it < total;
+            o.j = (uint32_t)it & ((1u << lg0) - 1);
+            o.i = o.live ? (uint32_t)(it >> lg0) : 0;
         }
-        if (live) body(i, u & ((1u << lg) - 1), 1u << lg);
+        return o;
+    };
+    // Software pipeline over a wave's units, two deep: while unit k runs, the
+    // descriptor of unit k+1 and the list entry of unit k+2 are in flight, so
+    // a tile starts with its descriptor in registers (the key, counter and
+    // first chunks are then one round trip away, not three).  Loads are
+    // unconditional (index 0 when past the end) to keep the waits exact.
+    if (first >= total) return;
+    uint32_t q0, q1;
+    Unit cur = locate(first, q0), nxt = locate(first + stride, q1);
+    if (planned) {
+        cur.i = pp.lists[q0];
+        nxt.i = pp.lists[q1];
+    }
+    rg_pkt_desc dcur = desc[cur.live ? cur.i : 0];
+    for (uint64_t it = first; it < total; it += stride) {
+        uint32_t q2;
+        Unit far = locate(it + 2 * stride, q2);
+        if (planned) far.i = pp.lists[q2];
+        const rg_pkt_desc dnxt = desc[nxt.live ? nxt.i : 0];
+        if (cur.live) body(cur.i, dcur, cur.j, 1u << cur.lg);
+        if (stamp) { // diagnostics: real-time ticks at the end of a wave's first two units
+            const uint64_t now = __builtin_amdgcn_s_memrealtime();
+            if (it == first) marks[0] = now;
+            else if (it == first + stride) marks[1] = now;
+        }
+        cur = nxt;
+        nxt = far;
+        dcur = dnxt;
     }
 }
 
 template <int MODE> __global__ __launch_bounds__(256) void pipe_seal_kernel(SealArgs a, uint32_t lg, PipePlan pp) {
     const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
-    pipe_walk(a.n, lg, pp, [=](uint32_t i, uint32_t j, uint32_t G) { pipe_seal_packet<MODE>(a, i, j, G); });
-    if (a.dbg) pipe_stamp(a.dbg, t0, r0);
+    uint64_t marks[2] = {0, 0};
+    pipe_walk(a.n, lg, pp, a.desc, a.dbg != nullptr, marks, [=](uint32_t i, const rg_pkt_desc &d, uint32_t j, uint32_t G) {
+        pipe_seal_packet<MODE>(a, i, d, j, G);
+    });
+    if (a.dbg) pipe_stamp(a.dbg, t0, r0, marks);
 }
 
 __global__ __launch_bounds__(256) void pipe_open_kernel(OpenArgs a, uint32_t lg, PipePlan pp) {
     const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
-    pipe_walk(a.n, lg, pp, [=](uint32_t i, uint32_t j, uint32_t G) { pipe_open_packet(a, i, j, G); });
-    if (a.dbg) pipe_stamp(a.dbg, t0, r0);
+    uint64_t marks[2] = {0, 0};
+    pipe_walk(a.n, lg, pp, a.desc, a.dbg != nullptr, marks, [=](uint32_t i, const rg_pkt_desc &d, uint32_t j, uint32_t G) {
+        pipe_open_packet(a, i, d, j, G);
+    });
+    if (a.dbg) pipe_stamp(a.dbg, t0, r0, marks);
 }
 
 static void pipe_grid(uint64_t units, const Launch &L, uint32_t &blocks, uint32_t &lds) {
@@ -499,10 +523,7 @@ hipError_t launch_pipe(const SealArgs *sa, const OpenArgs *oa, const Launch &L, 
         pp = *plan;
         const uint32_t wg = (uint32_t)(L.wg_per_cu > 0 ? L.wg_per_cu : 1);
         blocks = (uint32_t)(L.cus > 0 ? L.cus : 1) * wg;
-        lds = (kLdsPerCu / wg) & ~255u;
-        // balance per SIMD: co-resident waves share one SIMD's issue slots
-        hipLaunchKernelGGL(pipe_schedule_kernel, dim3(1), dim3(64), 0, s, pp.counts, pp.sched, blocks / wg * 4,
-                           pp.classes_out);
+        lds = (kLdsPerCu / wg) & ~255u; // sched[] was written by the planner (plan_kernel)
     } else {
         pipe_grid((uint64_t)n << lg, L, blocks, lds);
     }

@@ -49,9 +49,11 @@ __device__ __forceinline__ uint32_t class_of(uint32_t chunks) {
 constexpr uint32_t kPlanPer = 2;
 
 __global__ __launch_bounds__(256) void plan_kernel(const rg_pkt_desc *desc, uint32_t n, uint32_t open,
-                                                   uint32_t *counts, uint32_t *lists, uint32_t cap) {
+                                                   uint32_t *counts, uint32_t *lists, uint32_t cap, uint32_t *sched,
+                                                   uint32_t simds, uint32_t *classes_out) {
     __shared__ uint32_t hist[kClasses];
     __shared__ uint32_t gbase[kClasses];
+    __shared__ uint32_t last;
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     if (tid < kClasses) hist[tid] = 0;
     __syncthreads();
@@ -91,6 +93,21 @@ __global__ __launch_bounds__(256) void plan_kernel(const rg_pkt_desc *desc, uint
 #pragma unroll
     for (uint32_t k = 0; k < kPlanPer; ++k) {
         if (cls[k] != ~0u) lists[(uint64_t)cls[k] * cap + gbase[cls[k]] + rank[k]] = first + k * 256 + tid;
+    }
+    if (!sched) return; // tile kernels: every workgroup derives its schedule from the counts
+    // pipelined kernel: the last planner workgroup turns the final counts into
+    // its schedule (one launch fewer per batch than a separate schedule kernel)
+    // No fences: this workgroup's count atomics have returned (gbase) before
+    // the barrier, so they are performed at device scope before its finish
+    // increment, and schedule_classes reads the counts with device-scope
+    // atomic loads.  The lists reach the transport kernel at the kernel
+    // boundary.
+    __syncthreads();
+    if (tid == 0) last = atomicAdd(&counts[kClasses], 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (last && tid < 64) {
+        schedule_classes(counts, sched, simds, classes_out);
+        if (tid == 0) __hip_atomic_store(&counts[kClasses], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -704,9 +721,11 @@ static_assert(StagedCfg<2>::WG_LDS <= kLdsPerCu, "8 waves of G = 2 windows must 
 hipError_t launch_plan(const rg_pkt_desc *desc, uint32_t n, bool open, const TilePlan &tp, hipStream_t s) {
     if (n == 0) return hipSuccess;
     // counters start at zero: cleared at allocation and by the last workgroup
-    // of every tile kernel that consumed them
+    // of every tile kernel (or of the planner, for the pipelined kernel) that
+    // consumed them
     hipLaunchKernelGGL(plan_kernel, dim3((n + 256 * kPlanPer - 1) / (256 * kPlanPer)), dim3(256), 0, s, desc, n, open ? 1u : 0u,
-                       const_cast<uint32_t *>(tp.counts), const_cast<uint32_t *>(tp.lists), tp.cap);
+                       const_cast<uint32_t *>(tp.counts), const_cast<uint32_t *>(tp.lists), tp.cap, tp.sched, tp.simds,
+                       tp.sched ? tp.classes_out : nullptr);
     return hipGetLastError();
 }
 
