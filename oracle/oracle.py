@@ -47,7 +47,7 @@ def lib():
         L.rg_oracle_hchacha20.argtypes = [u8p, u8p, u8p]
         L.rg_oracle_blake2s.argtypes = [u8p, ctypes.c_size_t, u8p, ctypes.c_size_t, u8p, ctypes.c_size_t]
         L.rg_oracle_mac_verify_batch.argtypes = [u8p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int, u8p,
-                                                 ctypes.c_size_t, u8p, u8p, u8p]
+                                                 ctypes.c_size_t, u8p, ctypes.c_size_t, u8p, u8p]
         L.rg_oracle_xaead_seal.argtypes = [u8p, u8p, u8p, ctypes.c_size_t, u8p, ctypes.c_size_t, u8p]
         L.rg_oracle_xaead_open.argtypes = [u8p, u8p, u8p, ctypes.c_size_t, u8p, ctypes.c_size_t, u8p]
         L.rg_oracle_xaead_open.restype = ctypes.c_int
@@ -132,7 +132,7 @@ def mac_verify_batch(keys: np.ndarray, which: int, desc: np.ndarray, buf: np.nda
     status = np.zeros(max(n, 1), np.uint8)
     kout = np.zeros(max(n, 1), np.uint32)
     lib().rg_oracle_mac_verify_batch(_ptr(keys), keys.shape[1], keys.shape[0], which, _ptr(desc), n, _ptr(buf),
-                                     _ptr(status), _ptr(kout))
+                                     len(buf), _ptr(status), _ptr(kout))
     return status[:n], kout[:n]
 
 

@@ -408,13 +408,16 @@ void rg_oracle_blake2s(uint8_t *out, size_t outlen, const uint8_t *key, size_t k
  * every key in order and keeps the first match, as wg-proxy's peer scan
  * (wg-proxy/src/main.rs:217-229). */
 void rg_oracle_mac_verify_batch(const uint8_t *keys, size_t key_len, size_t nkeys, int which,
-                                const rg_oracle_desc *desc, size_t n, const uint8_t *buf, uint8_t *status,
-                                uint32_t *key_out) {
+                                const rg_oracle_desc *desc, size_t n, const uint8_t *buf, size_t buf_len,
+                                uint8_t *status, uint32_t *key_out) {
     for (size_t i = 0; i < n; i++) {
         const rg_oracle_desc *d = &desc[i];
         key_out[i] = 0xFFFFFFFFu;
         if ((d->offset & 15) != 0) { status[i] = RG_ORACLE_UNALIGNED; continue; }
-        if (d->len < 32) { status[i] = RG_ORACLE_INVALID; continue; }
+        if (d->len < 32 || d->offset > buf_len || d->len > buf_len - d->offset) {
+            status[i] = RG_ORACLE_INVALID; /* framing: the message must lie in the buffer */
+            continue;
+        }
         const size_t covered = d->len - (which == 2 ? 16 : 32);
         const uint8_t *msg = buf + d->offset;
         size_t lo = d->key_idx, hi = d->key_idx + 1;

@@ -52,8 +52,8 @@ int rg_oracle_xaead_open(const uint8_t key[32], const uint8_t nonce24[24], const
 void rg_oracle_blake2s(uint8_t *out, size_t outlen, const uint8_t *key, size_t keylen, const uint8_t *msg,
                        size_t len);
 void rg_oracle_mac_verify_batch(const uint8_t *keys, size_t key_len, size_t nkeys, int which,
-                                const rg_oracle_desc *desc, size_t n, const uint8_t *buf, uint8_t *status,
-                                uint32_t *key_out);
+                                const rg_oracle_desc *desc, size_t n, const uint8_t *buf, size_t buf_len,
+                                uint8_t *status, uint32_t *key_out);
 void rg_oracle_open_batch(const uint8_t *keys, const rg_oracle_desc *desc, size_t n, uint8_t *buf,
                           uint8_t *status, uint64_t *counters_out, int nthreads);
 /* open with the receiver -> session lookup of Sessions::decrypt_packet

@@ -163,6 +163,7 @@ struct rg_ctx {
     DevBuf d_keys, d_recv;
     DevBuf d_general;  // per-message drop-in arena
     DevBuf d_rx_desc;  // rg_open_batch_dev_rx: resolved descriptors
+    DevBuf d_mac_keys; // rg_mac_verify_batch_dev: per-key BLAKE2s states
     DevBuf d_jobs;
 };
 
@@ -230,6 +231,7 @@ void rg_destroy(rg_ctx *ctx) {
     ctx->d_recv.release();
     ctx->d_general.release();
     ctx->d_rx_desc.release();
+    ctx->d_mac_keys.release();
     ctx->d_jobs.release();
     delete ctx;
 }
@@ -527,6 +529,8 @@ int rg_mac_verify_batch_dev(rg_ctx *ctx, const uint8_t *keys, uint32_t key_len, 
     a.buf_len = buf_len;
     a.status = status;
     a.key_out = key_idx_out;
+    RG_HIP(ctx->d_mac_keys.reserve((size_t)nkeys * 32), "mac key states");
+    a.key_state = static_cast<uint32_t *>(ctx->d_mac_keys.p);
     RG_HIP(rg::launch_mac_verify(a, (hipStream_t)stream), "mac verify launch");
     return RG_OK;
 }

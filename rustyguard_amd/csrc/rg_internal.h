@@ -48,6 +48,7 @@ struct MacArgs {
     uint64_t buf_len;
     uint8_t *status;
     uint32_t *key_out; // or nullptr
+    uint32_t *key_state; // [nkeys][8] scratch: BLAKE2s state after each key block
 };
 hipError_t launch_mac_verify(const MacArgs &a, hipStream_t s);
 

@@ -6,6 +6,11 @@
 // RG_KEY_SCAN every key is tried in order and the first match is kept, as in
 // wg-proxy's peer scan (wg-proxy/src/main.rs:217-229).
 //
+// The keyed hash starts with the zero-padded key as its own block, so the
+// state after it depends on the key alone: mac_key_state_kernel computes it
+// once per key (one compression of three per 148-byte initiation saved), and
+// messages are read as 16-byte vectors.
+//
 // BLAKE2s (RFC 7693) is 32-bit ARX like ChaCha20 -- 10 rounds of 8 G mixes
 // over a 16-word state, rotations right by 16/12/8/7 -- so it runs on the
 // same VALU idioms (byte rotations as v_perm_b32); the message schedule sigma
@@ -57,40 +62,72 @@ __device__ __forceinline__ void b2s_compress(uint32_t h[8], const uint32_t m[16]
 }
 #undef B2S_G
 
-// little-endian word w of msg, zero past len (byte loads: mac offsets of the
-// handshake messages are 4-aligned, but the API accepts any length)
+// little-endian word at msg + byte, zero past len (byte loads: only for
+// lengths or mac offsets that are not multiples of 4, which no handshake
+// message has)
 __device__ __forceinline__ uint32_t msg_word(const uint8_t *msg, uint32_t len, uint32_t byte) {
-    if (byte + 4 <= len) {
-        return (uint32_t)msg[byte] | ((uint32_t)msg[byte + 1] << 8) | ((uint32_t)msg[byte + 2] << 16) |
-               ((uint32_t)msg[byte + 3] << 24);
-    }
     uint32_t w = 0;
     for (uint32_t b = 0; b < 4; ++b)
         if (byte + b < len) w |= (uint32_t)msg[byte + b] << (8 * b);
     return w;
 }
 
-// keyed BLAKE2s with a 16-byte digest: the key as a first zero-padded block
-// (RFC 7693 §3.3), then msg[0, len); returns the digest's 4 words
-__device__ __forceinline__ uint4 b2s_mac16(const uint32_t *key, uint32_t key_len, const uint8_t *msg, uint32_t len) {
-    uint32_t h[8];
+// the 16-byte piece p of a 16-byte aligned message, words past len zeroed
+// (a partial last word keeps its low len % 4 bytes).  Only pieces starting
+// below len are read; they end inside the frame, since the mac field follows.
+__device__ __forceinline__ void msg_piece(const uint8_t *msg, uint32_t len, uint32_t p, uint32_t m[4]) {
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (16 * p < len) v = *reinterpret_cast<const uint4 *>(msg + 16 * p);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t byte = 16 * p + 4 * i;
+        const uint32_t have = byte >= len ? 0u : min(len - byte, 4u);
+        m[i] = have == 4 ? w[i] : w[i] & ((1u << (8 * have)) - 1u);
+    }
+}
+
+// h after the key block (RFC 7693 §3.3: the zero-padded key is block 1 and,
+// for a non-empty message, never the last block), so it depends on the key
+// alone and is computed once per key by mac_key_state_kernel
+__device__ __forceinline__ void b2s_key_state(const uint32_t *key, uint32_t key_len, bool last, uint32_t h[8]) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) h[i] = kIV[i];
     h[0] ^= 0x01010000u ^ (key_len << 8) ^ 16u;
     uint32_t m[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) m[i] = (uint32_t)(4 * i) < key_len ? key[i] : 0u;
-    b2s_compress(h, m, 64, len == 0);
+    b2s_compress(h, m, 64, last);
+}
+
+// keyed BLAKE2s with a 16-byte digest of msg[0, len), len > 0, from the key
+// state; returns the digest's first 4 words
+__device__ __forceinline__ uint4 b2s_mac16(const uint32_t ks[8], const uint8_t *msg, uint32_t len) {
+    uint32_t h[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) h[i] = ks[i];
     uint32_t t = 64;
     for (uint32_t off = 0; off < len; off += 64) {
         const uint32_t rem = len - off;
         const bool last = rem <= 64;
+        uint32_t m[16];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) m[i] = msg_word(msg + off, rem, 4 * i);
+        for (int p = 0; p < 4; ++p) msg_piece(msg + off, rem, p, m + 4 * p);
         t += last ? rem : 64;
         b2s_compress(h, m, t, last);
     }
     return make_uint4(h[0], h[1], h[2], h[3]);
+}
+
+__global__ __launch_bounds__(64) void mac_key_state_kernel(const uint32_t *keys, uint32_t key_len, uint32_t nkeys,
+                                                          uint32_t *state) {
+    const uint32_t k = blockIdx.x * 64 + threadIdx.x;
+    if (k >= nkeys) return;
+    uint32_t h[8];
+    b2s_key_state(keys + (key_len / 4) * k, key_len, false, h);
+    uint4 *o = reinterpret_cast<uint4 *>(state + 8 * k);
+    o[0] = make_uint4(h[0], h[1], h[2], h[3]);
+    o[1] = make_uint4(h[4], h[5], h[6], h[7]);
 }
 
 __global__ __launch_bounds__(256) void mac_verify_kernel(MacArgs a) {
@@ -104,12 +141,27 @@ __global__ __launch_bounds__(256) void mac_verify_kernel(MacArgs a) {
     else {
         const uint8_t *msg = a.buf + d.offset;
         const uint32_t covered = d.len - (a.which == 2 ? 16u : 32u);
-        const uint4 want = make_uint4(msg_word(msg, d.len, covered), msg_word(msg, d.len, covered + 4),
-                                      msg_word(msg, d.len, covered + 8), msg_word(msg, d.len, covered + 12));
+        uint4 want;
+        if ((covered & 3u) == 0) {
+            const uint32_t *w = reinterpret_cast<const uint32_t *>(msg + covered);
+            want = make_uint4(w[0], w[1], w[2], w[3]);
+        } else {
+            want = make_uint4(msg_word(msg, d.len, covered), msg_word(msg, d.len, covered + 4),
+                              msg_word(msg, d.len, covered + 8), msg_word(msg, d.len, covered + 12));
+        }
         const bool scan = d.key_idx == RG_KEY_SCAN;
         const uint32_t lo = scan ? 0u : d.key_idx, hi = scan ? a.nkeys : min(d.key_idx + 1, a.nkeys);
         for (uint32_t k = lo; k < hi; ++k) {
-            const uint4 mac = b2s_mac16(a.keys + (a.key_len / 4) * k, a.key_len, msg, covered);
+            uint32_t ks[8];
+            if (covered > 0) {
+                const uint4 *s = reinterpret_cast<const uint4 *>(a.key_state + 8 * k);
+                const uint4 s0 = s[0], s1 = s[1];
+                ks[0] = s0.x; ks[1] = s0.y; ks[2] = s0.z; ks[3] = s0.w;
+                ks[4] = s1.x; ks[5] = s1.y; ks[6] = s1.z; ks[7] = s1.w;
+            } else { // empty covered part: the key block is the last block
+                b2s_key_state(a.keys + (a.key_len / 4) * k, a.key_len, true, ks);
+            }
+            const uint4 mac = covered > 0 ? b2s_mac16(ks, msg, covered) : make_uint4(ks[0], ks[1], ks[2], ks[3]);
             const uint32_t diff = (mac.x ^ want.x) | (mac.y ^ want.y) | (mac.z ^ want.z) | (mac.w ^ want.w);
             if (diff == 0 && found == RG_KEY_SKIP) found = k; // first match, every key still hashed
         }
@@ -123,6 +175,8 @@ __global__ __launch_bounds__(256) void mac_verify_kernel(MacArgs a) {
 
 hipError_t launch_mac_verify(const MacArgs &a, hipStream_t s) {
     if (a.n == 0) return hipSuccess;
+    hipLaunchKernelGGL(mac_key_state_kernel, dim3((a.nkeys + 63) / 64), dim3(64), 0, s, a.keys, a.key_len, a.nkeys,
+                       a.key_state);
     hipLaunchKernelGGL(mac_verify_kernel, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
     return hipGetLastError();
 }

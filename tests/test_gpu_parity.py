@@ -577,6 +577,41 @@ def test_mac_verify_batch_vs_oracle(engine, which):
     assert (st[pick[:500]] == 0).all()
 
 
+@pytest.mark.parametrize("which", [1, 2])
+def test_mac_verify_any_length(engine, which):
+    """The batch MAC check at every message length 32..300 (covered part empty, not a multiple of 4, on
+    and across 64-byte block edges) plus the descriptor checks (short, unaligned, out of range), against
+    the oracle."""
+    rng = np.random.default_rng(40 + which)
+    key_len = 32 if which == 1 else 16
+    tail = 32 if which == 1 else 16
+    keys = rng.integers(0, 256, (5, key_len), dtype=np.uint8)
+    sizes = np.arange(32, 301)
+    off = np.concatenate([[0], np.cumsum((sizes + 15) // 16 * 16)[:-1]]).astype(np.uint64)
+    buf = rng.integers(0, 256, int(off[-1]) + 320, dtype=np.uint8)
+    desc = np.zeros(len(sizes) + 4, DESC_DTYPE)
+    desc["offset"][: len(sizes)], desc["len"][: len(sizes)] = off, sizes
+    desc["key_idx"][: len(sizes)] = rng.integers(0, len(keys), len(sizes))
+    for i, L in enumerate(sizes):
+        o, cov = int(off[i]), int(L) - tail
+        if i % 3 == 2:
+            continue  # left unsigned: rejected
+        mac = oracle.blake2s(buf[o:o + cov].tobytes(), keys[desc["key_idx"][i]].tobytes(), 16)
+        buf[o + cov:o + cov + 16] = np.frombuffer(mac, np.uint8)
+    desc["key_idx"][: len(sizes)][rng.random(len(sizes)) < 0.3] = aead.KEY_SCAN
+    end = len(buf)
+    desc[len(sizes):] = [(0, 31, 0), (8, 148, 0), (end - 64, 148, 0), (0, 148, len(keys) + 3)]
+    want, wkey = oracle.mac_verify_batch(keys, which, desc, buf)
+    st = torch.zeros(len(desc), dtype=torch.uint8, device="cuda")
+    ko = torch.zeros(len(desc), dtype=torch.int32, device="cuda")
+    engine.mac_verify_dev(_dev(keys), which, _dev(desc.view(np.uint8).reshape(-1, 16)), _dev(buf), st, ko)
+    torch.cuda.synchronize()
+    st, ko = st.cpu().numpy(), ko.cpu().numpy().view(np.uint32)
+    assert list(st) == list(want) and list(ko) == list(wkey)
+    assert (st[: len(sizes)][np.arange(len(sizes)) % 3 != 2] == 0).all()
+    assert list(st[len(sizes):]) == [aead.PKT_INVALID, aead.PKT_UNALIGNED, aead.PKT_INVALID, aead.PKT_REJECTED]
+
+
 def test_mac_verify_reference_snapshot(engine):
     """The reference's mac_snapshot (prim.rs:483-489) checked on the GPU in mac1 form: a message whose
     bytes [len-32, len-16) are blake2s_mac(key, first len-32 bytes) verifies under the snapshot's key,

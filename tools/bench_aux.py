@@ -69,10 +69,18 @@ def main():
         else:
             eng.open_dev(b.keys, b.desc_open, b.buf, b.status)
 
-    ms_open, ms_rx = timed(lambda: seal_open(False), 10), timed(lambda: seal_open(True), 10)
+    # alternating repetitions, medians: box-to-box and run-to-run noise on a 2 ms
+    # step is larger than the ~50 us being measured
+    t_open, t_rx = [], []
+    for _ in range(7):
+        t_open.append(timed(lambda: seal_open(False), 10))
+        t_rx.append(timed(lambda: seal_open(True), 10))
     assert (b.status[: w.n] == 0).all().item()
+    ms_open, ms_rx = float(np.median(t_open)), float(np.median(t_rx))
     out["rx"] = {"workload": "cfg4 (1 Mi packets, 256 sessions)", "seal_open_ms": round(ms_open, 4),
-                 "seal_open_rx_ms": round(ms_rx, 4), "resolve_overhead_us": round((ms_rx - ms_open) * 1e3, 2)}
+                 "seal_open_rx_ms": round(ms_rx, 4), "resolve_overhead_us": round((ms_rx - ms_open) * 1e3, 2),
+                 "note": "medians of 7 alternating repetitions of 10 steps; the rx_resolve kernel itself is in the "
+                         "rocprofv3 kernel stats"}
     print(json.dumps(out))
 
 

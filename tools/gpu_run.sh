@@ -53,6 +53,8 @@ for s in "$@"; do
     micro) run micro 120 tools/build/microbench ;;
     mempat) run mempat 120 tools/build/mempattern ;;
     aux) run bench_aux 300 python tools/bench_aux.py ;;
+    prof_aux) run prof_aux 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_aux -o run -- \
+        python3 tools/bench_aux.py ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     test) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
     testall) run pytest_gpu 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread ;;
