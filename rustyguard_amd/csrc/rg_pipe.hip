@@ -30,6 +30,14 @@ struct Chunk {
     uint4 q0, q1, q2, q3;
 };
 
+// Chunks in flight per lane: while chunk t is processed, chunks t+1 .. t+kDepth-1
+// are loaded or loading (the load of chunk t + kDepth is issued at its end).
+#ifndef RG_PIPE_DEPTH
+#define RG_PIPE_DEPTH 3
+#endif
+constexpr int kDepth = RG_PIPE_DEPTH;
+static_assert(kDepth == 2 || kDepth == 3, "pipeline depth");
+
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 template <int NT> __device__ __forceinline__ uint4 ld16(const uint4 *p) {
     if constexpr (NT & 1) {
@@ -127,19 +135,19 @@ __device__ __forceinline__ void pipe_step(uint4 *pl, const Stream &st, const Mul
         have_prev = true;
     }
     pi = OPEN ? buf : x;
-    if constexpr (!TAIL) load_chunk<NT>(buf, pl, t + 2, nb - 1);
+    if constexpr (!TAIL) load_chunk<NT>(buf, pl, t + kDepth, nb - 1);
 }
 
 // Keystream XOR in place + Poly1305 over the ciphertext of nb 16-byte blocks
 // starting at chunk c0 of the payload (pl points there; keystream blocks from
-// c0 + 1); b0 / b1 hold its chunks 0 / 1 (loads already issued).  The
-// first step is peeled (nothing to absorb yet), so that every absorb inside
-// the loop is unconditional; chunk c always lives in buffer c % 2.
+// c0 + 1); b0 / b1 (/ b2) hold its chunks 0 / 1 (/ 2) (loads already issued).
+// The first step is peeled (nothing to absorb yet), so that every absorb
+// inside the loop is unconditional; chunk c always lives in buffer c % kDepth.
 // head / has_head: the DataHeader a seal writes in front of the payload (only
 // the lane whose segment starts the payload has one).
 template <bool OPEN, int MODE = 0>
 __device__ __forceinline__ Acc pipe_pass(uint4 *pl, const Stream &st, const Mul &r, uint32_t nb, uint32_t c0,
-                                         Chunk &b0, Chunk &b1, uint4 head, bool has_head) {
+                                         Chunk &b0, Chunk &b1, Chunk &b2, uint4 head, bool has_head) {
     const uint32_t F = nb >> 2, bl = nb & 3u; // full chunks, blocks in the partial last chunk
     Acc h = {0, 0, 0, 0, 0};
     Chunk pi = {};
@@ -149,20 +157,32 @@ __device__ __forceinline__ Acc pipe_pass(uint4 *pl, const Stream &st, const Mul 
     if (F > 0) {
         pipe_step<OPEN, false, false, MODE>(pl, st, r, h, pi, b0, prev, have_prev, 0, nb, c0);
         uint32_t t = 1;
-        // whole pairs only: a step that may be skipped would leave the waitcnt
-        // pass a path without its memory operations (vmcnt(0) at the next one)
-        for (; t + 1 < F; t += 2) {
-            pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0);
-            pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b0, prev, have_prev, t + 1, nb, c0);
+        // whole rounds of kDepth steps only: a step that may be skipped would
+        // leave the waitcnt pass a path without its memory operations
+        // (vmcnt(0) at the next one); the remainder steps run after the loop
+        if constexpr (kDepth == 3) {
+            for (; t + 2 < F; t += 3) {
+                pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0);
+                pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b2, prev, have_prev, t + 1, nb, c0);
+                pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b0, prev, have_prev, t + 2, nb, c0);
+            }
+            if (t < F) pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0);
+            if (t + 1 < F) pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b2, prev, have_prev, t + 1, nb, c0);
+        } else {
+            for (; t + 1 < F; t += 2) {
+                pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0);
+                pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b0, prev, have_prev, t + 1, nb, c0);
+            }
+            if (t < F) pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0);
         }
-        if (t < F) pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0);
         pending = 4;
     }
     if (bl > 0) {
-        // chunk F lives in b(F % 2); select by value (a reference select
-        // between the two buffers would move both to scratch memory)
-        const bool odd = F & 1u;
-        Chunk bp = {odd ? b1.q0 : b0.q0, odd ? b1.q1 : b0.q1, odd ? b1.q2 : b0.q2, odd ? b1.q3 : b0.q3};
+        // chunk F lives in b(F % kDepth); select by value (a reference select
+        // between the buffers would move them to scratch memory)
+        const uint32_t k = F % kDepth;
+        Chunk bp = {k == 1 ? b1.q0 : k == 2 ? b2.q0 : b0.q0, k == 1 ? b1.q1 : k == 2 ? b2.q1 : b0.q1,
+                    k == 1 ? b1.q2 : k == 2 ? b2.q2 : b0.q2, k == 1 ? b1.q3 : k == 2 ? b2.q3 : b0.q3};
         if (F > 0) pipe_step<OPEN, true, true, MODE>(pl, st, r, h, pi, bp, prev, have_prev, F, nb, c0);
         else pipe_step<OPEN, false, true, MODE>(pl, st, r, h, pi, bp, prev, have_prev, F, nb, c0);
         pending = bl;
@@ -274,14 +294,16 @@ __device__ __forceinline__ void pipe_seal_packet(const SealArgs &a, uint32_t i, 
     const Seg sg = make_seg(nb, j, G);
     // an empty segment reads (never writes) the payload start, which is in the frame
     uint4 *pl = reinterpret_cast<uint4 *>(frame + 16) + (sg.nb ? 4 * sg.c0 : 0);
-    Chunk b0, b1;
+    Chunk b0, b1, b2 = {};
     if constexpr (MODE == 1) {
         b0 = {make_uint4(i, 1, 2, 3), make_uint4(4, i, 6, 7), make_uint4(8, 9, i, 11), make_uint4(12, 13, 14, i)};
         b1 = b0;
+        b2 = b0;
     } else {
         constexpr int NT = MODE >= 4 ? MODE - 3 : 0;
         load_chunk<NT>(b0, pl, 0, sg.nb ? sg.nb - 1 : 0);
         load_chunk<NT>(b1, pl, 1, sg.nb ? sg.nb - 1 : 0);
+        if constexpr (kDepth == 3) load_chunk<NT>(b2, pl, 2, sg.nb ? sg.nb - 1 : 0);
     }
     const Key8 key = load_key(a.keys, d.key_idx);
     const uint64_t ctr = a.counters[i];
@@ -295,7 +317,7 @@ __device__ __forceinline__ void pipe_seal_packet(const SealArgs &a, uint32_t i, 
     // together with the first payload blocks
     const bool head = a.receivers != nullptr && j == 0;
     const uint4 hdr = make_uint4(4u, head ? a.receivers[d.key_idx] : 0u, n1, n2);
-    Acc h = pipe_pass<false, MODE>(pl, stm, r, sg.nb, sg.c0, b0, b1, hdr, head);
+    Acc h = pipe_pass<false, MODE>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, hdr, head);
     RG_MARK(3, h.h4);
     h = combine_segments(h, r, sg.after, G);
     RG_MARK(5, h.h4);
@@ -323,9 +345,27 @@ __device__ __forceinline__ void pipe_open_packet(const OpenArgs &a, uint32_t i, 
         st = RG_PKT_INVALID;
     else st = 0xFF;
     uint8_t *frame = a.buf + d.offset;
+    // Every load the lane needs is issued before the header is inspected, so
+    // the header check costs no round trip of its own.  Loads stay
+    // unconditional (exact waits): a frame that fails the descriptor checks
+    // reads its own descriptor instead (a valid address), a length that cannot
+    // decrypt reads no payload.
+    const bool desc_ok = st == 0xFF;
+    const bool go = desc_ok && W >= 32 && (W & 15u) == 0;
+    const uint32_t P = go ? W - 32 : 0;
+    const uint32_t nb = P >> 4;
+    const Seg sg = make_seg(nb, j, G);
+    uint4 *safe = const_cast<uint4 *>(reinterpret_cast<const uint4 *>(a.desc + i));
+    uint4 *pl = go ? reinterpret_cast<uint4 *>(frame + 16) + (sg.nb ? 4 * sg.c0 : 0) : safe;
+    const uint4 hdr = *(desc_ok ? reinterpret_cast<const uint4 *>(frame) : safe);
+    Chunk b0, b1, b2 = {};
+    load_chunk(b0, pl, 0, sg.nb ? sg.nb - 1 : 0);
+    load_chunk(b1, pl, 1, sg.nb ? sg.nb - 1 : 0);
+    if constexpr (kDepth == 3) load_chunk(b2, pl, 2, sg.nb ? sg.nb - 1 : 0);
+    const uint4 want = *(go ? reinterpret_cast<const uint4 *>(frame + 16 + P) : safe);
+    const Key8 key = load_key(a.keys, go ? d.key_idx : 0);
     uint64_t ctr = 0;
-    if (st == 0xFF) {
-        const uint4 hdr = *reinterpret_cast<const uint4 *>(frame);
+    if (desc_ok) {
         if (hdr.x != 4u) st = RG_PKT_NOT_DATA;
         else if ((W & 15u) != 0 || W < 16) st = RG_PKT_INVALID;
         else {
@@ -340,21 +380,12 @@ __device__ __forceinline__ void pipe_open_packet(const OpenArgs &a, uint32_t i, 
         }
         return;
     }
-    const uint32_t P = W - 32;
-    const uint32_t nb = P >> 4;
-    const Seg sg = make_seg(nb, j, G);
-    uint4 *pl = reinterpret_cast<uint4 *>(frame + 16) + (sg.nb ? 4 * sg.c0 : 0);
-    Chunk b0, b1;
-    load_chunk(b0, pl, 0, sg.nb ? sg.nb - 1 : 0);
-    load_chunk(b1, pl, 1, sg.nb ? sg.nb - 1 : 0);
-    const uint4 want = *reinterpret_cast<const uint4 *>(frame + 16 + P);
-    const Key8 key = load_key(a.keys, d.key_idx);
     const uint32_t n1 = (uint32_t)ctr, n2 = (uint32_t)(ctr >> 32);
     const Stream stm = make_stream(key, 0u, n1, n2);
     uint32_t ks[16];
     stream_block(stm, 0, ks);
     const Mul r = make_mul(ks[0], ks[1], ks[2], ks[3]);
-    Acc h = pipe_pass<true>(pl, stm, r, sg.nb, sg.c0, b0, b1, make_uint4(0, 0, 0, 0), false);
+    Acc h = pipe_pass<true>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, make_uint4(0, 0, 0, 0), false);
     h = combine_segments(h, r, sg.after, G);
     uint32_t tag[4];
     pipe_tag(h, r, P, ks + 4, tag);

@@ -13,7 +13,7 @@ for r in $(seq "$REPS"); do
             if [ "$v" = base ]; then unset RG_AEAD_LIB; else export RG_AEAD_LIB=tools/build/librg_$v.so; fi
             log=gpurun_out/ab_${v}_${w}_$r.log
             timeout -k 10 200 python bench.py --workload "$w" --steps 20 --warmup 3 --cpu-seconds 0 "$@" >"$log" 2>&1 || exit $?
-            echo "$v $w $r $(grep '"value"' "$log" | python3 -c 'import sys,json; d=json.loads(sys.stdin.read()); print(d["value"], d["seal_ms"], d["open_ms"])')"
+            echo "$v $w $r $(grep '"value"' "$log" | python3 -c 'import sys,json; d=json.loads(sys.stdin.read()); print(d["value"], d["seal_ms"], d["open_ms"], d.get("cold_cache", {}).get("gib_s"))')"
         done
     done
 done
