@@ -65,6 +65,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--e2e", action="store_true", help="also time the pinned host->GPU->host path")
+    ap.add_argument("--no-cold", dest="cold", action="store_false",
+                    help="skip the cold-cache pass (profiling runs: keeps per-kernel averages to the step's regime)")
     ap.add_argument("--no-verify", dest="verify", action="store_false",
                     help="skip the status check after the timed region (on by default, outside the timing)")
     return ap.parse_args()
@@ -74,7 +76,7 @@ def kernel_label(args, eng, w) -> str:
     k = eng.kernel_for(w.n)
     plan = ({0: "off", 1: "on"}).get(args.plan, "auto")
     if k == 0:
-        return (f"pipelined lanes ({eng.lanes_per_packet(w.n)} lane(s)/packet without plan, 2-deep chunk prefetch, "
+        return (f"pipelined lanes ({eng.lanes_per_packet(w.n)} lane(s)/packet without plan, 3 chunks in flight, "
                 f"Poly1305 in keystream rounds), planner {plan}")
     return f"lds-staged tiles, {k} chunks/window, planner {plan}, segments {args.segments or 'auto'}"
 
@@ -284,7 +286,7 @@ def main():
     open_ms = sum(e[2].elapsed_time(e[3]) for e in evs) / reps
     if args.verify:
         assert (b.status[: w.n] == 0).all().item(), "open failed in the kernel-timing pass"
-    cold = cold_cache_timing(eng, w, b, stream, args.verify) if w.buf_bytes < MALL_BYTES else None
+    cold = cold_cache_timing(eng, w, b, stream, args.verify) if args.cold and w.buf_bytes < MALL_BYTES else None
 
     t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
     if dist is not None:

@@ -154,7 +154,7 @@ int rg_get_lanes_per_packet(rg_ctx *ctx, size_t n);
 int rg_set_wg_per_cu(rg_ctx *ctx, int wg_per_cu);
 /* Kernel choice: -1 (default) = automatic by batch size (rg_get_kernel);
  * 0 = pipelined lane kernel (one packet -- or one of lanes_per_packet
- * contiguous segments -- per lane, 2-deep register prefetch, Poly1305 folded
+ * contiguous segments -- per lane, 3 chunks in flight, Poly1305 folded
  * into the keystream rounds); 1/2 = LDS-staged tiles (one packet (segment) per
  * lane, coalesced LDS-DMA windows of that many 64-byte chunks). */
 int rg_set_staged(rg_ctx *ctx, int kernel);

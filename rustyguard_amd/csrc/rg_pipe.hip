@@ -11,9 +11,9 @@
 // the loop head makes the wave wait for chunk t+1 one keystream period after
 // issuing it -- and (b) the serial Poly1305 chain, whose multiply-carry
 // dependencies leave issue slots empty.  Here
-//  * two chunk buffers alternate (the loop is unrolled twice, nothing in flight
-//    is ever copied): chunk t+2 is requested as soon as chunk t is written, so
-//    a load has two keystream periods (~3 us) to arrive;
+//  * kDepth (3) chunk buffers rotate (the loop is unrolled kDepth times,
+//    nothing in flight is ever copied): chunk t+3 is requested as soon as
+//    chunk t is written, so a load has three keystream periods to arrive;
 //  * chunk t-1's four Poly1305 blocks are absorbed inside chunk t's keystream
 //    rounds (after double rounds 1, 3, 5, 7), where the ARX chains leave the
 //    multiply chain's latency covered;
@@ -80,7 +80,7 @@ __device__ __forceinline__ void absorb_chunk(Acc &h, const Chunk &c, const Mul &
 
 // One step: keystream block t+1 -- with the previous chunk's four Poly1305
 // blocks (pi, always a full chunk) absorbed in its rounds when ABSORB -- XORed
-// into chunk t (buf) and stored; then chunk t+2 is requested into buf.  Full
+// into chunk t (buf) and stored; then chunk t+kDepth is requested into buf.  Full
 // steps store unconditionally: a store under a branch leaves the waitcnt pass
 // a path with fewer memory operations, and since vmcnt counts stores as well
 // as loads it would then also wait for the last step's stores to be acked.

@@ -68,14 +68,14 @@ for s in "$@"; do
     prof)
         W=${RG_WORKLOAD:-cfg2}
         run prof_$W 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$W -o run -- \
-            python3 bench.py --workload $W --steps 30 --warmup 5 --cpu-seconds 0 ;;
+            python3 bench.py --workload $W --steps 30 --warmup 5 --cpu-seconds 0 --no-cold ;;
     pmc_hbm)
         # separate passes: FETCH_SIZE and WRITE_SIZE do not fit one pass; never combined with tracing domains
         W=${RG_WORKLOAD:-cfg2}
         run pmc_fetch_$W 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch_$W -o p -- \
-            python3 bench.py --workload $W --steps 5 --warmup 2 --cpu-seconds 0
+            python3 bench.py --workload $W --steps 5 --warmup 2 --cpu-seconds 0 --no-cold
         run pmc_write_$W 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write_$W -o p -- \
-            python3 bench.py --workload $W --steps 5 --warmup 2 --cpu-seconds 0 ;;
+            python3 bench.py --workload $W --steps 5 --warmup 2 --cpu-seconds 0 --no-cold ;;
     variants) each_variant bench_variant; summ gpurun_out/var_*.log ;;
     stamps_v) each_variant stamp_variant ;;
     pmc_clock) each_variant pmc_variant; python3 tools/pmc_clock.py gpurun_out/pmcclk_* ;;
