@@ -235,6 +235,44 @@ def test_random_batches_vs_oracle(engine, mode, seed):
     _reset(engine)
 
 
+@pytest.mark.parametrize("wg", [1, 2, 3])
+def test_planned_pipe_residency_vs_oracle(engine, wg):
+    """The planned pipelined path deals its size-ordered tiles round robin over CUs x wg_per_cu x 4
+    waves (default 2 per CU): mixed sizes, invalid and skipped descriptors at 1, 2 and 3 resident
+    workgroups per CU give the oracle's bytes and statuses."""
+    _reset(engine)
+    engine.set_staged(0)
+    engine.set_plan(1)
+    engine.set_wg_per_cu(wg)
+    try:
+        rng = np.random.default_rng(50 + wg)
+        n = 20000
+        sizes = rng.choice([64, 576, 1504, 0, 16, 2048], n, p=[0.5, 0.3, 0.1, 0.04, 0.04, 0.02])
+        keys, rec, desc, ctr, buf = _random_batch(rng, n, nkeys=4, sizes=sizes)
+        want = buf.copy()
+        wst = np.zeros(n, np.uint8)
+        oracle.seal_batch(keys, rec, desc, ctr, want, nthreads=8, status=wst)
+        got, st = _gpu_seal(engine, keys, rec, desc, ctr, buf)
+        assert np.array_equal(st, wst) and np.array_equal(got, want)
+        od = desc.copy()
+        od["len"] += 32
+        od["len"][5::89] = 31  # not a whole number of 16-byte blocks: invalid after the header check
+        skip = np.zeros(n, bool)
+        skip[::97] = True  # RG_KEY_SKIP: rejected and untouched (the oracle never sees these frames)
+        want_open = got.copy()
+        wst = np.full(n, aead.PKT_REJECTED, np.uint8)
+        wco = np.zeros(n, np.uint64)
+        wst[~skip], wco[~skip] = oracle.open_batch(keys, od[~skip], want_open, nthreads=8)
+        od["key_idx"][skip] = aead.KEY_SKIP
+        back, st, co = _gpu_open(engine, keys, od, got)
+        assert np.array_equal(st, wst) and np.array_equal(back, want_open)
+        ok = wst == aead.PKT_OK
+        assert np.array_equal(co[ok], wco[ok])
+    finally:
+        engine.set_wg_per_cu(0)
+        _reset(engine)
+
+
 @pytest.mark.parametrize("mode", MODES, ids=_mode_id)
 def test_large_payload_mix_vs_oracle(engine, mode):
     """Every size class of the planner (up to the 1 MiB payload limit), shuffled with small packets,
