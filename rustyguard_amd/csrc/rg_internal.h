@@ -117,12 +117,19 @@ constexpr uint32_t kSchedWords = 128;
 constexpr uint32_t kSchedStart = 4, kSchedLg = 44, kSchedCnt = 84;
 static_assert(kSchedCnt + kClasses <= kSchedWords, "schedule words");
 
-// One wave (lanes 0-63), lane c owns size class c.  Segments per class: the
-// fewest (power of two) that keep a lane's slots (1 one-time-key block + its
-// chunks) within the batch's mean work per SIMD, so that no tile outlasts the
-// balanced schedule; tiles are numbered largest class first (the round robin
-// then deals long tiles before short ones).  Takes the planner's final class
-// counts over into sched[] and zeroes them for the next batch.
+// One wave (lanes 0-63), lane c owns size class c.  Segments per class: for
+// a target T, the fewest (power of two) that keep a lane's slots (1
+// one-time-key block + its chunks) within T.  Tiles are numbered by lane work
+// w = slots (+1 for the r^N combine of split packets), heaviest first, and the
+// kernel deals tile t to wave slot t mod (waves): waves t and t + simds share a
+// SIMD, so SIMD 0 carries the most work, sum_m w(tile m * simds).  That sum is
+// the launch's estimated makespan; the target is chosen among multiples of
+// the batch's mean work per SIMD (1, 1.25, 1.5, 2, 3, no splitting) by the
+// smallest estimate, then the least total work.  (A fixed target of the mean
+// left config 3 with 1029 tiles of ~6 slots for 1024 SIMDs: five SIMDs ran two,
+// 13 slots against a mean of 6.6, profiles/r1e_*; now 10 + 2.)
+// Takes the planner's final class counts over into sched[] and zeroes them
+// for the next batch.
 __device__ __forceinline__ void schedule_classes(uint32_t *counts, uint32_t *sched, uint32_t simds,
                                                  uint32_t *classes_out) {
     const uint32_t c = threadIdx.x & 63;
@@ -130,29 +137,61 @@ __device__ __forceinline__ void schedule_classes(uint32_t *counts, uint32_t *sch
         c < kClasses ? __hip_atomic_load(&counts[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
     if (c < kClasses) __hip_atomic_store(&counts[c], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t chunks = c < kClasses ? class_hi(c) : 0;
-    uint64_t work = (uint64_t)cnt * (1 + chunks); // lane slots with one lane per packet
+    // One wave, serial over candidates.  Cross-lane values move by readlane
+    // (scalar) over the non-empty classes and by ballots: a version with
+    // butterfly shuffle reductions (LDS permutes, serially dependent) and
+    // 64-bit divisions added 4-6 us to the planner.
+    const uint64_t used = __ballot(cnt > 0);
+    float work = 0.0f; // lane slots with one lane per packet
+    for (uint64_t m = used; m; m &= m - 1) {
+        const int j = __ffsll((unsigned long long)m) - 1;
+        work += (float)(uint32_t)__builtin_amdgcn_readlane((int)cnt, j) * (float)(1 + class_hi((uint32_t)j));
+    }
+    const uint32_t S = simds ? simds : 1;
+    const float mean = work / (64.0f * (float)S);
+    uint32_t best_est = ~0u, best_lg = 0, best_start = 0, best_total = 0;
+    float best_sum = 3.0e38f;
+    constexpr float kF[6] = {1.0f, 1.25f, 1.5f, 2.0f, 3.0f, 0.0f}; // target = mean x f; 0: no splitting
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) work += (uint64_t)__shfl_xor((long long)work, o);
-    const uint64_t per_simd = (work + 64ull * simds - 1) / (64ull * simds);
-    const uint32_t target = (uint32_t)(per_simd < 2 ? 2 : per_simd > 0xFFFF ? 0xFFFF : per_simd);
-    uint32_t lg = 0;
-    while (lg < 6 && 1 + (chunks + (1u << lg) - 1) / (1u << lg) > target) ++lg;
-    const uint32_t tiles = (uint32_t)((((uint64_t)cnt << lg) + 63) / 64);
-    // first tile of class c = tiles of all larger classes (suffix sum)
-    uint32_t suffix = tiles;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t v = (uint32_t)__shfl_down((int)suffix, o);
-        if (c + o < 64) suffix += v;
+    for (int k = 0; k < 6; ++k) {
+        const float tf = kF[k] > 0.0f ? ceilf(mean * kF[k]) : 65535.0f;
+        const uint32_t target = tf < 2.0f ? 2u : tf > 65535.0f ? 65535u : (uint32_t)tf;
+        uint32_t lg = 0;
+        while (lg < 6 && 1 + ((chunks + (1u << lg) - 1) >> lg) > target) ++lg;
+        const uint32_t tiles = cnt ? (uint32_t)((((uint64_t)cnt << lg) + 63) >> 6) : 0;
+        const uint32_t w = cnt ? 1 + ((chunks + (1u << lg) - 1) >> lg) + (lg ? 1 : 0) : 0;
+        // first tile: tiles of the classes ahead in (w desc, class desc) order
+        uint32_t start = 0, total = 0;
+        float sum = 0.0f;
+        for (uint64_t m = used; m; m &= m - 1) {
+            const int j = __ffsll((unsigned long long)m) - 1;
+            const uint32_t wj = (uint32_t)__builtin_amdgcn_readlane((int)w, j);
+            const uint32_t tj = (uint32_t)__builtin_amdgcn_readlane((int)tiles, j);
+            if (wj > w || (wj == w && (uint32_t)j > c)) start += tj;
+            total += tj;
+            sum += (float)tj * (float)wj;
+        }
+        // SIMD 0's work: the tiles m * S, m < ceil(total / S)
+        uint32_t est = 0;
+        for (uint32_t t = 0; t < total; t += S) {
+            const uint64_t hit = __ballot(tiles > 0 && start <= t && t < start + tiles);
+            est += (uint32_t)__builtin_amdgcn_readlane((int)w, __ffsll((unsigned long long)hit) - 1);
+        }
+        if (est < best_est || (est == best_est && sum < best_sum)) { // wave-uniform
+            best_est = est;
+            best_sum = sum;
+            best_lg = lg;
+            best_start = start;
+            best_total = total;
+        }
     }
     if (c < kClasses) {
-        sched[kSchedStart + c] = suffix - tiles;
-        sched[kSchedLg + c] = lg;
+        sched[kSchedStart + c] = best_start;
+        sched[kSchedLg + c] = best_lg;
         sched[kSchedCnt + c] = cnt;
     }
-    const uint64_t used = __ballot(cnt > 0);
     if (c == 0) {
-        sched[2] = suffix; // lane 0: all tiles
+        sched[2] = best_total;
         if (classes_out) *reinterpret_cast<volatile uint32_t *>(classes_out) = (uint32_t)__popcll(used);
     }
 }

@@ -430,7 +430,7 @@ __device__ __forceinline__ void pipe_stamp(uint64_t *dbg, uint64_t t0, uint64_t 
 // Identity order: lane units u = G * packet + segment, grid-stride (the stride
 // is a multiple of 256, so a packet's G lanes stay together in one wave);
 // lg = log2(G).
-// Planned order: wave w takes tiles w, w + W, ... of the size-ordered tile
+// Planned order: wave w takes tiles w, w + W, ... of the work-ordered tile
 // list; lane l of a tile of class c is unit (tile - first tile of c) * 64 + l
 // of that class.
 //

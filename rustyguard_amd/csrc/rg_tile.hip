@@ -46,7 +46,10 @@ __device__ __forceinline__ uint32_t class_of(uint32_t chunks) {
 // class one ballot -> one LDS atomic (runs of consecutive packets stay
 // together), then one global atomic per class and workgroup.  Uniform batches
 // therefore keep tiles of 64 consecutive frames.
-constexpr uint32_t kPlanPer = 2;
+#ifndef RG_PLAN_PER
+#define RG_PLAN_PER 2 // 1, 8 and 16 measured slower at config 3 (round r1e)
+#endif
+constexpr uint32_t kPlanPer = RG_PLAN_PER;
 
 __global__ __launch_bounds__(256) void plan_kernel(const rg_pkt_desc *desc, uint32_t n, uint32_t open,
                                                    uint32_t *counts, uint32_t *lists, uint32_t cap, uint32_t *sched,

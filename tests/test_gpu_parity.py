@@ -273,6 +273,40 @@ def test_planned_pipe_residency_vs_oracle(engine, wg):
         _reset(engine)
 
 
+@pytest.mark.parametrize("mix", ["imix", "half_1504_64", "576_1504", "spread"])
+def test_schedule_targets_vs_oracle(engine, mix):
+    """Size mixes whose best segment target differs (schedule_classes picks among multiples of the mean
+    work per SIMD by the estimated makespan): the planned pipelined path gives the oracle's bytes."""
+    _reset(engine)
+    engine.set_staged(0)
+    engine.set_plan(1)
+    try:
+        rng = np.random.default_rng(77)
+        n = 40000
+        if mix == "imix":
+            sizes = rng.choice([64, 576, 1504], n, p=[7 / 12, 4 / 12, 1 / 12])
+        elif mix == "half_1504_64":
+            sizes = rng.choice([64, 1504], n)
+        elif mix == "576_1504":
+            sizes = rng.choice([576, 1504], n)
+        else:
+            sizes = rng.integers(0, 129, n) * 16
+        keys, rec, desc, ctr, buf = _random_batch(rng, n, nkeys=2, sizes=sizes)
+        want = buf.copy()
+        oracle.seal_batch(keys, rec, desc, ctr, want, nthreads=8)
+        got, st = _gpu_seal(engine, keys, rec, desc, ctr, buf)
+        assert (st == aead.PKT_OK).all() and np.array_equal(got, want)
+        od = desc.copy()
+        od["len"] += 32
+        want_open = got.copy()
+        wst, wco = oracle.open_batch(keys, od, want_open, nthreads=8)
+        back, st, co = _gpu_open(engine, keys, od, got)
+        assert (wst == aead.PKT_OK).all() and np.array_equal(st, wst) and np.array_equal(co, wco)
+        assert np.array_equal(back, want_open)
+    finally:
+        _reset(engine)
+
+
 @pytest.mark.parametrize("mode", MODES, ids=_mode_id)
 def test_large_payload_mix_vs_oracle(engine, mode):
     """Every size class of the planner (up to the 1 MiB payload limit), shuffled with small packets,
