@@ -117,7 +117,7 @@ constexpr uint32_t kSchedWords = 128;
 constexpr uint32_t kSchedStart = 4, kSchedLg = 44, kSchedCnt = 84;
 static_assert(kSchedCnt + kClasses <= kSchedWords, "schedule words");
 
-// One wave (lanes 0-63), lane c owns size class c.  Segments per class: for
+// Lane c (of each wave) owns size class c.  Segments per class: for
 // a target T, the fewest (power of two) that keep a lane's slots (1
 // one-time-key block + its chunks) within T.  Tiles are numbered by lane work
 // w = slots (+1 for the r^N combine of split packets), heaviest first, and the
@@ -130,17 +130,21 @@ static_assert(kSchedCnt + kClasses <= kSchedWords, "schedule words");
 // 13 slots against a mean of 6.6, profiles/r1e_*; now 10 + 2.)
 // Takes the planner's final class counts over into sched[] and zeroes them
 // for the next batch.
+// Called by all 256 threads of the planner's last workgroup: wave v evaluates
+// candidates v and v + 4, wave 0 then writes the best one.
+constexpr int kTargets = 6;
 __device__ __forceinline__ void schedule_classes(uint32_t *counts, uint32_t *sched, uint32_t simds,
                                                  uint32_t *classes_out) {
-    const uint32_t c = threadIdx.x & 63;
+    __shared__ uint32_t s_lg[kTargets][64], s_start[kTargets][64], s_est[kTargets], s_total[kTargets];
+    __shared__ float s_sum[kTargets];
+    const uint32_t c = threadIdx.x & 63, v = threadIdx.x >> 6;
     const uint32_t cnt =
         c < kClasses ? __hip_atomic_load(&counts[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
-    if (c < kClasses) __hip_atomic_store(&counts[c], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t chunks = c < kClasses ? class_hi(c) : 0;
-    // One wave, serial over candidates.  Cross-lane values move by readlane
-    // (scalar) over the non-empty classes and by ballots: a version with
-    // butterfly shuffle reductions (LDS permutes, serially dependent) and
-    // 64-bit divisions added 4-6 us to the planner.
+    // Cross-lane values move by readlane (scalar) over the non-empty classes
+    // and by ballots: a version with butterfly shuffle reductions (LDS
+    // permutes, serially dependent) and 64-bit divisions added 4-6 us to the
+    // planner; one wave evaluating all candidates ~3 us.
     const uint64_t used = __ballot(cnt > 0);
     float work = 0.0f; // lane slots with one lane per packet
     for (uint64_t m = used; m; m &= m - 1) {
@@ -149,11 +153,8 @@ __device__ __forceinline__ void schedule_classes(uint32_t *counts, uint32_t *sch
     }
     const uint32_t S = simds ? simds : 1;
     const float mean = work / (64.0f * (float)S);
-    uint32_t best_est = ~0u, best_lg = 0, best_start = 0, best_total = 0;
-    float best_sum = 3.0e38f;
-    constexpr float kF[6] = {1.0f, 1.25f, 1.5f, 2.0f, 3.0f, 0.0f}; // target = mean x f; 0: no splitting
-#pragma unroll
-    for (int k = 0; k < 6; ++k) {
+    constexpr float kF[kTargets] = {1.0f, 1.25f, 1.5f, 2.0f, 3.0f, 0.0f}; // target = mean x f; 0: no splitting
+    for (uint32_t k = v; k < (uint32_t)kTargets; k += 4) {
         const float tf = kF[k] > 0.0f ? ceilf(mean * kF[k]) : 65535.0f;
         const uint32_t target = tf < 2.0f ? 2u : tf > 65535.0f ? 65535u : (uint32_t)tf;
         uint32_t lg = 0;
@@ -177,21 +178,27 @@ __device__ __forceinline__ void schedule_classes(uint32_t *counts, uint32_t *sch
             const uint64_t hit = __ballot(tiles > 0 && start <= t && t < start + tiles);
             est += (uint32_t)__builtin_amdgcn_readlane((int)w, __ffsll((unsigned long long)hit) - 1);
         }
-        if (est < best_est || (est == best_est && sum < best_sum)) { // wave-uniform
-            best_est = est;
-            best_sum = sum;
-            best_lg = lg;
-            best_start = start;
-            best_total = total;
+        s_lg[k][c] = lg;
+        s_start[k][c] = start;
+        if (c == 0) {
+            s_est[k] = est;
+            s_sum[k] = sum;
+            s_total[k] = total;
         }
     }
+    __syncthreads();
+    if (v != 0) return;
+    uint32_t best = 0;
+    for (uint32_t k = 1; k < (uint32_t)kTargets; ++k) // smallest estimate, then least total work
+        if (s_est[k] < s_est[best] || (s_est[k] == s_est[best] && s_sum[k] < s_sum[best])) best = k;
     if (c < kClasses) {
-        sched[kSchedStart + c] = best_start;
-        sched[kSchedLg + c] = best_lg;
+        __hip_atomic_store(&counts[c], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sched[kSchedStart + c] = s_start[best][c];
+        sched[kSchedLg + c] = s_lg[best][c];
         sched[kSchedCnt + c] = cnt;
     }
     if (c == 0) {
-        sched[2] = best_total;
+        sched[2] = s_total[best];
         if (classes_out) *reinterpret_cast<volatile uint32_t *>(classes_out) = (uint32_t)__popcll(used);
     }
 }

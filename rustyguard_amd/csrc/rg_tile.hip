@@ -108,7 +108,7 @@ __global__ __launch_bounds__(256) void plan_kernel(const rg_pkt_desc *desc, uint
     __syncthreads();
     if (tid == 0) last = atomicAdd(&counts[kClasses], 1u) == gridDim.x - 1;
     __syncthreads();
-    if (last && tid < 64) {
+    if (last) { // block-uniform: the whole workgroup schedules (its barrier inside)
         schedule_classes(counts, sched, simds, classes_out);
         if (tid == 0) __hip_atomic_store(&counts[kClasses], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
