@@ -389,7 +389,7 @@ static hipError_t launch_pipe_any(rg_ctx *ctx, const rg::SealArgs *sa, const rg:
     e = rg::launch_plan(sa ? sa->desc : oa->desc, n, oa != nullptr, tp, st);
     if (e != hipSuccess) return e;
     rg::PipePlan pp{static_cast<uint32_t *>(pb.counts.p), static_cast<const uint32_t *>(pb.lists.p), pb.cap,
-                    static_cast<uint32_t *>(pb.sched.p), pb.d_classes};
+                    static_cast<uint32_t *>(pb.sched.p), pb.d_classes, tp.simds};
     return rg::launch_pipe(sa, oa, Lp, &pp, st);
 }
 

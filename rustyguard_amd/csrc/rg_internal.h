@@ -120,14 +120,16 @@ static_assert(kSchedCnt + kClasses <= kSchedWords, "schedule words");
 // Lane c (of each wave) owns size class c.  Segments per class: for
 // a target T, the fewest (power of two) that keep a lane's slots (1
 // one-time-key block + its chunks) within T.  Tiles are numbered by lane work
-// w = slots (+1 for the r^N combine of split packets), heaviest first, and the
-// kernel deals tile t to wave slot t mod (waves): waves t and t + simds share a
-// SIMD, so SIMD 0 carries the most work, sum_m w(tile m * simds).  That sum is
-// the launch's estimated makespan; the target is chosen among multiples of
+// w = slots (+1 for the r^N combine of split packets), heaviest first.  The
+// kernel deals them in rounds of S = simds tiles, snake order (SIMD s takes
+// tile s of even rounds, S-1-s of odd ones; wave slots w and w + S share a
+// SIMD), so the heaviest and the lightest tiles meet on one SIMD.  The larger
+// work of SIMDs 0 and S-1 is the launch's estimated makespan (it matched the
+// true maximum in every mix simulated); the target is chosen among multiples of
 // the batch's mean work per SIMD (1, 1.25, 1.5, 2, 3, no splitting) by the
 // smallest estimate, then the least total work.  (A fixed target of the mean
 // left config 3 with 1029 tiles of ~6 slots for 1024 SIMDs: five SIMDs ran two,
-// 13 slots against a mean of 6.6, profiles/r1e_*; now 10 + 2.)
+// 13 slots against a mean of 6.6; now at most 10, profiles/r1e_*.)
 // Takes the planner's final class counts over into sched[] and zeroes them
 // for the next batch.
 // Called by all 256 threads of the planner's last workgroup: wave v evaluates
@@ -172,12 +174,18 @@ __device__ __forceinline__ void schedule_classes(uint32_t *counts, uint32_t *sch
             total += tj;
             sum += (float)tj * (float)wj;
         }
-        // SIMD 0's work: the tiles m * S, m < ceil(total / S)
-        uint32_t est = 0;
-        for (uint32_t t = 0; t < total; t += S) {
-            const uint64_t hit = __ballot(tiles > 0 && start <= t && t < start + tiles);
-            est += (uint32_t)__builtin_amdgcn_readlane((int)w, __ffsll((unsigned long long)hit) - 1);
+        // work of SIMDs 0 and S-1 under the snake deal: round m holds tiles
+        // [mS, mS + S), SIMD s takes tile mS + s in even rounds and
+        // mS + S-1-s in odd ones
+        uint32_t est0 = 0, est1 = 0;
+        for (uint32_t t = 0, m = 0; t < total; t += S, ++m) {
+            const uint32_t a = t + (m & 1u ? S - 1 : 0), b = t + (m & 1u ? 0 : S - 1);
+            const uint64_t ha = __ballot(tiles > 0 && start <= a && a < start + tiles);
+            const uint64_t hb = __ballot(tiles > 0 && start <= b && b < start + tiles);
+            if (ha) est0 += (uint32_t)__builtin_amdgcn_readlane((int)w, __ffsll((unsigned long long)ha) - 1);
+            if (hb) est1 += (uint32_t)__builtin_amdgcn_readlane((int)w, __ffsll((unsigned long long)hb) - 1);
         }
+        const uint32_t est = est0 > est1 ? est0 : est1;
         s_lg[k][c] = lg;
         s_start[k][c] = start;
         if (c == 0) {
@@ -209,6 +217,7 @@ struct PipePlan {
     uint32_t cap;
     uint32_t *sched;       // [kSchedWords] per-batch schedule
     uint32_t *classes_out; // host-mapped: non-empty classes of the batch (or nullptr)
+    uint32_t simds;        // S of the schedule: waves w and w + S share a SIMD (grid = S x passes waves)
 };
 hipError_t launch_pipe(const SealArgs *sa, const OpenArgs *oa, const Launch &L, const PipePlan *plan,
                        hipStream_t s);

@@ -430,9 +430,9 @@ __device__ __forceinline__ void pipe_stamp(uint64_t *dbg, uint64_t t0, uint64_t 
 // Identity order: lane units u = G * packet + segment, grid-stride (the stride
 // is a multiple of 256, so a packet's G lanes stay together in one wave);
 // lg = log2(G).
-// Planned order: wave w takes tiles w, w + W, ... of the work-ordered tile
-// list; lane l of a tile of class c is unit (tile - first tile of c) * 64 + l
-// of that class.
+// Planned order: the schedule's snake deal of the work-ordered tile list
+// (schedule_classes); lane l of a tile of class c is unit (tile - first tile
+// of c) * 64 + l of that class.
 //
 // Both orders share one loop, so the packet body has a single call site (two
 // would make the compiler emit it as a real function call: stack frame, kernel
@@ -442,18 +442,25 @@ __device__ __forceinline__ void pipe_walk(uint32_t n, uint32_t lg0, const PipePl
                                           bool stamp, uint64_t marks[2], Body &&body) {
     const uint32_t lane = threadIdx.x & 63;
     const bool planned = pp.counts != nullptr;
-    uint32_t my_cnt = 0, my_start = 0, my_lg = 0, my_tiles = 0;
+    uint32_t my_cnt = 0, my_start = 0, my_lg = 0, my_tiles = 0, S = 1, simd = 0, ntiles = 0;
     uint64_t total, first, stride;
     if (planned) {
         my_cnt = lane < kClasses ? pp.sched[kSchedCnt + lane] : 0;
         my_start = lane < kClasses ? pp.sched[kSchedStart + lane] : 0;
         my_lg = lane < kClasses ? pp.sched[kSchedLg + lane] : 0;
         my_tiles = (uint32_t)((((uint64_t)my_cnt << my_lg) + 63) / 64);
-        // static round robin over the size-ordered tiles (longest first): a shared
-        // queue counter would serialise every wave on one atomic
-        total = pp.sched[2];
-        first = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
-        stride = gridDim.x * (blockDim.x / 64);
+        // static snake deal over the work-ordered tiles (heaviest first): rounds
+        // of S tiles, SIMD s takes tile s of even rounds and S-1-s of odd ones;
+        // wave slot w is SIMD w mod S in pass w / S (the grid is S x passes
+        // waves), and takes rounds pass, pass + passes, ...  A shared queue
+        // counter would serialise every wave on one atomic.
+        S = pp.simds ? pp.simds : 1;
+        const uint32_t slot = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+        simd = slot % S;
+        ntiles = pp.sched[2];
+        total = (ntiles + S - 1) / S; // rounds
+        first = slot / S;
+        stride = gridDim.x * (blockDim.x / 64) / S;
     } else { // lane units, grid-stride
         total = (uint64_t)n << lg0;
         first = blockIdx.x * 256 + threadIdx.x;
@@ -469,13 +476,13 @@ __device__ __forceinline__ void pipe_walk(uint32_t n, uint32_t lg0, const PipePl
         Unit o;
         list_pos = 0;
         if (planned) {
-            const uint32_t tile = (uint32_t)it;
+            const uint32_t tile = (uint32_t)it * S + ((it & 1u) ? S - 1 - simd : simd);
             const uint64_t hit = __ballot(lane < kClasses && my_start <= tile && tile < my_start + my_tiles);
             const uint32_t c = uniform_u32((uint32_t)(__ffsll((unsigned long long)hit) - 1));
             o.lg = uniform_u32((uint32_t)__shfl((int)my_lg, (int)c));
             const uint32_t u = (tile - uniform_u32((uint32_t)__shfl((int)my_start, (int)c))) * 64 + lane;
             const uint32_t p = u >> o.lg;
-            o.live = it < total && p < uniform_u32((uint32_t)__shfl((int)my_cnt, (int)c));
+            o.live = tile < ntiles && p < uniform_u32((uint32_t)__shfl((int)my_cnt, (int)c));
             o.j = u & ((1u << o.lg) - 1);
             list_pos = o.live ? c * pp.cap + p : 0;
             o.i = 0;
@@ -555,6 +562,8 @@ hipError_t launch_pipe(const SealArgs *sa, const OpenArgs *oa, const Launch &L, 
         const uint32_t wg = (uint32_t)(L.wg_per_cu > 0 ? L.wg_per_cu : 1);
         blocks = (uint32_t)(L.cus > 0 ? L.cus : 1) * wg;
         lds = (kLdsPerCu / wg) & ~255u; // sched[] was written by the planner (plan_kernel)
+        // the snake deal needs the grid to be whole passes of pp.simds waves
+        if (pp.simds == 0 || ((uint64_t)blocks * 4) % pp.simds != 0) return hipErrorInvalidValue;
     } else {
         pipe_grid((uint64_t)n << lg, L, blocks, lds);
     }
