@@ -107,8 +107,8 @@ hipError_t prepare_tile_kernels();
 // Pipelined lane kernel (rg_pipe.hip): one packet per lane, double-buffered
 // chunk loads, Poly1305 absorbed inside the next chunk's keystream rounds.
 // With a plan (planner lists, rg_tile.hip): the planner's last workgroup picks
-// segments per size class from the batch's mean work (schedule_classes), then
-// one wave per SIMD walks tiles of 64 lanes, largest class first, round robin
+// segments per size class by the estimated makespan (schedule_classes), then
+// the waves walk tiles of 64 lanes, heaviest first, in the schedule's snake deal
 // (sched[] holds the schedule; the planner zeroes its counts again).  Without
 // one: lane units in array order, grid-stride.
 constexpr uint32_t kSchedWords = 128;

@@ -237,7 +237,7 @@ def test_random_batches_vs_oracle(engine, mode, seed):
 
 @pytest.mark.parametrize("wg", [1, 2, 3])
 def test_planned_pipe_residency_vs_oracle(engine, wg):
-    """The planned pipelined path deals its size-ordered tiles round robin over CUs x wg_per_cu x 4
+    """The planned pipelined path deals its work-ordered tiles in snake order over CUs x wg_per_cu x 4
     waves (default 2 per CU): mixed sizes, invalid and skipped descriptors at 1, 2 and 3 resident
     workgroups per CU give the oracle's bytes and statuses."""
     _reset(engine)
