@@ -162,8 +162,8 @@ int rg_set_staged(rg_ctx *ctx, int kernel);
 int rg_get_kernel(rg_ctx *ctx, size_t n);
 /* A device-side planner can first sort the batch into size classes so that
  * every 64-lane tile holds packets of similar length (both kernel families;
- * the pipelined kernel then also picks segments per class from the batch's
- * mean work and deals tiles longest first).
+ * the pipelined kernel then also picks segments per class by an estimated
+ * makespan and deals tiles heaviest first, in snake order over the SIMDs).
  * 0 = off (tiles take packets in array order), 1 = always, 2 (default) =
  * auto: plan unless the last planned batch of this context held a single size
  * class (re-checked every 32nd call).  Results are identical in every mode.
