@@ -5,17 +5,24 @@ Metric (BASELINE.json): GiB/s + Mpkt/s device-resident ChaCha20-Poly1305
 seal/open at 1/2/4/8 MI355X.
 
 One step = one batch sealed (in place, header + tag framed) and then opened
-(tag verified, plaintext restored) -- BASELINE config 2 ("64 Ki packets x
-1500 B, one session key, seal then open") on every rank.  Multi-GPU is a
-plain index split with no data-path collective: every rank runs its own
-batch (weak scaling); RCCL is used only for the timing barrier and the
-max-over-ranks reduction.
+(tag verified, plaintext restored).  N = 1 runs BASELINE config 2 ("64 Ki
+packets x 1500 B, one session key, seal then open").  N > 1 runs BASELINE
+config 5 ("8 Mi packets x 1500 B, one session key, batch split evenly across
+the GPUs, no collective"): rank r seals and opens packets [r 8Mi/N,
+(r+1) 8Mi/N) with their global counters (strong scaling).  The split is a
+plain index range with no data-path collective; RCCL only carries the timing
+barrier and the max-over-ranks reduction.
 
 value = payload bytes through AEAD (seal + open, P bytes each) summed over
 ranks / max-over-ranks wall time of the timed steps, in GiB/s.
 
-Launch (N > 1):  python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
-    --master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W
+Launch: `python bench.py --gpus N` starts N ranks itself (a torch.distributed.run
+child process, before anything touches a GPU); the driver's own
+`python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N` is
+accepted too.  A WORLD_SIZE that disagrees with --gpus is an error (exit 2).
+
+`--workload cfg1` times BASELINE config 1 instead: one 1500-B packet sealed and
+opened on one CPU thread (ns/packet), plus the per-message GPU drop-in.
 """
 from __future__ import annotations
 
@@ -53,7 +60,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--workload", default="cfg2", choices=["cfg2", "cfg3", "cfg4", "cfg5"])
+    ap.add_argument("--workload", default=None, choices=["cfg1", "cfg2", "cfg3", "cfg4", "cfg5"],
+                    help="BASELINE config (default: cfg2 on one GPU, the cfg5 split on several)")
     ap.add_argument("--lanes", type=int, default=0, help="lanes per packet (0 = auto)")
     ap.add_argument("--wg-per-cu", type=int, default=0, help="resident workgroups per CU (0 = auto, -1 = plain grid)")
     ap.add_argument("--staged", type=int, default=-1,
@@ -62,9 +70,12 @@ def parse():
     ap.add_argument("--segments", type=int, default=0, help="segments per packet for the tile kernels (0 = auto)")
     ap.add_argument("--debug-mode", type=int, default=0, help="seal diagnostics (invalid output): 1 compute-only, 2 memory-only")
     ap.add_argument("--no-graph", action="store_true", help="launch eagerly instead of replaying a captured HIP graph")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget (0 = skip)")
-    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="CPU baseline budget: port and OpenSSL, 1 thread and all cores, 5 runs each (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="all-core thread count (0 = this host's share)")
     ap.add_argument("--e2e", action="store_true", help="also time the pinned host->GPU->host path")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch/validate the ranks, print each rank's plan as JSON and exit before any GPU work")
     ap.add_argument("--no-cold", dest="cold", action="store_false",
                     help="skip the cold-cache pass (profiling runs: keeps per-kernel averages to the step's regime)")
     ap.add_argument("--no-verify", dest="verify", action="store_false",
@@ -81,18 +92,36 @@ def kernel_label(args, eng, w) -> str:
     return f"lds-staged tiles, {k} chunks/window, planner {plan}, segments {args.segments or 'auto'}"
 
 
-def cpu_baseline(w, seconds: float, threads: int, impl: str = "port"):
-    """A CPU implementation timed on this host's cores over a bounded sample of the workload.
+def host_cpu_info() -> dict:
+    """What the CPU baselines ran on: model, the machine's logical CPUs and this process's share."""
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity": aff}
 
-    impl "port": the C RFC 8439 restatement in oracle/ (kind "port"; the
-    reference's own CPU path, Rust + graviola 0.2.0, cannot be built here: no
-    cargo, crate not vendored).  impl "openssl": OpenSSL EVP ChaCha20-Poly1305
-    (BASELINE.md CPU-B, an assembly-optimised stand-in for graviola).
-    """
+
+def all_core_threads(requested: int) -> int:
+    """The host's CPU share: on the GPU box nproc and the affinity mask show the whole machine while
+    the job's share is OMP_NUM_THREADS (16 per GPU); here it is the affinity mask."""
+    if requested:
+        return requested
+    aff = host_cpu_info()["affinity"]
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return max(1, min(aff, omp) if omp > 0 else aff)
+
+
+def cpu_rate(w, impl: str, threads: int, rep_seconds: float, reps: int = 5):
+    """Median of `reps` timed runs (after one warm-up run) of seal+open over a bounded sample of the
+    workload on `threads` host threads: GiB/s of payload and Mpkt/s."""
     from oracle import oracle  # checker / baseline only
 
-    if impl == "openssl" and not oracle.openssl_available():
-        return None
     seal = oracle.openssl_seal_batch if impl == "openssl" else oracle.seal_batch
     n = min(w.n, 4096)
     desc = w.desc[:n].copy()
@@ -105,28 +134,130 @@ def cpu_baseline(w, seconds: float, threads: int, impl: str = "port"):
     od["len"] += np.uint32(32)
     ctr = w.counters[:n]
     payload = int(desc["len"].astype(np.int64).sum())
-    reps, t0 = 0, time.perf_counter()
-    while True:
-        seal(w.keys, w.receivers, desc, ctr, buf, nthreads=threads)
-        if impl == "openssl":
-            st = oracle.openssl_open_batch(w.keys, od, buf, nthreads=threads)
-        else:
-            st, _ = oracle.open_batch(w.keys, od, buf, nthreads=threads)
-        reps += 1
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
-    assert (st == 0).all()
-    gib = 2 * payload * reps / el / 2**30
-    what = ("C RFC 8439 restatement (oracle/rg_oracle.c)" if impl == "port" else
-            f"{oracle.openssl_version()} EVP_chacha20_poly1305, re-keyed per packet (oracle/rg_openssl_batch.c)")
-    out = {"value": round(gib, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
-           "mpkt_s": round(2 * n * reps / el / 1e6, 4),
-           "sample": f"{n} packets of {w.name} (mean P={payload / n:.1f}) seal+open x{reps} in {el:.1f}s, "
-                     f"{threads} threads, {what}"}
-    if impl == "openssl":
-        out["kind"] = "openssl (stand-in for graviola)"
-    return out
+
+    def one(seconds):
+        reps_, t0 = 0, time.perf_counter()
+        while True:
+            seal(w.keys, w.receivers, desc, ctr, buf, nthreads=threads)
+            if impl == "openssl":
+                st = oracle.openssl_open_batch(w.keys, od, buf, nthreads=threads)
+            else:
+                st, _ = oracle.open_batch(w.keys, od, buf, nthreads=threads)
+            reps_ += 1
+            el = time.perf_counter() - t0
+            if el >= seconds:
+                break
+        assert (st == 0).all()
+        return 2 * payload * reps_ / el / 2**30, 2 * n * reps_ / el / 1e6
+
+    one(min(0.2, rep_seconds))
+    runs = [one(rep_seconds) for _ in range(reps)]
+    gib = sorted(r[0] for r in runs)[reps // 2]
+    mpkt = sorted(r[1] for r in runs)[reps // 2]
+    return {"value": round(gib, 4), "unit": "GiB/s", "cores": threads, "mpkt_s": round(mpkt, 4),
+            "runs_gib_s": [round(r[0], 4) for r in runs], "median_of": reps, "n_sample": n,
+            "mean_payload": round(payload / n, 1)}
+
+
+def cpu_baselines(w, seconds: float, threads: int):
+    """CPU baselines of BASELINE.md §2, in the same run as the GPU numbers: the C restatement
+    (kind "port": the reference's Rust + graviola 0.2.0 path cannot be built here -- no cargo, crate
+    not vendored) and OpenSSL EVP ChaCha20-Poly1305 (an assembly-optimised stand-in for graviola),
+    each on 1 thread and on the host's cores, median of 5 runs over a bounded sample."""
+    from oracle import oracle
+
+    info = host_cpu_info()
+    impls = ["port"] + (["openssl"] if oracle.openssl_available() else [])
+    rep = max(0.1, seconds / (len(impls) * 2 * 5))
+    out = {}
+    for impl in impls:
+        many = cpu_rate(w, impl, threads, rep)
+        one = cpu_rate(w, impl, 1, rep)
+        what = ("C RFC 8439 restatement (oracle/rg_oracle.c)" if impl == "port" else
+                f"{oracle.openssl_version()} EVP_chacha20_poly1305, re-keyed per packet (oracle/rg_openssl_batch.c)")
+        d = dict(many)
+        d["kind"] = "port" if impl == "port" else "openssl (stand-in for graviola)"
+        d["one_thread"] = {"value": one["value"], "unit": "GiB/s", "mpkt_s": one["mpkt_s"],
+                           "runs_gib_s": one["runs_gib_s"]}
+        d["sample"] = (f"first {many['n_sample']} packets of {w.name} (mean P={many['mean_payload']}) sealed then "
+                       f"opened, {rep:.2f} s per run, median of 5 runs on {threads} threads and on 1 thread; {what}")
+        d.update(info)
+        out[impl] = d
+    return out.get("port"), out.get("openssl")
+
+
+def bench_cfg1(args):
+    """BASELINE config 1: a single 1500-B transport packet (L = 1500, P = 1504) sealed then opened on
+    one CPU thread -- ns/packet for the C restatement and for OpenSSL -- plus the per-message GPU
+    drop-in (rg_chacha20poly1305_enc/_dec: H2D, kernel, D2H per call) for comparison."""
+    from oracle import oracle
+    from rustyguard_amd import workloads
+
+    w = workloads.build("cfg1")
+    key = w.keys[0].tobytes()
+    P = int(w.desc["len"][0])
+    iters = 20000
+    res = {}
+    for impl in ["port"] + (["openssl"] if oracle.openssl_available() else []):
+        oracle.time_one(impl, key, P, iters // 10)
+        runs = [oracle.time_one(impl, key, P, iters) for _ in range(5)]
+        seal_ns = sorted(r[0] for r in runs)[2]
+        open_ns = sorted(r[1] for r in runs)[2]
+        res[impl] = {"seal_ns": round(seal_ns, 1), "open_ns": round(open_ns, 1),
+                     "seal_open_ns": round(seal_ns + open_ns, 1), "median_of": 5, "iters": iters}
+    gpu = None
+    try:
+        import torch
+
+        if torch.cuda.is_available():
+            from rustyguard_amd.aead import Engine, nonce
+
+            eng = Engine(0)
+            pt = bytearray(np.random.default_rng(1).integers(0, 256, P, dtype=np.uint8).tobytes())
+            for _ in range(20):
+                t = eng.chacha20poly1305_enc(key, nonce(0), b"", pt)
+                eng.chacha20poly1305_dec(key, nonce(0), b"", pt, t)
+            ts, to = [], []
+            for i in range(200):
+                t0 = time.perf_counter()
+                t = eng.chacha20poly1305_enc(key, nonce(i), b"", pt)
+                t1 = time.perf_counter()
+                eng.chacha20poly1305_dec(key, nonce(i), b"", pt, t)
+                t2 = time.perf_counter()
+                ts.append(t1 - t0)
+                to.append(t2 - t1)
+            gpu = {"seal_us": round(float(np.median(ts)) * 1e6, 2), "open_us": round(float(np.median(to)) * 1e6, 2),
+                   "note": "per-message drop-in rg_chacha20poly1305_enc/_dec (host buffers: H2D + kernel + D2H + "
+                           "sync per call), median of 200"}
+            eng.close()
+    except Exception as e:  # the CPU measurement stands on its own
+        gpu = {"error": str(e)}
+    best = res.get("openssl", res["port"])
+    out = {"metric": "ns/packet, single 1500-B transport packet seal+open on one CPU thread (BASELINE config 1)",
+           "value": best["seal_open_ns"], "unit": "ns/packet", "n_gpus": 0, "higher_is_better": False,
+           "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+           "config": {"workload": f"cfg1: {workloads.CONFIGS['cfg1']}", "payload_bytes": P, "wire_bytes": P + 32},
+           "cpu": res, "gpu_per_message": gpu, **host_cpu_info(),
+           "note": "value = OpenSSL EVP (stand-in for graviola 0.2.0, which cannot be built here) when libcrypto is "
+                   "present, else the C restatement"}
+    print(json.dumps(out), flush=True)
+
+
+def launch_ranks(n: int) -> int:
+    """Start n ranks of this script under torch.distributed.run as a child process (nothing here has
+    touched a GPU yet) and return its exit code."""
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
 
 
 MALL_BYTES = 256 * 2**20  # MI355X Infinity Cache (memory-side, in front of HBM)
@@ -179,10 +310,28 @@ def load_traffic(workload: str):
 
 def main():
     args = parse()
+    if args.gpus < 1:
+        print("bench.py: --gpus must be >= 1", file=sys.stderr)
+        sys.exit(2)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1 and args.workload != "cfg1":
+        sys.exit(launch_ranks(args.gpus))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.workload != "cfg1" and world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a "
+              f"{world}-rank run as {args.gpus} GPUs", file=sys.stderr)
+        sys.exit(2)
+    if args.workload == "cfg1":
+        bench_cfg1(args)
+        return
+    workload = args.workload or ("cfg2" if world == 1 else "cfg5")
+    if args.dry_run:
+        line = json.dumps({"rank": int(os.environ.get("RANK", "0")), "world": world, "gpus": args.gpus,
+                           "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "workload": workload}) + "\n"
+        os.write(1, line.encode())  # one write: ranks sharing the pipe never interleave a line
+        return
     import torch
 
     rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dist = None
@@ -208,10 +357,10 @@ def main():
         eng.set_plan(args.plan)
     if args.segments:
         eng.set_segments(args.segments)
-    if args.workload == "cfg5":
-        w = workloads.build("cfg5", rank, world)
+    if workload == "cfg5":
+        w = workloads.build("cfg5", rank, world)  # strong split of the 8 Mi batch
     else:
-        w = workloads.build(args.workload)
+        w = workloads.build(workload)
     b = DeviceBatch(eng, w)
     b.fill()
     torch.cuda.synchronize()
@@ -302,7 +451,7 @@ def main():
     dominant = "seal" if seal_ms >= open_ms else "open"
     dom_ms, dom_alg = (seal_ms, seal_alg) if dominant == "seal" else (open_ms, open_alg)
     achieved = dom_alg / (dom_ms / 1e3) / 1e9
-    pmc = load_traffic(args.workload)
+    pmc = load_traffic(workload)
     traffic = None
     # only counters of the kernel family this run used (a kernel change makes them stale)
     if pmc and pmc.get(dominant) and pmc[dominant].get("family") == eng.kernel_for(w.n):
@@ -319,11 +468,14 @@ def main():
         "gpu_ms_per_step": round(step_ms, 5),
         "graph": graph is not None,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if workload == "cfg5" else "weak",
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic (SplitMix64 payload, fixed-seed keys; rustyguard_amd/workloads.py)",
-        "config": {"workload": f"{w.name}: {workloads.CONFIGS[w.name]}", "packets_per_gpu": w.n,
+        "config": {"workload": f"{w.name}: {workloads.CONFIGS[w.name]}" +
+                               (f" (strong split: {w.meta['total']} packets over {world} GPU(s), "
+                                f"{w.n} per GPU)" if workload == "cfg5" else ""),
+                   "packets_per_gpu": w.n,
                    "payload_bytes_per_packet": int(w.desc["len"][0]) if w.n else 0,
                    "mean_payload_bytes": round(payload / max(w.n, 1), 2), "wire_bytes_per_gpu": w.wire_bytes,
                    "sessions": int(w.meta.get("sessions", 1)), "parallelism": f"split{world} (no collective)",
@@ -356,9 +508,8 @@ def main():
     if args.e2e and rank == 0:
         out["e2e"] = e2e_host(eng, w, b)
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        thr = args.cpu_threads or min(16, os.cpu_count() or 1)
-        out["cpu_baseline"] = cpu_baseline(w, args.cpu_seconds, thr)
-        ossl = cpu_baseline(w, args.cpu_seconds / 2, thr, impl="openssl")
+        port, ossl = cpu_baselines(w, args.cpu_seconds, all_core_threads(args.cpu_threads))
+        out["cpu_baseline"] = port
         if ossl:
             out["cpu_openssl"] = ossl
     if rank == 0:

@@ -78,11 +78,13 @@ typedef enum rg_status {
 enum rg_pkt_status {
     RG_PKT_OK = 0,
     RG_PKT_DECRYPT_ERR = 1, /* Error::DecryptionError: tag mismatch / < 16 B after header */
-    RG_PKT_INVALID = 2,     /* Error::InvalidMessage: W % 16 != 0, W < 16, bad seal desc */
+    RG_PKT_INVALID = 2,     /* Error::InvalidMessage: W % 16 != 0, W < 16, message type
+                               not 1-4 (lib.rs:627), bad seal desc */
     RG_PKT_REJECTED = 3,    /* Error::Rejected: replayed/too old counter, no session,
                                REJECT_AFTER_MESSAGES reached, or RG_KEY_SKIP */
     RG_PKT_UNALIGNED = 4,   /* Error::Unaligned: frame not 16-byte aligned */
-    RG_PKT_NOT_DATA = 5,    /* type != MSG_DATA: route to the handshake path */
+    RG_PKT_NOT_DATA = 5,    /* type 1, 2 or 3 (handshake init/resp, cookie): route to the
+                               handshake path (lib.rs:622-624) */
 };
 
 /* ---------------------------------------------------------------- context */

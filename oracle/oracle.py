@@ -62,6 +62,8 @@ def lib():
         L.rg_openssl_seal_batch.restype = ctypes.c_int
         L.rg_openssl_open_batch.argtypes = [u8p, u8p, ctypes.c_size_t, u8p, u8p, ctypes.c_int]
         L.rg_openssl_open_batch.restype = ctypes.c_int
+        L.rg_cpu_time_one.argtypes = [ctypes.c_int, u8p, ctypes.c_uint32, ctypes.c_uint64, u8p]
+        L.rg_cpu_time_one.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -233,3 +235,13 @@ def openssl_open_batch(keys, desc, buf, nthreads=1):
     if rc != 0:
         raise RuntimeError("libcrypto.so.3 not available")
     return status[: len(desc)]
+
+
+def time_one(impl: str, key: bytes, P: int, iters: int) -> tuple[float, float]:
+    """BASELINE config 1 on one thread: mean ns of one seal and one open of a single P-byte
+    transport frame (impl "port": the C restatement, "openssl": EVP re-keyed per packet)."""
+    out = np.zeros(2, np.float64)
+    rc = lib().rg_cpu_time_one(1 if impl == "openssl" else 0, _ptr(_u8(key)), P, iters, _ptr(out))
+    if rc != 0:
+        raise RuntimeError(f"rg_cpu_time_one({impl}) failed: {rc}")
+    return float(out[0]), float(out[1])

@@ -6,7 +6,8 @@
  * graviola 0.2.0 AEAD (Cargo.lock:370-373), which cannot be built here.  Same
  * buffer contract as rg_oracle_seal_batch / rg_oracle_open_batch; like the
  * reference (rustyguard-crypto/src/prim.rs:186-200, ChaCha20Poly1305::new per
- * call) every packet re-keys the cipher context.
+ * call) every packet re-keys the cipher context (key setup only: the cipher
+ * object is fetched once per worker thread).
  */
 #define _GNU_SOURCE
 #include <dlfcn.h>
@@ -90,6 +91,10 @@ static void *worker(void *arg) {
     job_t *j = (job_t *)arg;
     EVP_CIPHER_CTX *c = ssl.ctx_new();
     uint8_t nonce[12];
+    /* the cipher is fetched and bound once per context; each packet then only re-keys it
+     * (EVP_CipherInit_ex with a NULL cipher), the equivalent of graviola's per-call
+     * ChaCha20Poly1305::new(key) key setup */
+    ssl.cipher_init(c, ssl.chacha(), NULL, NULL, NULL, j->open ? 0 : 1);
     for (size_t i = j->lo; i < j->hi; i++) {
         const rg_oracle_desc *d = &j->desc[i];
         uint8_t *frame = j->buf + d->offset;
@@ -98,7 +103,7 @@ static void *worker(void *arg) {
         if (!j->open) {
             const uint64_t ctr = j->counters[i];
             rg_oracle_wg_nonce(ctr, nonce);
-            ok &= ssl.cipher_init(c, ssl.chacha(), NULL, key, nonce, 1);
+            ok &= ssl.cipher_init(c, NULL, NULL, key, nonce, 1);
             ok &= ssl.cipher_update(c, frame + 16, &outl, frame + 16, (int)d->len);
             ok &= ssl.cipher_final(c, frame + 16 + d->len, &outl);
             ok &= ssl.ctrl(c, CTRL_AEAD_GET_TAG, 16, frame + 16 + d->len);
@@ -108,9 +113,13 @@ static void *worker(void *arg) {
                 put64(frame + 8, ctr);
             }
         } else {
+            if (d->len < 32) { /* no room for header + tag: prim.rs:427-429 */
+                if (j->status) j->status[i] = RG_ORACLE_DECRYPT_ERR;
+                continue;
+            }
             const uint32_t P = d->len - 32;
             rg_oracle_wg_nonce(get64(frame + 8), nonce);
-            ok &= ssl.cipher_init(c, ssl.chacha(), NULL, key, nonce, 0);
+            ok &= ssl.cipher_init(c, NULL, NULL, key, nonce, 0);
             ok &= ssl.ctrl(c, CTRL_AEAD_SET_TAG, 16, frame + 16 + P);
             ok &= ssl.cipher_update(c, frame + 16, &outl, frame + 16, (int)P);
             ok &= ssl.cipher_final(c, frame + 16 + P, &outl) > 0;
@@ -148,4 +157,67 @@ int rg_openssl_open_batch(const uint8_t *keys, const rg_oracle_desc *desc, size_
                           int nthreads) {
     job_t p = {1, keys, NULL, desc, NULL, buf, status, 0, 0};
     return run(p, n, nthreads);
+}
+
+/* ---- BASELINE config 1: one transport packet, one thread (bench.py --workload cfg1) ----
+ * Seals then opens one frame of payload P `iters` times (counter i for round i, so every seal is a
+ * fresh nonce, as EncryptionKey::encrypt would use it) and returns the mean wall-clock ns of one
+ * seal and of one open.  impl 0: the C restatement (rg_oracle_seal_one / _open_one); impl 1:
+ * OpenSSL EVP, re-keyed per packet like graviola's ChaCha20Poly1305::new per call. */
+#include <stdlib.h>
+#include <time.h>
+
+static double now_ns(void) {
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (double)t.tv_sec * 1e9 + (double)t.tv_nsec;
+}
+
+int rg_cpu_time_one(int impl, const uint8_t key[32], uint32_t P, uint64_t iters, double out_ns[2]) {
+    if (impl == 1 && !rg_openssl_available()) return -1;
+    uint8_t *frame = aligned_alloc(64, ((size_t)P + 32 + 63) & ~(size_t)63);
+    if (!frame) return -2;
+    for (uint32_t b = 0; b < P + 32; b++) frame[b] = (uint8_t)(b * 131u + 7u);
+    const uint32_t recv = 0x12345678u;
+    rg_oracle_desc ds = {0, P, 0}, dopen = {0, P + 32, 0};
+    EVP_CIPHER_CTX *c = NULL;
+    if (impl == 1) c = ssl.ctx_new();
+    uint8_t nonce[12], status = 0;
+    double t_seal = 0, t_open = 0;
+    int ok = 1, outl = 0;
+    for (uint64_t i = 0; i < iters; i++) {
+        double t0 = now_ns();
+        if (impl == 0) {
+            rg_oracle_seal_one(key, &recv, &ds, i, frame, &status);
+            ok &= status == RG_ORACLE_OK;
+        } else {
+            rg_oracle_wg_nonce(i, nonce);
+            ok &= ssl.cipher_init(c, i == 0 ? ssl.chacha() : NULL, NULL, key, nonce, 1);
+            ok &= ssl.cipher_update(c, frame + 16, &outl, frame + 16, (int)P);
+            ok &= ssl.cipher_final(c, frame + 16 + P, &outl);
+            ok &= ssl.ctrl(c, CTRL_AEAD_GET_TAG, 16, frame + 16 + P);
+            put32(frame, 4u);
+            put32(frame + 4, recv);
+            put64(frame + 8, i);
+        }
+        double t1 = now_ns();
+        if (impl == 0) {
+            rg_oracle_open_one(key, &dopen, frame, &status, NULL);
+            ok &= status == RG_ORACLE_OK;
+        } else {
+            rg_oracle_wg_nonce(get64(frame + 8), nonce);
+            ok &= ssl.cipher_init(c, NULL, NULL, key, nonce, 0);
+            ok &= ssl.ctrl(c, CTRL_AEAD_SET_TAG, 16, frame + 16 + P);
+            ok &= ssl.cipher_update(c, frame + 16, &outl, frame + 16, (int)P);
+            ok &= ssl.cipher_final(c, frame + 16 + P, &outl) > 0;
+        }
+        double t2 = now_ns();
+        t_seal += t1 - t0;
+        t_open += t2 - t1;
+    }
+    if (c) ssl.ctx_free(c);
+    free(frame);
+    out_ns[0] = t_seal / (double)(iters ? iters : 1);
+    out_ns[1] = t_open / (double)(iters ? iters : 1);
+    return ok ? 0 : -3;
 }

@@ -469,7 +469,10 @@ void rg_oracle_open_one(const uint8_t *keys, const rg_oracle_desc *d, uint8_t *b
     if (counter_out) *counter_out = 0;
     if ((d->offset & 15) != 0) { *status = RG_ORACLE_UNALIGNED; return; }      /* lib.rs:613-615 */
     if (w < 4) { *status = RG_ORACLE_INVALID; return; }                          /* lib.rs:619-620 */
-    if (ld32(frame) != 4u) { *status = RG_ORACLE_NOT_DATA; return; }             /* lib.rs:621-628 */
+    if (ld32(frame) != 4u) {                                                    /* lib.rs:621-628 */
+        *status = ld32(frame) - 1u < 3u ? RG_ORACLE_NOT_DATA : RG_ORACLE_INVALID; /* 1-3 handshake/cookie, else :627 */
+        return;
+    }
     if ((w & 15) != 0 || w < 16) { *status = RG_ORACLE_INVALID; return; }        /* types lib.rs:181-196 */
     uint64_t counter = ld64(frame + 8);
     if (counter_out) *counter_out = counter;
@@ -497,7 +500,10 @@ void rg_oracle_open_one_rx(const uint8_t *keys, const uint32_t *rx_rec, const ui
     if (key_out) *key_out = 0xFFFFFFFFu;
     if ((d->offset & 15) != 0) { *status = RG_ORACLE_UNALIGNED; return; }      /* lib.rs:613-615 */
     if (w < 4) { *status = RG_ORACLE_INVALID; return; }                          /* lib.rs:619-620 */
-    if (ld32(frame) != 4u) { *status = RG_ORACLE_NOT_DATA; return; }             /* lib.rs:621-628 */
+    if (ld32(frame) != 4u) {                                                    /* lib.rs:621-628 */
+        *status = ld32(frame) - 1u < 3u ? RG_ORACLE_NOT_DATA : RG_ORACLE_INVALID; /* 1-3 handshake/cookie, else :627 */
+        return;
+    }
     if ((w & 15) != 0 || w < 16) { *status = RG_ORACLE_INVALID; return; }        /* types lib.rs:181-196 */
     const uint32_t receiver = ld32(frame + 4);
     size_t s = 0;

@@ -945,7 +945,7 @@ int rg_recv_batch(rg_sessions *s, const rg_pkt_desc *desc, size_t n, uint8_t *bu
         else {
             uint32_t type, recv;
             memcpy(&type, buf + off, 4);
-            if (type != 4u) st = RG_PKT_NOT_DATA; // handshake/cookie: control plane
+            if (type != 4u) st = type - 1u < 3u ? RG_PKT_NOT_DATA : RG_PKT_INVALID; // 1-3: control plane; else lib.rs:627
             else if (w % 16 != 0 || w < 16) st = RG_PKT_INVALID; // message_mut_from
             else {
                 memcpy(&recv, buf + off + 4, 4);
@@ -967,15 +967,36 @@ int rg_recv_batch(rg_sessions *s, const rg_pkt_desc *desc, size_t n, uint8_t *bu
     int rc = rg_open_batch_host(s->ctx, s->keys.data(), 2 * s->cap, d.data(), n, buf, buf_len, status, nullptr);
     if (rc) return rc;
     // in-order post-pass (RFC 6479 §3.4.3: only authenticated counters advance the window)
+    std::vector<rg_pkt_desc> undo;
+    std::vector<uint64_t> undo_ctr;
     for (size_t i = 0; i < n; ++i) {
         if (host_status[i] != 0xFF) {
             status[i] = host_status[i];
         } else if (status[i] == RG_PKT_OK) {
             rg_antireplay *r = &s->s[slot_of[i]].replay;
-            if (rg_antireplay_would_accept(r, ctr[i])) rg_antireplay_mark_seen(r, ctr[i]);
-            else status[i] = RG_PKT_REJECTED; // duplicate inside this batch
+            if (rg_antireplay_would_accept(r, ctr[i])) {
+                rg_antireplay_mark_seen(r, ctr[i]);
+            } else {
+                // a second copy of a counter accepted earlier in this batch, or one the window
+                // has moved past since: the reference rejects it before decrypting
+                // (prim.rs:420-423), so the GPU's plaintext is put back to ciphertext
+                status[i] = RG_PKT_REJECTED;
+                undo.push_back(rg_pkt_desc{d[i].offset, d[i].len - 32, d[i].key_idx});
+                undo_ctr.push_back(ctr[i]);
+            }
         }
         if (slots_out) slots_out[i] = slot_of[i];
+    }
+    if (!undo.empty()) {
+        // Re-sealing the plaintext under the same key and nonce reproduces the ciphertext and,
+        // since the tag is the MAC of that ciphertext, the frame's own (verified) tag; without
+        // receivers the header is not rewritten.  The frame is byte-for-byte what arrived.
+        std::vector<uint8_t> st2(undo.size());
+        rc = rg_seal_batch_host(s->ctx, s->keys.data(), nullptr, 2 * s->cap, undo.data(), undo_ctr.data(),
+                                undo.size(), buf, buf_len, st2.data());
+        if (rc) return rc;
+        for (uint8_t x : st2)
+            if (x != RG_PKT_OK) return set_err(RG_EDEVICE, "recv_batch: restoring a replayed frame failed");
     }
     return RG_OK;
 }

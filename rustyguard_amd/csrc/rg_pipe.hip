@@ -366,7 +366,7 @@ __device__ __forceinline__ void pipe_open_packet(const OpenArgs &a, uint32_t i, 
     const Key8 key = load_key(a.keys, go ? d.key_idx : 0);
     uint64_t ctr = 0;
     if (desc_ok) {
-        if (hdr.x != 4u) st = RG_PKT_NOT_DATA;
+        if (hdr.x != 4u) st = hdr.x - 1u < 3u ? RG_PKT_NOT_DATA : RG_PKT_INVALID; // types 1-3 handshake/cookie, else lib.rs:627
         else if ((W & 15u) != 0 || W < 16) st = RG_PKT_INVALID;
         else {
             ctr = ((uint64_t)hdr.w << 32) | hdr.z;

@@ -345,7 +345,7 @@ __global__ __launch_bounds__(512) void tile_kernel(SealArgs sa, OpenArgs oa, Til
                     st = RG_PKT_INVALID;
                 if (st == 0xFF) {
                     const uint4 hdr = *reinterpret_cast<const uint4 *>(buf + d.offset);
-                    if (hdr.x != 4u) st = RG_PKT_NOT_DATA;                            // lib.rs:621-628
+                    if (hdr.x != 4u) st = hdr.x - 1u < 3u ? RG_PKT_NOT_DATA : RG_PKT_INVALID; // lib.rs:621-628
                     else if ((W & 15u) != 0 || W < 16) st = RG_PKT_INVALID;             // types/lib.rs:181-196
                     else {
                         ctr = ((uint64_t)hdr.w << 32) | hdr.z;

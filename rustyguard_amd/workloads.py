@@ -9,7 +9,8 @@ Generators (all from the stateless SplitMix64 finaliser ``mix64``):
   keys       key j = le64(mix64(KEY_SEED + 4 j + t)), t = 0..3
   receivers  session j's peer index = low 32 bits of mix64(RECV_SEED + j)
   payload    packet i inner bytes = le64(mix64(DATA_SEED + (i << 16) + word)),
-             zero padding up to P (device fill: rg_synth_fill_dev)
+             zero padding up to P (device fill: rg_synth_fill_dev); a cfg5 shard
+             [lo, hi) uses seed DATA_SEED + (lo << 16), i.e. the global indices
   IMIX       class of packet i = mix64(IMIX_SEED + i) % 12:
              0-6 -> L=64, 7-10 -> L=576, 11 -> L=1500  (7:4:1 in expectation)
   sessions   cfg4: perm = stable argsort(mix64(SESS_SEED + i)); packet i
@@ -147,6 +148,9 @@ def shard(total: int, rank: int, world: int, L: int = 1500, name: str = "cfg5") 
     lo = total * rank // world
     hi = total * (rank + 1) // world
     w = uniform(hi - lo, L, name=name, counter_base=lo, index_base=lo)
+    # payload of local packet k = that of global packet lo + k: the generator keys on
+    # seed + (index << 16), so the shard's seed is advanced by lo << 16 (wrapping)
+    w.data_seed = (DATA_SEED + (lo << 16)) % (1 << 64)
     w.meta.update({"total": total, "rank": rank, "world": world, "shard": [lo, hi]})
     return w
 

@@ -1,0 +1,43 @@
+"""bench.py's launch contract, checked on CPU (no GPU work: --dry-run stops before it).
+
+`python bench.py --gpus N` must start N ranks itself and report N (not silently one), a
+WORLD_SIZE that disagrees with --gpus must fail, and N > 1 defaults to BASELINE config 5's
+strong split.
+"""
+import json
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, env_extra=None, timeout=240):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(REPO, "bench.py")] + args, env=env, cwd=REPO,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+def test_gpus_n_launches_n_ranks():
+    r = _run(["--gpus", "2", "--dry-run"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert sorted(x["rank"] for x in lines) == [0, 1]
+    assert all(x["world"] == 2 and x["gpus"] == 2 and x["workload"] == "cfg5" for x in lines)
+    assert sorted(x["local_rank"] for x in lines) == [0, 1]
+
+
+def test_single_gpu_defaults_to_cfg2():
+    r = _run(["--dry-run"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    (line,) = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert line == {"rank": 0, "world": 1, "gpus": 1, "local_rank": 0, "workload": "cfg2"}
+
+
+def test_world_size_mismatch_is_an_error():
+    r = _run(["--gpus", "4", "--dry-run"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode == 2
+    assert "WORLD_SIZE=2" in r.stderr
+    r = _run(["--gpus", "1", "--dry-run"], {"WORLD_SIZE": "8", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode == 2

@@ -384,6 +384,12 @@ def test_open_malformed_statuses_match_oracle(engine, mode):
         (640, 32, 4, 0),      # empty payload + random tag -> DecryptionError
         (704, 48, 4, 0xFFFFFFFF),  # skipped by the host
         (4080, 48, 4, 0),     # runs past the arena
+        (768, 48, 0, 0),      # type 0 -> InvalidMessage (lib.rs:627)
+        (832, 48, 5, 0),      # type 5 -> InvalidMessage
+        (896, 48, 0xFF, 0),   # type 0xFF -> InvalidMessage
+        (960, 48, 2, 0),      # handshake response -> not data
+        (1024, 64, 3, 0),     # cookie reply -> not data
+        (1088, 48, 0x104, 0), # type word 0x104: the whole LE u32 is compared -> InvalidMessage
     ]
     desc = np.zeros(len(cases), DESC_DTYPE)
     for i, (o, w, t, k) in enumerate(cases):
@@ -391,11 +397,12 @@ def test_open_malformed_statuses_match_oracle(engine, mode):
         if o + 4 <= len(buf):
             buf[o:o + 4] = np.frombuffer(np.uint32(t).tobytes(), np.uint8)
             buf[o + 8:o + 16] = rng.integers(0, 256, 8, dtype=np.uint8)
-    want, wctr = oracle.open_batch(keys, desc[[0, 1, 2, 3, 4, 5, 6]], buf.copy())
+    checked = [0, 1, 2, 3, 4, 5, 6, 9, 10, 11, 12, 13, 14]
+    want, wctr = oracle.open_batch(keys, desc[checked], buf.copy())
     back, st, co = _gpu_open(engine, keys, desc, buf)
-    assert list(st[:7]) == list(want)
+    assert list(st[checked]) == list(want)
     assert st[7] == aead.PKT_REJECTED and st[8] == aead.PKT_INVALID
-    assert list(st) == [1, 2, 2, 1, 5, 4, 1, 3, 2]
+    assert list(st) == [1, 2, 2, 1, 5, 4, 1, 3, 2, 2, 2, 2, 5, 5, 2]
     _reset(engine)
 
 
@@ -476,6 +483,39 @@ def test_full_config_digest(engine, name):
         for d in w.desc[:: max(1, w.n // 500)]:
             o, p = int(d["offset"]), int(d["len"])
             assert np.array_equal(hb[o + 16:o + 16 + p], plain[o + 16:o + 16 + p])
+    _reset(engine)
+
+
+@pytest.mark.parametrize("rank", [0, 7])
+def test_cfg5_shard_digest(engine, rank):
+    """BASELINE config 5 as one rank of 8 runs it: 1 Mi x 1500-B packets, one key, counters and
+    payload bytes of global packets [rank * 1 Mi, (rank + 1) * 1 Mi) (workloads.shard), sealed and
+    opened on the GPU under the automatic kernel choice and the pipelined kernel, against the
+    oracle's SHA-256 digests (tests/golden/cfg5_digests.json)."""
+    from rustyguard_amd.device import DeviceBatch
+
+    g = load_golden("cfg5_digests.json")
+    dig = g[f"rank{rank}"]
+    w = workloads.build("cfg5", rank, g["world"])
+    assert w.n == dig["n"] and w.buf_bytes == dig["buf_bytes"] and int(w.counters[0]) == dig["first_counter"]
+    b = DeviceBatch(engine, w)
+    b.fill()
+    torch.cuda.synchronize()
+    assert hashlib.sha256(b.host_buf().tobytes()).hexdigest() == dig["plain_sha256"]
+    for staged in (-1, 0):
+        engine.set_staged(staged)
+        b.fill()
+        b.seal()
+        torch.cuda.synchronize()
+        assert (b.status[: w.n] == 0).all().item()
+        assert hashlib.sha256(b.host_buf().tobytes()).hexdigest() == dig["sealed_sha256"], staged
+        b.open()
+        torch.cuda.synchronize()
+        assert (b.status[: w.n] == 0).all().item()
+        assert torch.equal(b.counters_out[: w.n], b.counters)
+        assert hashlib.sha256(b.host_buf().tobytes()).hexdigest() == dig["opened_sha256"], staged
+    del b
+    torch.cuda.empty_cache()
     _reset(engine)
 
 

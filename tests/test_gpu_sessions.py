@@ -144,8 +144,10 @@ def test_roundtrip_duplicates_replays_and_forgeries(pair):
         if st[k] == aead.PKT_OK:
             src = int(desc[i]["offset"])
             assert np.array_equal(ob[o + 16:o + w - 16], plain[src + 16: src + 16 + int(desc[i]["len"])])
-        elif st[k] == aead.PKT_DECRYPT_ERR:
+        else:  # DecryptionError, or Rejected (in-batch duplicate): never left decrypted
+            assert st[k] in (aead.PKT_DECRYPT_ERR, aead.PKT_REJECTED)
             assert np.array_equal(ob[o:o + w], frames_before[o:o + w])  # untouched
+    assert (st == aead.PKT_REJECTED).sum() >= 2  # the duplicated 3 and 7 reach the post-pass
     # a forged copy did not burn its counter: the genuine frame is accepted later
     g = np.zeros(int(od[5]["len"]) + 16, np.uint8)
     g[:int(od[5]["len"])] = sealed[int(od[5]["offset"]): int(od[5]["offset"]) + int(od[5]["len"])]
@@ -186,9 +188,19 @@ def test_recv_dispatch_checks(pair):
     buf[384:388] = [4, 0, 0, 0]
     buf[388:392] = [0x22, 0x22, 0, 0]
     desc[4] = (384, 16, 0)
-    st, slots = b.recv_batch(desc, buf)
+    # unknown message types are Error::InvalidMessage (lib.rs:627); 1-3 go to the control plane
+    types = [0, 2, 3, 5, 0xFF, 0x104]
+    extra = np.zeros(len(types), DESC_DTYPE)
+    big = np.zeros(512 + 64 * len(types), np.uint8)
+    big[:512] = buf
+    for k, t in enumerate(types):
+        o = 512 + 64 * k
+        big[o:o + 4] = np.frombuffer(np.uint32(t).tobytes(), np.uint8)
+        extra[k] = (o, 48, 0)
+    st, slots = b.recv_batch(np.concatenate([desc, extra]), big)
     assert list(st) == [aead.PKT_REJECTED, aead.PKT_NOT_DATA, aead.PKT_UNALIGNED, aead.PKT_INVALID,
-                        aead.PKT_DECRYPT_ERR]
+                        aead.PKT_DECRYPT_ERR, aead.PKT_INVALID, aead.PKT_NOT_DATA, aead.PKT_NOT_DATA,
+                        aead.PKT_INVALID, aead.PKT_INVALID, aead.PKT_INVALID]
 
 
 def test_per_message_key_objects(engine):
@@ -210,3 +222,25 @@ def test_per_message_key_objects(engine):
     assert ek.counter() == 2
     with pytest.raises(aead.DecryptionError):
         dk.decrypt(5, bytearray(8))
+
+
+def test_window_shift_inside_a_batch_rejects_and_restores(pair):
+    """Packet j is accepted iff its tag verifies and would_accept(n_j) holds after packets 0..j-1
+    (AntiReplay, rustyguard-utils/src/anti_replay.rs:25-64): a high counter accepted first pushes a
+    low one out of the 1984-counter window.  The reference rejects that packet before decrypting
+    (prim.rs:420-423), so its frame must come back exactly as it arrived."""
+    a, b, sa, sb, sc, keys = pair
+    rng = np.random.default_rng(9)
+    desc, buf = _frames([64, 64], rng)
+    st, _ = a.send_batch([sa], desc[:1], buf)  # counter 0
+    a.set_send_counter(sa, 5000)
+    st2, _ = a.send_batch([sa], desc[1:], buf)  # counter 5000
+    assert (st == 0).all() and (st2 == 0).all()
+    od = desc.copy()
+    od["len"] += 32
+    rd = od[[1, 0]].copy()  # 5000 first, then 0 (5000 - 0 >= 1984: too old once 5000 is seen)
+    before = buf.copy()
+    st3, _ = b.recv_batch(rd, buf)
+    assert list(st3) == [aead.PKT_OK, aead.PKT_REJECTED]
+    o, w = int(od[0]["offset"]), int(od[0]["len"])
+    assert np.array_equal(buf[o:o + w], before[o:o + w])

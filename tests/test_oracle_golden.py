@@ -148,3 +148,21 @@ def test_blake2s_reference_snapshots_and_vectors():
     assert oracle.blake2s(bytes.fromhex(g["rfc7693_abc"]["msg"])).hex() == g["rfc7693_abc"]["hash"]
     for v in g["keyed_macs"]:
         assert oracle.blake2s(bytes.fromhex(v["msg"]), bytes.fromhex(v["key"]), 16).hex() == v["mac"]
+
+
+def test_message_type_dispatch():
+    """Sessions::recv_message (rustyguard-core/src/lib.rs:619-628): the little-endian u32 type word
+    selects handshake init / response / cookie (1, 2, 3: routed to the control plane, NOT_DATA) or
+    data (4); every other value is Error::InvalidMessage."""
+    import numpy as np
+
+    keys = np.zeros((1, 32), np.uint8)
+    types = [0, 1, 2, 3, 5, 0xFF, 0x104, 0xFFFFFFFF]
+    buf = np.zeros(64 * len(types), np.uint8)
+    desc = np.zeros(len(types), oracle.DESC_DTYPE)
+    for k, t in enumerate(types):
+        buf[64 * k:64 * k + 4] = np.frombuffer(np.uint32(t).tobytes(), np.uint8)
+        desc[k] = (64 * k, 48, 0)
+    st, _ = oracle.open_batch(keys, desc, buf)
+    I, N = oracle.INVALID, oracle.NOT_DATA
+    assert list(st) == [I, N, N, N, I, I, I, I]

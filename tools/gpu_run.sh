@@ -61,10 +61,11 @@ for s in "$@"; do
     bench) run bench 400 python bench.py --steps 50 --warmup 10 --cpu-seconds 10 ;;
     benchq) run bench 300 python bench.py --steps 30 --warmup 5 --cpu-seconds 0 ;;
     bench_all)
-        for w in cfg2 cfg3 cfg4 cfg5; do run bench_$w 300 python bench.py --workload $w --steps 30 --warmup 5 --cpu-seconds 0; done
+        for w in ${RG_WORKLOADS:-cfg2 cfg3 cfg4 cfg5}; do run bench_$w 300 python bench.py --workload $w --steps 30 --warmup 5 --cpu-seconds 0; done
         summ gpurun_out/bench_cfg*.log ;;
     e2e) run e2e 400 python bench.py --steps 10 --warmup 3 --cpu-seconds 0 --e2e ;;
     default) run bench_default 600 python bench.py ;;
+    cfg1) run bench_cfg1 300 python bench.py --workload cfg1 ;;
     prof)
         W=${RG_WORKLOAD:-cfg2}
         run prof_$W 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$W -o run -- \
@@ -76,6 +77,14 @@ for s in "$@"; do
             python3 bench.py --workload $W --steps 5 --warmup 2 --cpu-seconds 0 --no-cold
         run pmc_write_$W 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write_$W -o p -- \
             python3 bench.py --workload $W --steps 5 --warmup 2 --cpu-seconds 0 --no-cold ;;
+    valu)
+        # issue counters of the transport kernels (one pass: 8 SQ + 2 GRBM), per BASELINE config
+        for W in ${RG_WORKLOADS:-cfg2 cfg3 cfg4}; do
+            run valu_$W 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
+                SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_SALU GRBM_GUI_ACTIVE GRBM_COUNT \
+                --kernel-trace --output-format csv -d gpurun_out/valu_$W -o p -- \
+                python3 bench.py --workload $W --steps 5 --warmup 2 --cpu-seconds 0 --no-cold
+        done ;;
     variants) each_variant bench_variant; summ gpurun_out/var_*.log ;;
     stamps_v) each_variant stamp_variant ;;
     pmc_clock) each_variant pmc_variant; python3 tools/pmc_clock.py gpurun_out/pmcclk_* ;;
