@@ -14,7 +14,7 @@ REPO = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIBDIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIBDIR, "librg_aead.so")
-SOURCES = ["rg_kernels.hip", "rg_tile.hip", "rg_pipe.hip", "rg_mac.hip", "rg_api.cpp"]
+SOURCES = ["rg_kernels.hip", "rg_tile.hip", "rg_pipe.hip", "rg_flat.hip", "rg_mac.hip", "rg_api.cpp"]
 HEADERS = ["rg_device.h", "rg_internal.h"]
 ARCH = os.environ.get("RG_OFFLOAD_ARCH", "gfx950")
 

@@ -74,7 +74,8 @@ def _gpu_open(engine, keys, desc_open, buf):
 # packet (0 = automatic)
 MODES = [("auto",), ("pipe", 0), ("pipe", 1), ("pipe", 2), ("pipe", 4),
          ("tile", 2, 2, 0), ("tile", 2, 1, 0), ("tile", 1, 1, 1), ("tile", 2, 1, 2), ("tile", 2, 1, 4),
-         ("tile", 2, 0, 1), ("tile", 2, 0, 2), ("tile", 1, 0, 4), ("tile", 1, 1, 0)]
+         ("tile", 2, 0, 1), ("tile", 2, 0, 2), ("tile", 1, 0, 4), ("tile", 1, 1, 0),
+         ("flat", 1), ("flat", 0), ("flat", 2)]
 
 
 def _configure(engine, mode):
@@ -89,6 +90,9 @@ def _configure(engine, mode):
         engine.set_staged(g)
         engine.set_plan(plan)
         engine.set_segments(k)
+    elif mode[0] == "flat":  # ("flat", plan): flattened chunk stream, units planned / by count / auto
+        engine.set_staged(3)
+        engine.set_plan(mode[1])
 
 
 def _reset(engine):
@@ -104,6 +108,8 @@ def _mode_id(m):
         return "auto"
     if m[0] == "pipe":
         return f"pipe{m[1]}" if m[1] else "pipe_plan"
+    if m[0] == "flat":
+        return f"flat_p{m[1]}"
     return f"tile_g{m[1]}_p{m[2]}_k{m[3]}"
 
 
@@ -335,6 +341,42 @@ def test_large_payload_mix_vs_oracle(engine, mode):
     o, w = int(od[j]["offset"]), int(od[j]["len"])
     assert np.array_equal(back[o:o + w], tampered[o:o + w])
     for i in np.nonzero(ok)[0][::7]:
+        o, p = int(desc[i]["offset"]), int(desc[i]["len"])
+        assert np.array_equal(back[o + 16: o + 16 + p], buf[o + 16: o + 16 + p])
+    _reset(engine)
+
+
+@pytest.mark.parametrize("plan", [0, 1])
+def test_flat_subunits_vs_oracle(engine, plan):
+    """The flattened kernel stages at most kFlatMaxPk (256) packets of a unit in LDS at a time:
+    400 Ki small packets (keepalives P = 0 and 16/64-byte payloads) put ~400 packets in each of
+    the 1024 units, so every wave runs several sub-units; forged frames in the middle of them."""
+    engine.set_staged(3)
+    engine.set_plan(plan)
+    rng = np.random.default_rng(77)
+    n = 400 * 1024
+    sizes = rng.choice(np.array([0, 16, 64, 128]), n, p=[0.4, 0.3, 0.2, 0.1])
+    keys, rec, desc, ctr, buf = _random_batch(rng, n, nkeys=4, sizes=sizes, stride=160)
+    want = buf.copy()
+    oracle.seal_batch(keys, rec, desc, ctr, want, nthreads=8)
+    got, st = _gpu_seal(engine, keys, rec, desc, ctr, buf)
+    assert (st == aead.PKT_OK).all()
+    assert np.array_equal(got, want)
+    od = desc.copy()
+    od["len"] += 32
+    forged = rng.choice(n, 50, replace=False)
+    tampered = got.copy()
+    for i in forged:
+        tampered[int(od[i]["offset"]) + int(od[i]["len"]) - 1] ^= 1
+    back, st, co = _gpu_open(engine, keys, od, tampered)
+    bad = np.zeros(n, bool)
+    bad[forged] = True
+    assert (st[~bad] == aead.PKT_OK).all() and (st[bad] == aead.PKT_DECRYPT_ERR).all()
+    assert np.array_equal(co, ctr)
+    for i in forged:
+        o, w = int(od[i]["offset"]), int(od[i]["len"])
+        assert np.array_equal(back[o:o + w], tampered[o:o + w])
+    for i in np.nonzero(~bad)[0][::97]:
         o, p = int(desc[i]["offset"]), int(desc[i]["len"])
         assert np.array_equal(back[o + 16: o + 16 + p], buf[o + 16: o + 16 + p])
     _reset(engine)

@@ -58,11 +58,12 @@ for s in "$@"; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     test) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
     testall) run pytest_gpu 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread ;;
+    ktest) run pytest_k 900 python -u -m pytest tests -m gpu -x -v -k "${PYTEST_K}" --timeout 180 --timeout-method thread ;;
     bench) run bench 400 python bench.py --steps 50 --warmup 10 --cpu-seconds 10 ;;
     benchq) run bench 300 python bench.py --steps 30 --warmup 5 --cpu-seconds 0 ;;
     bench_all)
         for w in ${RG_WORKLOADS:-cfg2 cfg3 cfg4 cfg5}; do run bench_$w 300 python bench.py --workload $w --steps 30 --warmup 5 --cpu-seconds 0; done
-        summ gpurun_out/bench_cfg*.log ;;
+        summ gpurun_out/bench_cfg[2-5].log ;;
     e2e) run e2e 400 python bench.py --steps 10 --warmup 3 --cpu-seconds 0 --e2e ;;
     default) run bench_default 600 python bench.py ;;
     cfg1) run bench_cfg1 300 python bench.py --workload cfg1 ;;
