@@ -88,23 +88,6 @@ struct PlanBuf {
     volatile uint32_t *h_classes = nullptr;
     uint32_t *d_classes = nullptr;
     uint64_t calls = 0;
-    // flattened-kernel planner (rg_flat.hip): per-group prefix sums, group totals, finish ticket
-    DevBuf flat_incl, flat_grp, flat_prefix, flat_ticket;
-    uint32_t flat_G = 0;
-    hipError_t reserve_flat(size_t n) {
-        const uint32_t G = (uint32_t)((n + rg::kFlatGroup - 1) / rg::kFlatGroup);
-        if (!flat_ticket.p) {
-            hipError_t e = flat_ticket.reserve(64);
-            if (e == hipSuccess) e = hipMemset(flat_ticket.p, 0, 64);
-            if (e != hipSuccess) return e;
-        }
-        if (G <= flat_G) return hipSuccess;
-        hipError_t e = flat_incl.reserve((size_t)G * rg::kFlatGroup * 4);
-        if (e == hipSuccess) e = flat_grp.reserve((size_t)G * 12);
-        if (e == hipSuccess) e = flat_prefix.reserve(((size_t)G + 1) * 8);
-        if (e == hipSuccess) flat_G = G;
-        return e;
-    }
     hipError_t reserve(size_t n) {
         if (!counts.p) { // counters + done count; the tile kernels leave them zeroed
             hipError_t e = counts.reserve((rg::kClasses + 1) * sizeof(uint32_t));
@@ -137,11 +120,6 @@ struct PlanBuf {
         counts.release();
         lists.release();
         sched.release();
-        flat_incl.release();
-        flat_grp.release();
-        flat_prefix.release();
-        flat_ticket.release();
-        flat_G = 0;
         cap = 0;
         if (h_classes) (void)hipHostFree(const_cast<uint32_t *>(h_classes));
         h_classes = nullptr;
@@ -419,27 +397,12 @@ static hipError_t launch_pipe_any(rg_ctx *ctx, const rg::SealArgs *sa, const rg:
     return rg::launch_pipe(sa, oa, Lp, &pp, st);
 }
 
-// Flattened chunk-stream kernel: planned (units of equal work) or, for a batch
-// whose packets all have the same work, units of equal packet count.
-static hipError_t launch_flat_any(rg_ctx *ctx, const rg::SealArgs *sa, const rg::OpenArgs *oa, PlanBuf &pb,
-                                  hipStream_t st) {
-    const uint32_t n = sa ? sa->n : oa->n;
+// Flattened chunk-stream kernel: units of equal work (planner on / auto) or of
+// equal packet counts (planner off); the balancing runs inside the kernel.
+static hipError_t launch_flat_any(rg_ctx *ctx, const rg::SealArgs *sa, const rg::OpenArgs *oa, hipStream_t st) {
     hipError_t e = ctx->d_junk.reserve(rg::flat_junk_bytes(ctx->cus));
     if (e != hipSuccess) return e;
-    e = pb.reserve(0); // host-mapped class report
-    if (e != hipSuccess) return e;
-    bool plan = ctx->plan == 1 || (ctx->plan == 2 && pb.want_plan());
-    if (!plan) return rg::launch_flat(sa, oa, nullptr, static_cast<uint4 *>(ctx->d_junk.p), ctx->cus, st);
-    e = pb.reserve_flat(n);
-    if (e != hipSuccess) return e;
-    rg::FlatPlan fp{};
-    fp.local_incl = static_cast<uint32_t *>(pb.flat_incl.p);
-    fp.grp_sum = static_cast<uint32_t *>(pb.flat_grp.p);
-    fp.grp_prefix = static_cast<uint64_t *>(pb.flat_prefix.p);
-    fp.ticket = static_cast<uint32_t *>(pb.flat_ticket.p);
-    fp.classes_out = pb.d_classes;
-    fp.G = (uint32_t)((n + rg::kFlatGroup - 1) / rg::kFlatGroup);
-    return rg::launch_flat(sa, oa, &fp, static_cast<uint4 *>(ctx->d_junk.p), ctx->cus, st);
+    return rg::launch_flat(sa, oa, ctx->plan != 0, static_cast<uint4 *>(ctx->d_junk.p), ctx->cus, st);
 }
 
 static hipError_t launch_seal_any(rg_ctx *ctx, const rg::SealArgs &a0, PlanBuf &pb, hipStream_t st) {
@@ -447,7 +410,7 @@ static hipError_t launch_seal_any(rg_ctx *ctx, const rg::SealArgs &a0, PlanBuf &
     const rg::Launch L = launch_cfg(ctx, a.n, false);
     // stamps: debug mode 3, or any diagnostic mode of the pipelined kernel
     a.dbg = L.debug_mode == 3 || (L.staged_g == 0 && L.debug_mode != 0) ? ctx->dbg : nullptr;
-    if (L.staged_g == 3) return launch_flat_any(ctx, &a, nullptr, pb, st);
+    if (L.staged_g == 3) return launch_flat_any(ctx, &a, nullptr, st);
     if (L.staged_g == 0) return launch_pipe_any(ctx, &a, nullptr, pb, L, st);
     return launch_tiles_any(ctx, &a, nullptr, pb, L, st);
 }
@@ -456,7 +419,7 @@ static hipError_t launch_open_any(rg_ctx *ctx, const rg::OpenArgs &a0, PlanBuf &
     rg::OpenArgs a = a0;
     const rg::Launch L = launch_cfg(ctx, a.n, true);
     a.dbg = L.debug_mode == 3 ? ctx->dbg : nullptr;
-    if (L.staged_g == 3) return launch_flat_any(ctx, nullptr, &a, pb, st);
+    if (L.staged_g == 3) return launch_flat_any(ctx, nullptr, &a, st);
     if (L.staged_g == 0) return launch_pipe_any(ctx, nullptr, &a, pb, L, st);
     return launch_tiles_any(ctx, nullptr, &a, pb, L, st);
 }

@@ -223,23 +223,12 @@ struct PipePlan {
 hipError_t launch_pipe(const SealArgs *sa, const OpenArgs *oa, const Launch &L, const PipePlan *plan,
                        hipStream_t s);
 
-// Flattened chunk-stream kernel (rg_flat.hip, kernel family 3).  The planner
-// writes, per group of kFlatGroup packets, the inclusive prefix of each
-// packet's work (1 + 64-byte chunks) and the group totals; its last workgroup
-// scans the totals into grp_prefix[0..G] and reports through classes_out
-// whether all packets had the same work (1) or not (2).  Without a plan
-// (grp_prefix == nullptr) the units are equal packet counts.
+// Flattened chunk-stream kernel (rg_flat.hip, kernel family 3): units of
+// whole packets, one per wave, cut inside groups of kFlatGroup packets at equal
+// work (balance) or equal packet counts; the chunks of a unit are dealt evenly
+// over the wave's 64 lanes.
 constexpr uint32_t kFlatGroup = 1024;
-struct FlatPlan {
-    uint32_t *local_incl;  // [G * kFlatGroup]
-    uint32_t *grp_sum;     // [3 G]: totals, minimum and maximum work per group
-    uint64_t *grp_prefix;  // [G + 1]
-    uint32_t *ticket;      // finished-workgroup count, zero between launches
-    uint32_t *classes_out; // host-mapped (or nullptr)
-    uint32_t G;
-};
-hipError_t launch_flat(const SealArgs *sa, const OpenArgs *oa, const FlatPlan *fp, uint4 *junk, int cus,
-                       hipStream_t s);
+hipError_t launch_flat(const SealArgs *sa, const OpenArgs *oa, bool balance, uint4 *junk, int cus, hipStream_t s);
 uint32_t flat_junk_bytes(int cus);
 hipError_t prepare_flat_kernels();
 hipError_t prepare_pipe_kernels(int max_wg[2]); // [seal, open] resident 256-thread workgroups per CU

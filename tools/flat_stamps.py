@@ -1,0 +1,65 @@
+#!/usr/bin/env python3
+"""Phase times of the flattened kernel (rg_flat.hip, debug mode 3): per wave s_memtime at the end of
+unit search, descriptor staging + chunk scan, phase A (one-time keys), phase C (chunk stream),
+carries, phase F (tags) of its first sub-unit, and the wave's end.  Prints mean / max cycles per
+phase over the waves, for seal and open."""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from rustyguard_amd import workloads  # noqa: E402
+from rustyguard_amd.aead import Engine  # noqa: E402
+from rustyguard_amd.device import DeviceBatch  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--workload", default="cfg3")
+ap.add_argument("--plan", type=int, default=1)
+args = ap.parse_args()
+eng = Engine(0)
+eng.set_staged(3)
+eng.set_plan(args.plan)
+w = workloads.build(args.workload)
+b = DeviceBatch(eng, w)
+b.fill()
+dbg = torch.zeros(8 * 1024 * 2, dtype=torch.int64, device="cuda")
+eng.set_debug_buffer(dbg)
+names = ["search", "stage+scan", "phaseA", "phaseC", "carry", "phaseF", "end"]
+res = {}
+for op in ("seal", "open"):
+    for rep in range(3):
+        eng.set_debug_mode(0)
+        if op == "open":
+            b.seal()
+        torch.cuda.synchronize()
+        dbg.zero_()
+        eng.set_debug_mode(3)
+        b.seal() if op == "seal" else b.open()
+        torch.cuda.synchronize()
+        eng.set_debug_mode(0)
+        if op == "seal":
+            b.open()
+        torch.cuda.synchronize()
+    d = dbg.cpu().numpy().reshape(-1, 8).astype(np.int64)
+    d = d[d[:, 0] != 0]
+    t0 = d[:, 0:1]
+    rel = d - t0
+    rel[d == 0] = -1
+    out = {"waves": int(len(d))}
+    prev = np.zeros(len(d), np.int64)
+    for i, nm in enumerate(names, start=1):
+        col = rel[:, i]
+        ok = col >= 0
+        seg = np.where(ok, col - prev, 0)
+        out[nm] = {"mean_cyc": int(seg[ok].mean()) if ok.any() else None, "max_cyc": int(seg[ok].max()) if ok.any() else None}
+        prev = np.where(ok, col, prev)
+    out["wave_total"] = {"mean_cyc": int(rel[:, 7].mean()), "max_cyc": int(rel[:, 7].max())}
+    start = d[:, 0] - d[:, 0].min()
+    out["start_spread_cyc"] = int(start.max())
+    res[op] = out
+    print(op, json.dumps(out), flush=True)

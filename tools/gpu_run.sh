@@ -81,10 +81,10 @@ for s in "$@"; do
     valu)
         # issue counters of the transport kernels (one pass: 8 SQ + 2 GRBM), per BASELINE config
         for W in ${RG_WORKLOADS:-cfg2 cfg3 cfg4}; do
-            run valu_$W 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
+            run valu_$W 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_INSTS_LDS \
                 SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_SALU GRBM_GUI_ACTIVE GRBM_COUNT \
                 --kernel-trace --output-format csv -d gpurun_out/valu_$W -o p -- \
-                python3 bench.py --workload $W --steps 5 --warmup 2 --cpu-seconds 0 --no-cold
+                python3 bench.py --workload $W --steps 5 --warmup 2 --cpu-seconds 0 --no-cold ${RG_BENCH_FLAGS:-}
         done ;;
     variants) each_variant bench_variant; summ gpurun_out/var_*.log ;;
     stamps_v) each_variant stamp_variant ;;

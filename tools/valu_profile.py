@@ -46,6 +46,7 @@ def summarise(d):
                   "clock_ghz": round(grbm / 8 / us / 1e3, 3) if us else None,
                   "waves": int(waves), "valu_insts_per_wave": round(m.get("SQ_INSTS_VALU", 0) / waves, 1),
                   "salu_insts_per_wave": round(m.get("SQ_INSTS_SALU", 0) / waves, 1),
+                  "lds_insts_per_wave": round(m.get("SQ_INSTS_LDS", 0) / waves, 1),
                   "valu_active": round(m.get("SQ_ACTIVE_INST_VALU", 0) / wc, 4),
                   "wait_any": round(m.get("SQ_WAIT_ANY", 0) / wc, 4),
                   "wait_inst_any": round(m.get("SQ_WAIT_INST_ANY", 0) / wc, 4),
