@@ -784,3 +784,61 @@ def test_mac_verify_reference_snapshot(engine):
     engine.mac_verify_dev(_dev(keys), 1, _dev(desc.view(np.uint8).reshape(-1, 16)), _dev(buf), st, ko)
     torch.cuda.synchronize()
     assert list(st.cpu().numpy()) == [0, aead.PKT_REJECTED] and ko.cpu().numpy()[0] == 1
+
+
+def test_mac1_on_reference_handshake_messages(engine):
+    """The reference's recorded handshake initiation (148 B) and response (92 B) from its test
+    `snapshot` (rustyguard-core/src/snapshots/rustyguard_core__tests__snapshot{,-2}.snap) pass
+    HasMac::verify_mac1 (rustyguard-crypto/src/lib.rs:142-148) on the GPU under their receivers'
+    mac1 keys (re-derived by tests/golden/make_handshake.py), are found by the wg-proxy peer scan
+    among decoy keys, and fail with any bit of the covered bytes or of the mac1 field flipped."""
+    g = load_golden("handshake_vectors.json")["handshake_macs"]
+    msgs = [bytes.fromhex(g["initiation"]), bytes.fromhex(g["response"])]
+    real = [bytes.fromhex(g["initiation_mac1_key"]), bytes.fromhex(g["response_mac1_key"])]
+    rng = np.random.default_rng(8)
+    keys = np.stack([rng.integers(0, 256, 32, dtype=np.uint8) for _ in range(6)])
+    keys[2] = np.frombuffer(real[0], np.uint8)
+    keys[5] = np.frombuffer(real[1], np.uint8)
+    frames, desc_rows = [], []
+    off = 0
+    for mi, msg in enumerate(msgs):
+        for variant in ("ok", "scan", "body", "mac"):
+            b = bytearray(msg)
+            if variant == "body":
+                b[5] ^= 0x01  # sender index byte, covered by mac1
+            if variant == "mac":
+                b[len(b) - 32] ^= 0x80  # first byte of the mac1 field
+            frames.append((off, bytes(b)))
+            key = aead.KEY_SCAN if variant == "scan" else (2 if mi == 0 else 5)
+            desc_rows.append((off, len(b), key))
+            off += (len(b) + 15) // 16 * 16
+    buf = np.zeros(off, np.uint8)
+    for o, b in frames:
+        buf[o:o + len(b)] = np.frombuffer(b, np.uint8)
+    desc = np.array(desc_rows, DESC_DTYPE)
+    st = torch.zeros(len(desc), dtype=torch.uint8, device="cuda")
+    ko = torch.zeros(len(desc), dtype=torch.int32, device="cuda")
+    engine.mac_verify_dev(_dev(keys), 1, _dev(desc.view(np.uint8).reshape(-1, 16)), _dev(buf), st, ko)
+    torch.cuda.synchronize()
+    R = aead.PKT_REJECTED
+    assert list(st.cpu().numpy()) == [0, 0, R, R, 0, 0, R, R]
+    k = ko.cpu().numpy()
+    assert k[1] == 2 and k[5] == 5  # the scan names the receiver's key
+
+
+def test_aead_with_aad_reference_handshake_snapshot(engine):
+    """The per-message drop-in with a non-empty AAD against the reference's own bytes: resp.empty of
+    its test `handshake` (rustyguard-crypto/src/snapshots/rustyguard_crypto__tests__handshake-3.snap)
+    is ChaCha20-Poly1305(K, nonce 0, AAD = the transcript hash, empty payload); K and the hash are
+    re-derived by tests/golden/make_handshake.py (which also reproduces the snapshot's transport
+    keys).  Opening accepts it; a flipped AAD bit is a DecryptionError."""
+    v = load_golden("handshake_vectors.json")["aead_with_aad"]
+    key, nonce, aad = bytes.fromhex(v["key"]), bytes.fromhex(v["nonce"]), bytes.fromhex(v["aad"])
+    empty = bytearray()
+    tag = engine.chacha20poly1305_enc(key, nonce, aad, empty)
+    assert tag.hex() == v["tag"]
+    engine.chacha20poly1305_dec(key, nonce, aad, bytearray(), tag)
+    bad = bytearray(aad)
+    bad[31] ^= 1
+    with pytest.raises(aead.DecryptionError):
+        engine.chacha20poly1305_dec(key, nonce, bytes(bad), bytearray(), tag)

@@ -166,3 +166,17 @@ def test_message_type_dispatch():
     st, _ = oracle.open_batch(keys, desc, buf)
     I, N = oracle.INVALID, oracle.NOT_DATA
     assert list(st) == [I, N, N, N, I, I, I, I]
+
+
+def test_reference_handshake_vectors():
+    """tests/golden/handshake_vectors.json (made by make_handshake.py from the reference's own
+    snapshots): the oracle reproduces resp.empty (AEAD with a 32-byte AAD, handshake-3.snap) and
+    BLAKE2s-128 reproduces the mac1 fields of the recorded initiation and response."""
+    g = load_golden("handshake_vectors.json")
+    v = g["aead_with_aad"]
+    ct, tag = oracle.aead_seal(bytes.fromhex(v["key"]), bytes.fromhex(v["nonce"]), bytes.fromhex(v["aad"]), b"")
+    assert ct == b"" and tag.hex() == v["tag"]
+    m = g["handshake_macs"]
+    init, resp = bytes.fromhex(m["initiation"]), bytes.fromhex(m["response"])
+    assert oracle.blake2s(init[:116], bytes.fromhex(m["initiation_mac1_key"]), 16) == init[116:132]
+    assert oracle.blake2s(resp[:60], bytes.fromhex(m["response_mac1_key"]), 16) == resp[60:76]
