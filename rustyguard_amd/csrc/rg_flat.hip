@@ -137,7 +137,26 @@ struct FLane {
     Acc h;
     FChunk pi;           // seal: ciphertext chunk waiting to be absorbed (one step behind)
     uint32_t pi_cnt, pk; // its blocks and packet
+    // r^e for the carry of the lane's last piece (e = data blocks of that packet after the lane),
+    // square-and-multiply from bit pb down, one bit in each of two free slots of a step's rounds
+    Acc px;
+    Mul pr;
+    uint32_t pe;
+    int pb;
 };
+
+// one square-and-multiply step of the carry power (pb is wave-uniform)
+__device__ __forceinline__ void pow_step(FLane &s) {
+    if (s.pb < 0) return;
+    Acc sq = s.px;
+    acc_mul_gen(sq, make_gen(s.px));
+    Acc xr = sq;
+    acc_mul(xr, s.pr);
+    const bool bit = (s.pe >> s.pb) & 1u;
+    s.px.h0 = bit ? xr.h0 : sq.h0; s.px.h1 = bit ? xr.h1 : sq.h1; s.px.h2 = bit ? xr.h2 : sq.h2;
+    s.px.h3 = bit ? xr.h3 : sq.h3; s.px.h4 = bit ? xr.h4 : sq.h4;
+    --s.pb;
+}
 
 __device__ __forceinline__ void put_h(FlatLds &L, uint32_t k, const Acc &h, uint32_t lane) {
     uint4 *o = reinterpret_cast<uint4 *>(L.hs[k]);
@@ -169,6 +188,10 @@ __device__ __forceinline__ void flat_step(FLane &s, FChunk &b, uint32_t j, FlatL
             if (dr == 7) acc_block_pred(s.h, s.pi.q3, s.r, s.pi_cnt > 3);
         }
         if (dr % 2 == 1) pin_acc(s.h);
+        if (dr == 2 || dr == 6) {
+            pow_step(s);
+            pin_acc(s.px);
+        }
     });
     const FChunk x = {xor4(b.q0, ks + 0), xor4(b.q1, ks + 4), xor4(b.q2, ks + 8), xor4(b.q3, ks + 12)};
     uint4 *dst = const_cast<uint4 *>(s.cur.pl) + 4 * s.cur.t;
@@ -306,44 +329,43 @@ template <bool OPEN> __global__ __launch_bounds__(256) void flat_kernel(FlatArgs
             const uint32_t f1 = (uint32_t)min((uint64_t)NU, (((uint64_t)g + 1) * kFlatGroup * NU + n - 1) / n);
             const uint32_t kg = f1 - f0, j = u - f0;
             const uint32_t gb = g * kFlatGroup, gn = min(kFlatGroup, n - gb);
+            // coalesced: lane l holds packets l + 64 q of the group (q = 0..15)
             rg_pkt_desc d[16];
-            uint32_t w[16], run = 0;
+            uint32_t w[16];
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
-                const uint32_t i = 16 * lane + q;
+                const uint32_t i = lane + 64 * q;
                 d[q] = desc[gb + (i < gn ? i : 0)];
-                w[q] = 0;
             }
+            // inclusive prefix E of the work in packet order (q-major), one wave scan per q
+            uint32_t base = 0;
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
-                const uint32_t i = 16 * lane + q;
-                if (i < gn) w[q] = A.balance ? flat_work(d[q], OPEN) : 1u;
-                run += w[q];
-                w[q] = run; // inclusive within the lane
-            }
-            uint32_t x = run;
+                const uint32_t i = lane + 64 * q;
+                const uint32_t wq = i < gn ? (A.balance ? flat_work(d[q], OPEN) : 1u) : 0u;
+                uint32_t x = wq;
 #pragma unroll
-            for (int dd = 1; dd < 64; dd <<= 1) {
-                const uint32_t y = (uint32_t)__shfl_up((int)x, dd);
-                if ((int)lane >= dd) x += y;
-            }
-            const uint32_t before = x - run, total = uniform_u32((uint32_t)__shfl((int)x, 63));
-            const uint64_t t[2] = {(uint64_t)total * j / kg, (uint64_t)total * (j + 1) / kg};
-            uint32_t cut[2];
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                uint32_t first = 16, prev = before;
-#pragma unroll
-                for (int q = 0; q < 16; ++q) {
-                    const uint32_t E = before + w[q], wq = E - prev;
-                    if (first == 16 && 16 * lane + q < gn && 2ull * E - wq >= 2 * t[h]) first = (uint32_t)q;
-                    prev = E;
+                for (int dd = 1; dd < 64; dd <<= 1) {
+                    const uint32_t y = (uint32_t)__shfl_up((int)x, dd);
+                    if ((int)lane >= dd) x += y;
                 }
-                const uint64_t hit = __ballot(first < 16);
-                cut[h] = hit ? 16u * (uint32_t)(__ffsll((unsigned long long)hit) - 1) +
-                                   (uint32_t)__shfl((int)first, __ffsll((unsigned long long)hit) - 1)
-                             : gn;
-                cut[h] = uniform_u32(cut[h]);
+                w[q] = base + x; // E of packet i
+                base += uniform_u32((uint32_t)__shfl((int)x, 63));
+            }
+            const uint32_t total = base;
+            const uint64_t t[2] = {(uint64_t)total * j / kg, (uint64_t)total * (j + 1) / kg};
+            // a packet belongs to the unit its work midpoint (E_{i-1} + E_i) / 2 falls in; the midpoints
+            // rise with i, so a cut is the number of packets whose midpoint lies below the target
+            uint32_t cut[2] = {0, 0};
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const uint32_t i = lane + 64 * q;
+                const uint32_t Eprev = (uint32_t)__shfl_up((int)w[q], 1);
+                const uint32_t Eb = lane ? Eprev : (q ? uniform_u32((uint32_t)__shfl((int)w[q > 0 ? q - 1 : 0], 63)) : 0u);
+                const uint64_t mid2 = (uint64_t)w[q] + Eb; // 2 x midpoint = E_i + E_{i-1}
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+                    cut[h] += (uint32_t)__popcll(__ballot(i < gn && mid2 < 2 * t[h]));
             }
             if (j == 0) cut[0] = 0;
             if (j + 1 == kg) cut[1] = gn;
@@ -352,11 +374,8 @@ template <bool OPEN> __global__ __launch_bounds__(256) void flat_kernel(FlatArgs
             // stage the first sub-unit straight from the registers
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
-                const uint32_t i = 16 * lane + q;
-                if (i >= cut[0] && i < cut[1] && i - cut[0] < kFlatMaxPk) {
-                    const uint32_t k = i - cut[0];
-                    flat_stage<OPEN>(L, k, d[q], nkeys, buf_len);
-                }
+                const uint32_t i = lane + 64 * q;
+                if (i >= cut[0] && i < cut[1] && i - cut[0] < kFlatMaxPk) flat_stage<OPEN>(L, i - cut[0], d[q], nkeys, buf_len);
             }
             staged = 1;
         } else { // more than kFlatGroup packets per unit: whole groups
@@ -546,6 +565,31 @@ template <bool OPEN> __global__ __launch_bounds__(256) void flat_kernel(FlatArgs
             s.pi = FChunk{};
             s.pi_cnt = 0;
             s.pk = s.cur.k;
+            // the carry's power: the packet of the lane's last chunk, when it goes on past the lane
+            {
+                s.pe = 0;
+                uint32_t kend = 0;
+                if (s.nsteps) {
+                    uint32_t lo = 0, hi = m; // last k with cs[k] <= c_hi - 1
+                    while (hi - lo > 1) {
+                        const uint32_t mid = (lo + hi) >> 1;
+                        if (L.rec[mid].w <= c_hi - 1) lo = mid;
+                        else hi = mid;
+                    }
+                    kend = lo;
+                    const uint4 rc = L.rec[kend];
+                    const uint32_t nbe = rc.z & ~kLiveBit, tend = c_hi - rc.w; // chunks of kend through the lane
+                    if (4 * tend < nbe) s.pe = nbe - 4 * tend;
+                }
+                const FKey q = fkey(L, kend);
+                s.pr = make_mul(q.r[0], q.r[1], q.r[2], q.r[3]);
+                s.px = Acc{1, 0, 0, 0, 0};
+                uint32_t mx = s.pe;
+#pragma unroll
+                for (int o = 32; o >= 1; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+                s.pb = 31 - (int)__clz((int)uniform_u32(mx)); // -1 when no lane has a carry
+                if (mx == 0) s.pb = -1;
+            }
             {
                 uint32_t j = 0;
                 for (; j + 3 <= S; j += 3) {
@@ -577,8 +621,12 @@ template <bool OPEN> __global__ __launch_bounds__(256) void flat_kernel(FlatArgs
                     after = s.cur.nb - 4 * s.cur.t;
                 }
             }
-            // carry = h r^after for the packet the next lane continues
-            const Acc cv = flat_pow_mul(s.h, s.r, ck != ~0u ? after : 0u);
+            // carry = h r^after for the packet the next lane continues (the power was computed during
+            // phase C; after == s.pe whenever there is a carry)
+            while (s.pb >= 0) pow_step(s);
+            Acc cv = s.h;
+            if (ck != ~0u) acc_mul_gen(cv, make_gen(s.px));
+            (void)after;
             L.ck[lane] = s.nsteps ? ck : kNoChunks;
             L.ch[lane][0] = cv.h0; L.ch[lane][1] = cv.h1; L.ch[lane][2] = cv.h2; L.ch[lane][3] = cv.h3;
             L.ch[lane][4] = cv.h4;
