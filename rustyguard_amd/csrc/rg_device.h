@@ -21,6 +21,31 @@ __device__ __forceinline__ uint64_t uniform_u64(uint64_t v) {
 
 __device__ __forceinline__ uint32_t rotl(uint32_t v, int n) { return __builtin_rotateleft32(v, n); }
 
+// ----------------------------------------------------------- wave scans
+// DPP moves (VALU, no LDS round trip; a shuffle through ds_bpermute costs an LDS
+// latency per step).  update_dpp(old, src, ctrl, row_mask, bank_mask, bound_ctrl):
+// with bound_ctrl a lane whose source is out of range reads 0; rows outside
+// row_mask keep `old`.
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ uint32_t dpp0(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROW_MASK, 0xF, true);
+}
+// inclusive prefix sum over the 64 lanes: row_shr 1/2/4/8 inside rows of 16,
+// then row_bcast:15 / row_bcast:31 carry the row totals up (GFX9 DPP)
+__device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x) {
+    x += dpp0<0x111>(x);
+    x += dpp0<0x112>(x);
+    x += dpp0<0x114>(x);
+    x += dpp0<0x118>(x);
+    x += dpp0<0x142, 0xA>(x);
+    x += dpp0<0x143, 0xC>(x);
+    return x;
+}
+// value of lane - 1 (0 for lane 0): wave_shr:1
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t x) { return dpp0<0x138>(x); }
+// value of lane 63, wave-uniform
+__device__ __forceinline__ uint32_t lane63(uint32_t x) { return (uint32_t)__builtin_amdgcn_readlane((int)x, 63); }
+
 // Byte rotations as v_perm_b32 byte selects instead of v_alignbit_b32
 // (tools/microbench.hip: ChaCha20 +4-5 % at one wave per SIMD, equal at eight).
 // Selector byte i picks source byte sel_i of {v, v} (0-3 = bytes of src1).

@@ -50,7 +50,7 @@ __device__ __forceinline__ uint32_t flat_work(const rg_pkt_desc &d, bool open) {
 // -------------------------------------------------------------- LDS image
 // One per wave, one record set per packet of the sub-unit, laid out so that a
 // lane moving on to the next packet issues all its LDS reads at once.
-constexpr uint32_t kFlatMaxPk = 256;
+constexpr uint32_t kFlatMaxPk = 128;
 struct FlatLds {
     uint4 rec[kFlatMaxPk + 1];    // {offset lo, offset hi, nb | kLiveBit, cs}; rec[m].w = D
     uint32_t kr[kFlatMaxPk][16];  // key[8], counter lo/hi, r[4] (unclamped), desc len, desc key_idx
@@ -61,7 +61,7 @@ struct FlatLds {
 };
 constexpr uint32_t kLiveBit = 0x80000000u, kFail = 2u;
 constexpr uint32_t kNoChunks = 0xFFFFFFFEu;
-constexpr uint32_t kFlatWaves = 4; // one per SIMD
+constexpr uint32_t kFlatWaves = 8; // two per SIMD: one wave's latency-bound phases overlap the other's keystream
 static_assert(kFlatWaves * sizeof(FlatLds) <= kLdsPerCu, "flat LDS image");
 
 __device__ __forceinline__ void wave_sync() {
@@ -188,10 +188,12 @@ __device__ __forceinline__ void flat_step(FLane &s, FChunk &b, uint32_t j, FlatL
             if (dr == 7) acc_block_pred(s.h, s.pi.q3, s.r, s.pi_cnt > 3);
         }
         if (dr % 2 == 1) pin_acc(s.h);
+#ifdef RG_FLAT_POW_HOOK
         if (dr == 2 || dr == 6) {
             pow_step(s);
             pin_acc(s.px);
         }
+#endif
     });
     const FChunk x = {xor4(b.q0, ks + 0), xor4(b.q1, ks + 4), xor4(b.q2, ks + 8), xor4(b.q3, ks + 12)};
     uint4 *dst = const_cast<uint4 *>(s.cur.pl) + 4 * s.cur.t;
@@ -296,7 +298,7 @@ __device__ __forceinline__ uint32_t flat_stage(FlatLds &L, uint32_t k, const rg_
     return (nb + 3) >> 2;
 }
 
-template <bool OPEN> __global__ __launch_bounds__(256) void flat_kernel(FlatArgs A) {
+template <bool OPEN> __global__ __launch_bounds__(512) void flat_kernel(FlatArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t flat_lds[];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     FlatLds &L = reinterpret_cast<FlatLds *>(flat_lds)[wv];
@@ -317,7 +319,11 @@ template <bool OPEN> __global__ __launch_bounds__(256) void flat_kernel(FlatArgs
         if (dbg && mk[slot] == 0) mk[slot] = __builtin_amdgcn_s_memtime(); \
     } while (0)
     const uint32_t NU = A.units;
-    for (uint32_t u = wid; u < NU; u += nw) {
+    // the two waves of a SIMD (wv and wv + 4) take units from opposite ends of the batch, so that
+    // the groups they come from, and their imbalance, differ
+    const uint32_t slot = blockIdx.x * 4 + (wv & 3u);
+    const uint32_t u0 = (wv < 4) ? slot : nw - 1 - slot;
+    for (uint32_t u = u0; u < NU; u += nw) {
         // ---- this unit's packets [s, e) and, when it is read from a group, its first sub-unit staged
         uint32_t s0, e0, staged = 0;
         if ((uint64_t)n <= (uint64_t)kFlatGroup * NU) {
@@ -338,42 +344,50 @@ template <bool OPEN> __global__ __launch_bounds__(256) void flat_kernel(FlatArgs
                 d[q] = desc[gb + (i < gn ? i : 0)];
             }
             // inclusive prefix E of the work in packet order (q-major), one wave scan per q
-            uint32_t base = 0;
+            uint32_t base = 0, rb[17]; // rb[q]: work of the packets before round q (wave-uniform)
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
                 const uint32_t i = lane + 64 * q;
                 const uint32_t wq = i < gn ? (A.balance ? flat_work(d[q], OPEN) : 1u) : 0u;
-                uint32_t x = wq;
-#pragma unroll
-                for (int dd = 1; dd < 64; dd <<= 1) {
-                    const uint32_t y = (uint32_t)__shfl_up((int)x, dd);
-                    if ((int)lane >= dd) x += y;
-                }
+                const uint32_t x = wave_scan_incl(wq);
+                rb[q] = base;
                 w[q] = base + x; // E of packet i
-                base += uniform_u32((uint32_t)__shfl((int)x, 63));
+                base += lane63(x);
             }
+            rb[16] = base;
             const uint32_t total = base;
+#ifdef RG_FLAT_PRO_STAMPS
+            if (dbg && mk[2] == 0) mk[2] = __builtin_amdgcn_s_memtime();
+#endif
             const uint64_t t[2] = {(uint64_t)total * j / kg, (uint64_t)total * (j + 1) / kg};
             // a packet belongs to the unit its work midpoint (E_{i-1} + E_i) / 2 falls in; the midpoints
-            // rise with i, so a cut is the number of packets whose midpoint lies below the target
+            // rise with i, so a cut is the number of packets whose midpoint lies below the target.
+            // Rounds wholly below / above a target are counted from the round bases; only the round
+            // holding it needs a ballot.
             uint32_t cut[2] = {0, 0};
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
-                const uint32_t i = lane + 64 * q;
-                const uint32_t Eprev = (uint32_t)__shfl_up((int)w[q], 1);
-                const uint32_t Eb = lane ? Eprev : (q ? uniform_u32((uint32_t)__shfl((int)w[q > 0 ? q - 1 : 0], 63)) : 0u);
-                const uint64_t mid2 = (uint64_t)w[q] + Eb; // 2 x midpoint = E_i + E_{i-1}
 #pragma unroll
-                for (int h = 0; h < 2; ++h)
-                    cut[h] += (uint32_t)__popcll(__ballot(i < gn && mid2 < 2 * t[h]));
+                for (int h = 0; h < 2; ++h) {
+                    if (rb[q] >= t[h]) continue;                       // every midpoint >= target
+                    const uint32_t real = gn > 64u * q ? min(64u, gn - 64u * q) : 0u;
+                    if (rb[q + 1] < t[h]) { cut[h] += real; continue; } // every midpoint < target
+                    const uint32_t i = lane + 64 * q;
+                    const uint32_t Eb = lane ? wave_shr1(w[q]) : rb[q];
+                    cut[h] += (uint32_t)__popcll(__ballot(i < gn && (uint64_t)w[q] + Eb < 2 * t[h]));
+                }
             }
             if (j == 0) cut[0] = 0;
             if (j + 1 == kg) cut[1] = gn;
+#ifdef RG_FLAT_PRO_STAMPS
+            if (dbg && mk[3] == 0) mk[3] = __builtin_amdgcn_s_memtime();
+#endif
             s0 = gb + cut[0];
             e0 = gb + cut[1];
             // stage the first sub-unit straight from the registers
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
+                if (64u * q + 63 < cut[0] || 64u * q >= min(cut[1], cut[0] + kFlatMaxPk)) continue; // uniform
                 const uint32_t i = lane + 64 * q;
                 if (i >= cut[0] && i < cut[1] && i - cut[0] < kFlatMaxPk) flat_stage<OPEN>(L, i - cut[0], d[q], nkeys, buf_len);
             }
@@ -402,14 +416,9 @@ template <bool OPEN> __global__ __launch_bounds__(256) void flat_kernel(FlatArgs
                 if (64 * q >= m) break; // wave-uniform
                 const uint32_t k = lane + 64 * q;
                 const uint32_t c = k < m ? (L.rec[k].z + 3) >> 2 : 0u;
-                uint32_t x = c;
-#pragma unroll
-                for (int d = 1; d < 64; d <<= 1) {
-                    const uint32_t y = (uint32_t)__shfl_up((int)x, d);
-                    if ((int)lane >= d) x += y;
-                }
+                const uint32_t x = wave_scan_incl(c);
                 if (k < m) L.rec[k].w = run + x - c;
-                run += uniform_u32((uint32_t)__shfl((int)x, 63));
+                run += lane63(x);
             }
             const uint32_t D = run;
             // statuses of the descriptor checks, kept for phase A in registers
@@ -688,7 +697,9 @@ template <bool OPEN> __global__ __launch_bounds__(256) void flat_kernel(FlatArgs
                                 stream_block(stm, p.t + 1, ks);
                                 uint4 *w = const_cast<uint4 *>(p.pl) + 4 * p.t;
                                 const uint32_t c = min(4u, p.nb - 4 * p.t);
-                                for (uint32_t b = 0; b < c; ++b) w[b] = xor4(w[b], ks + 4 * b);
+#pragma unroll
+                                for (uint32_t b = 0; b < 4; ++b)
+                                    if (b < c) w[b] = xor4(w[b], ks + 4 * b);
                             }
                             if (fcur_next(p, L, buf, m) && p.k < m) {
                                 q = fkey(L, p.k);

@@ -9,7 +9,7 @@ shift
 out=tools/build/var_$name
 mkdir -p "$out"
 objs=()
-for src in rg_kernels.hip rg_tile.hip rg_pipe.hip rg_mac.hip rg_api.cpp; do
+for src in rg_kernels.hip rg_tile.hip rg_pipe.hip rg_flat.hip rg_mac.hip rg_api.cpp; do
     x=()
     [[ $src == *.cpp ]] && x=(-x hip)
     /opt/rocm/bin/hipcc "${x[@]}" --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall "$@" -I include \

@@ -59,6 +59,8 @@ for op in ("seal", "open"):
         out[nm] = {"mean_cyc": int(seg[ok].mean()) if ok.any() else None, "max_cyc": int(seg[ok].max()) if ok.any() else None}
         prev = np.where(ok, col, prev)
     out["wave_total"] = {"mean_cyc": int(rel[:, 7].mean()), "max_cyc": int(rel[:, 7].max())}
+    out["slot_mean_from_start"] = [int(rel[:, i][rel[:, i] >= 0].mean()) if (rel[:, i] >= 0).any() else None
+                                   for i in range(1, 8)]
     start = d[:, 0] - d[:, 0].min()
     out["start_spread_cyc"] = int(start.max())
     res[op] = out
