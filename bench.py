@@ -300,6 +300,54 @@ def cold_cache_timing(eng, w, b, stream, verify: bool):
             "gib_s": round(2 * pay / ((seal_ms + open_ms) / 1e3) / 2**30, 3)}
 
 
+def expected_payload(w, k: int) -> np.ndarray:
+    """Synthetic plaintext of packet k (the generator of rustyguard_amd/workloads.py)."""
+    from rustyguard_amd import workloads
+
+    P = int(w.desc["len"][k])
+    words = workloads.mix64(np.uint64(w.data_seed) + (np.uint64(k) << np.uint64(16)) +
+                            np.arange((P + 7) // 8, dtype=np.uint64))
+    out = words.astype("<u8").view(np.uint8)[:P].copy()
+    out[int(w.inner_len[k]):] = 0
+    return out
+
+
+def strict_check(w, b, stream):
+    """Outside the timed region: one more seal and open with the statuses preset to a sentinel (a
+    kernel that skipped a packet would leave it), and a sample of frames checked byte for byte --
+    sealed: header {4, receiver, counter} and payload != plaintext; opened: payload == plaintext."""
+    import torch
+
+    rng = np.random.default_rng(5)
+    idx = np.unique(np.concatenate([[0, w.n - 1], rng.choice(w.n, min(w.n, 254), replace=False)]))
+    exp = {int(k): expected_payload(w, int(k)) for k in idx}
+
+    def frames():
+        out = {}
+        for k in idx:
+            o, p = int(w.desc["offset"][k]), int(w.desc["len"][k])
+            out[int(k)] = b.buf[o:o + p + 32].cpu().numpy()
+        return out
+
+    b.status.fill_(0xEE)
+    b.seal(stream=stream)
+    torch.cuda.synchronize()
+    assert (b.status[: w.n] == 0).all().item(), "seal skipped or failed packets"
+    for k, fr in frames().items():
+        hdr = np.frombuffer(fr[:16].tobytes(), "<u4")
+        key = int(w.desc["key_idx"][k])
+        assert hdr[0] == 4 and hdr[1] == int(w.receivers[key]), f"seal header of packet {k}"
+        assert int(hdr[2]) | (int(hdr[3]) << 32) == int(w.counters[k]), f"seal counter of packet {k}"
+        if len(exp[k]) >= 16:
+            assert not np.array_equal(fr[16:16 + len(exp[k])], exp[k]), f"packet {k} left in plaintext"
+    b.status.fill_(0xEE)
+    b.open(stream=stream, counters_out=False)
+    torch.cuda.synchronize()
+    assert (b.status[: w.n] == 0).all().item(), "open skipped or failed packets"
+    for k, fr in frames().items():
+        assert np.array_equal(fr[16:16 + len(exp[k])], exp[k]), f"open did not restore packet {k}"
+
+
 def load_traffic(workload: str):
     p = os.path.join(REPO, "profiles", f"pmc_{workload}.json")
     if os.path.exists(p):
@@ -436,6 +484,8 @@ def main():
     if args.verify:
         assert (b.status[: w.n] == 0).all().item(), "open failed in the kernel-timing pass"
     cold = cold_cache_timing(eng, w, b, stream, args.verify) if args.cold and w.buf_bytes < MALL_BYTES else None
+    if args.verify:
+        strict_check(w, b, stream)
 
     t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
     if dist is not None:

@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define RG_ABI_VERSION 1
+#define RG_ABI_VERSION 2
 
 typedef struct rg_ctx rg_ctx;
 
@@ -258,10 +258,10 @@ rg_antireplay *rg_sessions_replay(rg_sessions *s, uint32_t slot);
 
 /* Batched PeerState::encrypt_message + frame_in_place over host frames.
  * Packets are processed in array order: each takes the next counter of its
- * session (EncryptionKey::encrypt, prim.rs:386-394).  status[i]: OK, INVALID
- * (P % 16 != 0 / bad desc), REJECTED (counter >= REJECT_AFTER_MESSAGES,
- * lib.rs:204-206, 260-262).  rekey_out[i] (nullable) = 1 when the session
- * counter reached REKEY_AFTER_MESSAGES (lib.rs:564-570). */
+ * session (EncryptionKey::encrypt, prim.rs:386-394) and sets its sent time.  status[i]:
+ * OK, INVALID (P % 16 != 0 / bad desc), REJECTED (counter >= REJECT_AFTER_MESSAGES or
+ * the session older than REJECT_AFTER_TIME, lib.rs:204-209, 260-262).  rekey_out[i]
+ * (nullable) = 1 when the session counter reached REKEY_AFTER_MESSAGES (lib.rs:564-570). */
 int rg_send_batch(rg_sessions *s, const uint32_t *slots, const rg_pkt_desc *desc, size_t n, uint8_t *buf,
                   size_t buf_len, uint8_t *status, uint8_t *rekey_out);
 /* Batched Sessions::recv_message for data frames: alignment/type/length
@@ -271,6 +271,28 @@ int rg_send_batch(rg_sessions *s, const uint32_t *slots, const rg_pkt_desc *desc
  * slots_out[i] = session slot (or 0xFFFFFFFF). */
 int rg_recv_batch(rg_sessions *s, const rg_pkt_desc *desc, size_t n, uint8_t *buf, size_t buf_len,
                   uint8_t *status, uint32_t *slots_out);
+
+/* rg_recv_batch with decrypt_packet's side effects (rustyguard-core/src/lib.rs:664-679):
+ * src[i] (nullable) is an opaque tag of packet i's source address; for every packet that is
+ * authenticated and accepted, in array order, the session's endpoint becomes src[i] (only
+ * authenticated packets move it: whitepaper §6.5, the reference's recv_message fuzz
+ * invariant) and flags_out[i] (nullable) gets RG_RECV_AUTHENTICATED, plus RG_RECV_KEEPALIVE
+ * when sent + KEEPALIVE_TIMEOUT < now and no keepalive is pending yet (the caller schedules
+ * the Keepalive timer; rg_sessions_keepalive_due runs it).  Other packets get flags 0. */
+#define RG_RECV_AUTHENTICATED 1u
+#define RG_RECV_KEEPALIVE 2u
+int rg_recv_batch_ex(rg_sessions *s, const rg_pkt_desc *desc, size_t n, uint8_t *buf, size_t buf_len,
+                     const uint64_t *src, uint8_t *status, uint32_t *slots_out, uint8_t *flags_out);
+/* The table's clock: Sessions::turn's state.now (lib.rs:396-413) as monotonic nanoseconds.
+ * Sessions take it as started / sent when inserted; rg_send_batch sets sent and rejects
+ * once started + REJECT_AFTER_TIME (180 s) < now (should_expire, lib.rs:207-209). */
+void rg_sessions_set_time(rg_sessions *s, uint64_t now_ns);
+/* the endpoint tag of the session's last authenticated packet; RG_ENOTFOUND before any */
+int rg_sessions_endpoint(const rg_sessions *s, uint32_t slot, uint64_t *src_out);
+/* the Keepalive timer entry (rustyguard-core/src/time.rs:114-141): clears keepalive_pending
+ * and returns 1 when sent + KEEPALIVE_TIMEOUT < now (should_keepalive, lib.rs:201-203): the
+ * caller then seals an empty payload (P = 0) for the session with rg_send_batch. */
+int rg_sessions_keepalive_due(rg_sessions *s, uint32_t slot);
 
 /* ------------------------------------------------ synthetic workloads */
 /* Device fill of payload bytes: inner bytes [0, inner_len[i]) of packet i

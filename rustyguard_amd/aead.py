@@ -27,6 +27,7 @@ from ._lib import check, lib
 from .workloads import DESC_DTYPE
 
 PKT_OK, PKT_DECRYPT_ERR, PKT_INVALID, PKT_REJECTED, PKT_UNALIGNED, PKT_NOT_DATA = range(6)
+RECV_AUTHENTICATED, RECV_KEEPALIVE = 1, 2
 KEY_SCAN = 0xFFFFFFFE  # rg_mac_verify_batch_dev: try every key
 KEY_SKIP = 0xFFFFFFFF
 REKEY_AFTER_MESSAGES = 1 << 60
@@ -352,13 +353,37 @@ class Sessions:
               "rg_send_batch")
         return status[:n], rekey[:n]
 
-    def recv_batch(self, desc: np.ndarray, buf: np.ndarray):
+    def recv_batch(self, desc: np.ndarray, buf: np.ndarray, src=None, flags: bool = False):
+        """Sessions::recv_message for a batch of data frames; with src (one opaque source tag per
+        frame) the authenticated ones move their session's endpoint (decrypt_packet,
+        rustyguard-core/src/lib.rs:664-679).  Returns (status, slots) or, with flags=True,
+        (status, slots, flags) where flags holds RECV_AUTHENTICATED / RECV_KEEPALIVE bits."""
         n = len(desc)
         status = np.zeros(max(n, 1), np.uint8)
         slots = np.zeros(max(n, 1), np.uint32)
-        check(lib().rg_recv_batch(self._h, _vp(desc), n, _vp(buf), buf.nbytes, _vp(status), _vp(slots)),
-              "rg_recv_batch")
-        return status[:n], slots[:n]
+        fl = np.zeros(max(n, 1), np.uint8)
+        srcs = None if src is None else np.ascontiguousarray(src, np.uint64)
+        check(lib().rg_recv_batch_ex(self._h, _vp(desc), n, _vp(buf), buf.nbytes, _vp(srcs), _vp(status),
+                                     _vp(slots), _vp(fl)), "rg_recv_batch_ex")
+        return (status[:n], slots[:n], fl[:n]) if flags else (status[:n], slots[:n])
+
+    def set_time(self, now_ns: int):
+        """The table's clock (Sessions::turn's state.now), monotonic nanoseconds."""
+        lib().rg_sessions_set_time(self._h, int(now_ns))
+
+    def endpoint(self, slot: int):
+        """Source tag of the session's last authenticated packet, or None."""
+        out = ctypes.c_uint64()
+        rc = lib().rg_sessions_endpoint(self._h, slot, ctypes.byref(out))
+        if rc == -4:  # RG_ENOTFOUND
+            return None
+        check(rc, "rg_sessions_endpoint")
+        return int(out.value)
+
+    def keepalive_due(self, slot: int) -> bool:
+        """The Keepalive timer entry (time.rs:114-141): clears the pending flag; True when a keepalive
+        (an empty payload through send_batch) should go out now."""
+        return bool(check(lib().rg_sessions_keepalive_due(self._h, slot), "rg_sessions_keepalive_due"))
 
 
 def rx_table(receivers, key_idx, cap: int | None = None) -> np.ndarray:

@@ -823,12 +823,22 @@ struct Session {
     uint32_t local_id = 0, remote_id = 0;
     uint64_t send_ctr = 0;
     rg_antireplay replay{};
+    // rustyguard-core/src/lib.rs:185-191: when the session started and last sent, whether a
+    // keepalive is already scheduled; plus the peer endpoint learned from authenticated packets
+    uint64_t started = 0, sent = 0;
+    bool keepalive_pending = false;
+    bool has_endpoint = false;
+    uint64_t endpoint = 0;
 };
+constexpr uint64_t kNsPerSec = 1000000000ull;
+constexpr uint64_t kKeepaliveTimeout = 10 * kNsPerSec; // KEEPALIVE_TIMEOUT, lib.rs:70
+constexpr uint64_t kRejectAfterTime = 180 * kNsPerSec; // REJECT_AFTER_TIME, lib.rs:67
 } // namespace
 
 struct rg_sessions {
     rg_ctx *ctx = nullptr;
     uint32_t cap = 0;
+    uint64_t now = 0; // Sessions' clock (state.now, advanced by turn: lib.rs:396-413), nanoseconds
     std::vector<Session> s;
     std::vector<uint8_t> keys;       // rows [0,cap): send keys, [cap,2cap): recv keys
     std::vector<uint32_t> receivers; // remote ids for send rows
@@ -867,6 +877,7 @@ int rg_sessions_insert(rg_sessions *s, uint32_t local_id, uint32_t remote_id, co
         x.used = true;
         x.local_id = local_id;
         x.remote_id = remote_id;
+        x.started = x.sent = s->now; // handshake.rs:119-124, :215-216
         memcpy(&s->keys[(size_t)i * 32], send_key, 32);
         memcpy(&s->keys[((size_t)s->cap + i) * 32], recv_key, 32);
         s->receivers[i] = remote_id;
@@ -907,6 +918,24 @@ rg_antireplay *rg_sessions_replay(rg_sessions *s, uint32_t slot) {
     return &s->s[slot].replay;
 }
 
+void rg_sessions_set_time(rg_sessions *s, uint64_t now_ns) {
+    if (s) s->now = now_ns;
+}
+
+int rg_sessions_endpoint(const rg_sessions *s, uint32_t slot, uint64_t *src_out) {
+    if (!s || slot >= s->cap || !s->s[slot].used || !src_out) return set_err(RG_EINVAL, "endpoint: bad slot");
+    if (!s->s[slot].has_endpoint) return RG_ENOTFOUND;
+    *src_out = s->s[slot].endpoint;
+    return RG_OK;
+}
+
+int rg_sessions_keepalive_due(rg_sessions *s, uint32_t slot) {
+    if (!s || slot >= s->cap || !s->s[slot].used) return set_err(RG_EINVAL, "keepalive: bad slot");
+    Session &x = s->s[slot];
+    x.keepalive_pending = false;                     // time.rs:118
+    return x.sent + kKeepaliveTimeout < s->now ? 1 : 0; // should_keepalive, lib.rs:201-203
+}
+
 int rg_send_batch(rg_sessions *s, const uint32_t *slots, const rg_pkt_desc *desc, size_t n, uint8_t *buf,
                   size_t buf_len, uint8_t *status, uint8_t *rekey_out) {
     if (!s || !slots || !desc || !buf || !status) return set_err(RG_EINVAL, "send_batch: bad args");
@@ -921,8 +950,9 @@ int rg_send_batch(rg_sessions *s, const uint32_t *slots, const rg_pkt_desc *desc
             host_status[i] = RG_PKT_REJECTED; // no transport session: caller must handshake
         } else if (d[i].len % 16 != 0) {
             host_status[i] = RG_PKT_INVALID; // force_encrypt's padding assert, lib.rs:273-277
-        } else if (s->s[slot].send_ctr >= RG_REJECT_AFTER_MESSAGES) {
-            host_status[i] = RG_PKT_REJECTED; // should_reject, lib.rs:204-206
+        } else if (s->s[slot].send_ctr >= RG_REJECT_AFTER_MESSAGES ||
+                   s->s[slot].started + kRejectAfterTime < s->now) {
+            host_status[i] = RG_PKT_REJECTED; // should_reject / should_expire, lib.rs:204-209
         }
         if (host_status[i] != RG_PKT_OK) {
             d[i].key_idx = RG_KEY_SKIP;
@@ -930,6 +960,7 @@ int rg_send_batch(rg_sessions *s, const uint32_t *slots, const rg_pkt_desc *desc
         }
         Session &x = s->s[slot];
         ctr[i] = x.send_ctr++; // EncryptionKey::encrypt, prim.rs:387-388
+        x.sent = s->now;        // force_encrypt, lib.rs:285
         d[i].key_idx = slot;
         if (rekey_out && x.send_ctr >= RG_REKEY_AFTER_MESSAGES) rekey_out[i] = 1; // lib.rs:564-570
     }
@@ -943,6 +974,11 @@ int rg_send_batch(rg_sessions *s, const uint32_t *slots, const rg_pkt_desc *desc
 
 int rg_recv_batch(rg_sessions *s, const rg_pkt_desc *desc, size_t n, uint8_t *buf, size_t buf_len,
                   uint8_t *status, uint32_t *slots_out) {
+    return rg_recv_batch_ex(s, desc, n, buf, buf_len, nullptr, status, slots_out, nullptr);
+}
+
+int rg_recv_batch_ex(rg_sessions *s, const rg_pkt_desc *desc, size_t n, uint8_t *buf, size_t buf_len,
+                     const uint64_t *src, uint8_t *status, uint32_t *slots_out, uint8_t *flags_out) {
     if (!s || !desc || !buf || !status) return set_err(RG_EINVAL, "recv_batch: bad args");
     if (n == 0) return RG_OK;
     std::vector<rg_pkt_desc> d(desc, desc + n);
@@ -983,13 +1019,28 @@ int rg_recv_batch(rg_sessions *s, const rg_pkt_desc *desc, size_t n, uint8_t *bu
     // in-order post-pass (RFC 6479 §3.4.3: only authenticated counters advance the window)
     std::vector<rg_pkt_desc> undo;
     std::vector<uint64_t> undo_ctr;
+    if (flags_out) memset(flags_out, 0, n);
     for (size_t i = 0; i < n; ++i) {
         if (host_status[i] != 0xFF) {
             status[i] = host_status[i];
         } else if (status[i] == RG_PKT_OK) {
-            rg_antireplay *r = &s->s[slot_of[i]].replay;
+            Session &x = s->s[slot_of[i]];
+            rg_antireplay *r = &x.replay;
             if (rg_antireplay_would_accept(r, ctr[i])) {
                 rg_antireplay_mark_seen(r, ctr[i]);
+                // decrypt_packet after the AEAD (rustyguard-core/src/lib.rs:664-678): the endpoint
+                // moves only for an authenticated packet (whitepaper §6.5), and the first
+                // authenticated packet of a quiet session asks for a keepalive
+                uint8_t fl = RG_RECV_AUTHENTICATED;
+                if (x.sent + kKeepaliveTimeout < s->now && !x.keepalive_pending) {
+                    x.keepalive_pending = true;
+                    fl |= RG_RECV_KEEPALIVE;
+                }
+                if (src) {
+                    x.endpoint = src[i];
+                    x.has_endpoint = true;
+                }
+                if (flags_out) flags_out[i] = fl;
             } else {
                 // a second copy of a counter accepted earlier in this batch, or one the window
                 // has moved past since: the reference rejects it before decrypting

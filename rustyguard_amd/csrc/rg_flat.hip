@@ -50,7 +50,7 @@ __device__ __forceinline__ uint32_t flat_work(const rg_pkt_desc &d, bool open) {
 // -------------------------------------------------------------- LDS image
 // One per wave, one record set per packet of the sub-unit, laid out so that a
 // lane moving on to the next packet issues all its LDS reads at once.
-constexpr uint32_t kFlatMaxPk = 128;
+constexpr uint32_t kFlatMaxPk = 256;
 struct FlatLds {
     uint4 rec[kFlatMaxPk + 1];    // {offset lo, offset hi, nb | kLiveBit, cs}; rec[m].w = D
     uint32_t kr[kFlatMaxPk][16];  // key[8], counter lo/hi, r[4] (unclamped), desc len, desc key_idx
@@ -61,7 +61,7 @@ struct FlatLds {
 };
 constexpr uint32_t kLiveBit = 0x80000000u, kFail = 2u;
 constexpr uint32_t kNoChunks = 0xFFFFFFFEu;
-constexpr uint32_t kFlatWaves = 8; // two per SIMD: one wave's latency-bound phases overlap the other's keystream
+constexpr uint32_t kFlatWaves = 4; // one per SIMD (two per SIMD, with half-size units, measured slower)
 static_assert(kFlatWaves * sizeof(FlatLds) <= kLdsPerCu, "flat LDS image");
 
 __device__ __forceinline__ void wave_sync() {
@@ -298,7 +298,7 @@ __device__ __forceinline__ uint32_t flat_stage(FlatLds &L, uint32_t k, const rg_
     return (nb + 3) >> 2;
 }
 
-template <bool OPEN> __global__ __launch_bounds__(512) void flat_kernel(FlatArgs A) {
+template <bool OPEN> __global__ __launch_bounds__(64 * kFlatWaves) void flat_kernel(FlatArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t flat_lds[];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     FlatLds &L = reinterpret_cast<FlatLds *>(flat_lds)[wv];
@@ -318,12 +318,11 @@ template <bool OPEN> __global__ __launch_bounds__(512) void flat_kernel(FlatArgs
     do {                                                                    \
         if (dbg && mk[slot] == 0) mk[slot] = __builtin_amdgcn_s_memtime(); \
     } while (0)
+#ifdef RG_FLAT_START_MARK
+    if (dbg && lane == 0) dbg[8ull * wid + 6] = 0xABCD0000ull + wv;
+#endif
     const uint32_t NU = A.units;
-    // the two waves of a SIMD (wv and wv + 4) take units from opposite ends of the batch, so that
-    // the groups they come from, and their imbalance, differ
-    const uint32_t slot = blockIdx.x * 4 + (wv & 3u);
-    const uint32_t u0 = (wv < 4) ? slot : nw - 1 - slot;
-    for (uint32_t u = u0; u < NU; u += nw) {
+    for (uint32_t u = wid; u < NU; u += nw) {
         // ---- this unit's packets [s, e) and, when it is read from a group, its first sub-unit staged
         uint32_t s0, e0, staged = 0;
         if ((uint64_t)n <= (uint64_t)kFlatGroup * NU) {
@@ -731,8 +730,8 @@ hipError_t launch_flat(const SealArgs *sa, const OpenArgs *oa, bool balance, uin
     A.junk = junk;
     A.balance = balance ? 1u : 0u;
     const uint32_t lds = kFlatWaves * (uint32_t)sizeof(FlatLds);
-    if (sa) hipLaunchKernelGGL(flat_kernel<false>, dim3(blocks), dim3(256), lds, s, A);
-    else hipLaunchKernelGGL(flat_kernel<true>, dim3(blocks), dim3(256), lds, s, A);
+    if (sa) hipLaunchKernelGGL(flat_kernel<false>, dim3(blocks), dim3(64 * kFlatWaves), lds, s, A);
+    else hipLaunchKernelGGL(flat_kernel<true>, dim3(blocks), dim3(64 * kFlatWaves), lds, s, A);
     return hipGetLastError();
 }
 

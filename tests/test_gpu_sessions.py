@@ -244,3 +244,81 @@ def test_window_shift_inside_a_batch_rejects_and_restores(pair):
     assert list(st3) == [aead.PKT_OK, aead.PKT_REJECTED]
     o, w = int(od[0]["offset"]), int(od[0]["len"])
     assert np.array_equal(buf[o:o + w], before[o:o + w])
+
+
+S = 1_000_000_000  # ns
+
+
+def test_keepalive_flag_and_timer(pair):
+    """decrypt_packet (rustyguard-core/src/lib.rs:664-678): once the session has not sent for more than
+    KEEPALIVE_TIMEOUT (10 s), the first authenticated packet asks for a keepalive and marks one pending;
+    later packets do not until the Keepalive timer runs (time.rs:114-141), which fires only while the
+    session is still quiet; a send resets the clock."""
+    a, b, sa, sb, sc, keys = pair
+    rng = np.random.default_rng(21)
+    desc, buf = _frames([16] * 6, rng)
+    st, _ = a.send_batch([sa] * 6, desc, buf)
+    assert (st == 0).all()
+    od = desc.copy()
+    od["len"] += 32
+
+    def recv(idx, now):
+        b.set_time(now)
+        d = od[idx].copy()
+        fr = buf.copy()
+        return b.recv_batch(d, fr, src=np.full(len(idx), 7, np.uint64), flags=True)
+
+    st, _, fl = recv([0], 5 * S)  # B inserted at t=0 has sent nothing since: 5 s < 10 s
+    assert st[0] == 0 and fl[0] == aead.RECV_AUTHENTICATED
+    st, _, fl = recv([1, 2], 11 * S)  # quiet for 11 s: the first packet asks, the second finds it pending
+    assert list(st) == [0, 0]
+    assert list(fl) == [aead.RECV_AUTHENTICATED | aead.RECV_KEEPALIVE, aead.RECV_AUTHENTICATED]
+    st, _, fl = recv([3], 12 * S)
+    assert fl[0] == aead.RECV_AUTHENTICATED  # still pending
+    b.set_time(13 * S)
+    assert b.keepalive_due(sb)  # the timer: still quiet -> send an empty packet
+    kd, kb = _frames([0], rng)
+    st, _ = b.send_batch([sb], kd, kb)  # the keepalive itself (P = 0) resets `sent`
+    assert st[0] == 0
+    st, _, fl = recv([4], 14 * S)
+    assert fl[0] == aead.RECV_AUTHENTICATED  # sent 1 s ago
+    st, _, fl = recv([5], 30 * S)  # the timer cleared `pending`; quiet again for > 10 s
+    assert fl[0] == aead.RECV_AUTHENTICATED | aead.RECV_KEEPALIVE
+
+
+def test_endpoint_moves_only_on_authenticated_packets(pair):
+    """The reference's recv_message fuzz invariant (fuzz/fuzz_targets/recv_message.rs:70-122) and
+    whitepaper §6.5: forged or replayed packets from another source never redirect the endpoint."""
+    a, b, sa, sb, sc, keys = pair
+    rng = np.random.default_rng(22)
+    desc, buf = _frames([64, 64], rng)
+    st, _ = a.send_batch([sa, sa], desc, buf)
+    od = desc.copy()
+    od["len"] += 32
+    assert b.endpoint(sb) is None
+    fr = buf.copy()
+    st, _ = b.recv_batch(od[:1].copy(), fr, src=np.array([100], np.uint64))
+    assert st[0] == 0 and b.endpoint(sb) == 100
+    forged = buf.copy()
+    o, w = int(od[1]["offset"]), int(od[1]["len"])
+    forged[o + w - 1] ^= 1
+    st, _, fl = b.recv_batch(od[1:].copy(), forged, src=np.array([666], np.uint64), flags=True)
+    assert st[0] == aead.PKT_DECRYPT_ERR and fl[0] == 0 and b.endpoint(sb) == 100
+    replay = buf.copy()
+    st, _, fl = b.recv_batch(od[:1].copy(), replay, src=np.array([667], np.uint64), flags=True)
+    assert st[0] == aead.PKT_REJECTED and fl[0] == 0 and b.endpoint(sb) == 100
+    st, _ = b.recv_batch(od[1:].copy(), buf.copy(), src=np.array([101], np.uint64))
+    assert st[0] == 0 and b.endpoint(sb) == 101  # roaming: a genuine packet from a new address
+
+
+def test_send_rejects_after_reject_after_time(pair):
+    """should_expire (rustyguard-core/src/lib.rs:207-209): 180 s after the session started, send refuses."""
+    a, b, sa, sb, sc, keys = pair
+    rng = np.random.default_rng(23)
+    desc, buf = _frames([16, 16], rng)
+    a.set_time(180 * S)
+    st, _ = a.send_batch([sa], desc[:1].copy(), buf)
+    assert st[0] == 0  # started + 180 s is not < now
+    a.set_time(180 * S + 1)
+    st, _ = a.send_batch([sa], desc[1:].copy(), buf)
+    assert st[0] == aead.PKT_REJECTED
