@@ -191,7 +191,7 @@ int rg_set_debug_buffer(rg_ctx *ctx, void *dev_ptr);
 
 /* ----------------------------------------- host-memory batch (blocking) */
 /* Same contract with host pointers: frames are staged H2D, sealed/opened on
- * the GPU and copied back D2H, pipelined over two streams.  Pinned memory
+ * the GPU and copied back D2H, pipelined over three streams.  Pinned memory
  * (rg_host_alloc) gives the full PCIe rate. */
 int rg_seal_batch_host(rg_ctx *ctx, const uint8_t *keys, const uint32_t *receivers, uint32_t nkeys,
                        const rg_pkt_desc *desc, const uint64_t *counters, size_t n, uint8_t *buf, size_t buf_len,

@@ -159,7 +159,7 @@ struct rg_ctx {
     uint64_t *dbg = nullptr; // diagnostics buffer (device), stamp builds only
     int pipe_max_wg[2] = {0, 0}; // [seal, open] resident workgroups per CU of the pipelined kernel
     std::mutex mu;
-    Slot slots[2];
+    Slot slots[3]; // host pipeline: up to three slices in flight (H2D of one beside D2H of another)
     DevBuf d_keys, d_recv;
     DevBuf d_general;  // per-message drop-in arena
     DevBuf d_rx_desc;  // rg_open_batch_dev_rx: resolved descriptors
@@ -564,7 +564,7 @@ void rg_host_free(void *p) {
 // ------------------------------------------------------------ host pipeline
 namespace {
 
-constexpr size_t kSliceBytes = 32ull << 20; // frames per pipeline slice
+constexpr size_t kSliceBytes = 16ull << 20; // frames per pipeline slice
 constexpr size_t kSlicePkts = 1u << 16;
 constexpr uint64_t kOutOfRange = (UINT64_MAX / 2) & ~15ull;
 
@@ -672,7 +672,7 @@ int host_batch(rg_ctx *ctx, bool open, uint32_t nkeys, const rg_pkt_desc *desc, 
         s.i1 = j;
         s.busy = true;
         i = j;
-        which ^= 1;
+        which = (which + 1) % 3;
     }
     for (auto &s : ctx->slots) {
         int rc = finish_slot(s, status, open ? counters_out : nullptr);

@@ -38,6 +38,15 @@
 
 namespace rg {
 
+// floor(a / b) for a < 2^53, b > 0: a double estimate corrected to the exact quotient
+// (a 64-bit integer division is a long software loop on the GPU)
+__device__ __forceinline__ uint64_t fdiv(uint64_t a, uint64_t b) {
+    uint64_t q = (uint64_t)((double)a / (double)b);
+    if (q * b > a) --q;
+    if ((q + 1) * b <= a) ++q;
+    return q;
+}
+
 // ------------------------------------------------------ unit boundaries
 // Work of a packet: its one-time-key block and its 64-byte chunks (from the
 // descriptor alone).
@@ -329,9 +338,9 @@ template <bool OPEN> __global__ __launch_bounds__(64 * kFlatWaves) void flat_ker
             // Units of group g (kFlatGroup packets): those whose nominal start u n / NU falls in it;
             // inside the group the cut points split its work evenly (midpoint rule).  No global
             // pass: the wave reads the group's descriptors (16 per lane) and scans them itself.
-            const uint32_t g = (uint32_t)((uint64_t)u * n / NU / kFlatGroup);
-            const uint32_t f0 = (uint32_t)(((uint64_t)g * kFlatGroup * NU + n - 1) / n);
-            const uint32_t f1 = (uint32_t)min((uint64_t)NU, (((uint64_t)g + 1) * kFlatGroup * NU + n - 1) / n);
+            const uint32_t g = (uint32_t)fdiv((uint64_t)u * n, (uint64_t)NU * kFlatGroup);
+            const uint32_t f0 = (uint32_t)fdiv((uint64_t)g * kFlatGroup * NU + n - 1, n);
+            const uint32_t f1 = (uint32_t)min((uint64_t)NU, fdiv(((uint64_t)g + 1) * kFlatGroup * NU + n - 1, n));
             const uint32_t kg = f1 - f0, j = u - f0;
             const uint32_t gb = g * kFlatGroup, gn = min(kFlatGroup, n - gb);
             // coalesced: lane l holds packets l + 64 q of the group (q = 0..15)
@@ -343,38 +352,36 @@ template <bool OPEN> __global__ __launch_bounds__(64 * kFlatWaves) void flat_ker
                 d[q] = desc[gb + (i < gn ? i : 0)];
             }
             // inclusive prefix E of the work in packet order (q-major), one wave scan per q
-            uint32_t base = 0, rb[17]; // rb[q]: work of the packets before round q (wave-uniform)
+            // inclusive prefix E of the work in packet order (q-major), one DPP wave scan per round;
+            // group totals stay below 2^24 (1024 packets of at most 16386 blocks), so 32 bits suffice
+            uint32_t base = 0;
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
                 const uint32_t i = lane + 64 * q;
                 const uint32_t wq = i < gn ? (A.balance ? flat_work(d[q], OPEN) : 1u) : 0u;
                 const uint32_t x = wave_scan_incl(wq);
-                rb[q] = base;
                 w[q] = base + x; // E of packet i
                 base += lane63(x);
             }
-            rb[16] = base;
             const uint32_t total = base;
 #ifdef RG_FLAT_PRO_STAMPS
             if (dbg && mk[2] == 0) mk[2] = __builtin_amdgcn_s_memtime();
 #endif
-            const uint64_t t[2] = {(uint64_t)total * j / kg, (uint64_t)total * (j + 1) / kg};
+            // targets j total / kg and (j + 1) total / kg without a 64-bit division
+            const uint32_t tq = total / kg, tr = total % kg;
+            const uint32_t t2[2] = {2 * (tq * j + tr * j / kg), 2 * (tq * (j + 1) + tr * (j + 1) / kg)};
             // a packet belongs to the unit its work midpoint (E_{i-1} + E_i) / 2 falls in; the midpoints
-            // rise with i, so a cut is the number of packets whose midpoint lies below the target.
-            // Rounds wholly below / above a target are counted from the round bases; only the round
-            // holding it needs a ballot.
+            // rise with i, so a cut is the number of packets whose midpoint lies below the target
             uint32_t cut[2] = {0, 0};
+            uint32_t prev63 = 0; // E of the packet before round q
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    if (rb[q] >= t[h]) continue;                       // every midpoint >= target
-                    const uint32_t real = gn > 64u * q ? min(64u, gn - 64u * q) : 0u;
-                    if (rb[q + 1] < t[h]) { cut[h] += real; continue; } // every midpoint < target
-                    const uint32_t i = lane + 64 * q;
-                    const uint32_t Eb = lane ? wave_shr1(w[q]) : rb[q];
-                    cut[h] += (uint32_t)__popcll(__ballot(i < gn && (uint64_t)w[q] + Eb < 2 * t[h]));
-                }
+                const uint32_t i = lane + 64 * q;
+                const uint32_t sh = wave_shr1(w[q]);
+                const uint32_t mid2 = w[q] + (lane ? sh : prev63);
+                prev63 = lane63(w[q]);
+                cut[0] += (uint32_t)__popcll(__ballot(i < gn && mid2 < t2[0]));
+                cut[1] += (uint32_t)__popcll(__ballot(i < gn && mid2 < t2[1]));
             }
             if (j == 0) cut[0] = 0;
             if (j + 1 == kg) cut[1] = gn;
@@ -393,8 +400,8 @@ template <bool OPEN> __global__ __launch_bounds__(64 * kFlatWaves) void flat_ker
             staged = 1;
         } else { // more than kFlatGroup packets per unit: whole groups
             const uint32_t G = (n + kFlatGroup - 1) / kFlatGroup;
-            s0 = (uint32_t)min((uint64_t)n, (uint64_t)u * G / NU * kFlatGroup);
-            e0 = (uint32_t)min((uint64_t)n, (uint64_t)(u + 1) * G / NU * kFlatGroup);
+            s0 = (uint32_t)min((uint64_t)n, fdiv((uint64_t)u * G, NU) * kFlatGroup);
+            e0 = (uint32_t)min((uint64_t)n, fdiv((uint64_t)(u + 1) * G, NU) * kFlatGroup);
         }
         RG_FLAT_MARK(1);
         for (uint32_t sb = s0; sb < e0; sb += kFlatMaxPk) {
@@ -426,7 +433,7 @@ template <bool OPEN> __global__ __launch_bounds__(64 * kFlatWaves) void flat_ker
             if (lane == 0) L.rec[m] = make_uint4(0, 0, 0, D);
             RG_FLAT_MARK(2);
             // ---- the lane's chunk range and start packet
-            const uint32_t c_lo = (uint32_t)((uint64_t)lane * D / 64), c_hi = (uint32_t)((uint64_t)(lane + 1) * D / 64);
+            const uint32_t c_lo = (uint32_t)(((uint64_t)lane * D) >> 6), c_hi = (uint32_t)(((uint64_t)(lane + 1) * D) >> 6);
             FLane s;
             s.nsteps = c_hi - c_lo;
             uint32_t kstart = m;
@@ -653,10 +660,11 @@ template <bool OPEN> __global__ __launch_bounds__(64 * kFlatWaves) void flat_ker
                 // the packet's other pieces: the carries of the lanes just before its final lane
                 // (lanes without chunks sit between them when D < 64 and pass through)
                 for (int l = (int)h4l.y - 1; l >= 0; --l) {
-                    const uint32_t c = L.ck[l];
+                    const uint32_t c = L.ck[l]; // read with the value: one LDS round trip per lane
+                    const Acc cv = {L.ch[l][0], L.ch[l][1], L.ch[l][2], L.ch[l][3], L.ch[l][4]};
                     if (c == kNoChunks) continue;
                     if (c != k) break;
-                    acc_add_acc(h, Acc{L.ch[l][0], L.ch[l][1], L.ch[l][2], L.ch[l][3], L.ch[l][4]});
+                    acc_add_acc(h, cv);
                     acc_fold(h);
                 }
                 const uint32_t P = (rc.z & ~kLiveBit) * 16;
