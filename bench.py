@@ -69,6 +69,8 @@ def parse():
     ap.add_argument("--plan", type=int, default=-1, help="size-class planner: 0 off, 1 on, 2 auto, -1 library default (auto)")
     ap.add_argument("--segments", type=int, default=0, help="segments per packet for the tile kernels (0 = auto)")
     ap.add_argument("--debug-mode", type=int, default=0, help="seal diagnostics (invalid output): 1 compute-only, 2 memory-only")
+    ap.add_argument("--split", type=int, default=1,
+                    help="sub-batches per step: seal of part k+1 overlaps open of part k on a second stream")
     ap.add_argument("--no-graph", action="store_true", help="launch eagerly instead of replaying a captured HIP graph")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="CPU baseline budget: port and OpenSSL, 1 thread and all cores, 5 runs each (0 = skip)")
@@ -392,19 +394,24 @@ def main():
     from rustyguard_amd.aead import Engine
     from rustyguard_amd.device import DeviceBatch
 
-    eng = Engine(local)
-    if args.lanes:
-        eng.set_lanes_per_packet(args.lanes)
-    if args.wg_per_cu:
-        eng.set_wg_per_cu(args.wg_per_cu)
-    if args.debug_mode:
-        eng.set_debug_mode(args.debug_mode)
-    if args.staged != -1:
-        eng.set_staged(args.staged)
-    if args.plan >= 0:
-        eng.set_plan(args.plan)
-    if args.segments:
-        eng.set_segments(args.segments)
+    def configured_engine():
+        e = Engine(local)
+        if args.lanes:
+            e.set_lanes_per_packet(args.lanes)
+        if args.wg_per_cu:
+            e.set_wg_per_cu(args.wg_per_cu)
+        if args.debug_mode:
+            e.set_debug_mode(args.debug_mode)
+        if args.staged != -1:
+            e.set_staged(args.staged)
+        if args.plan >= 0:
+            e.set_plan(args.plan)
+        if args.segments:
+            e.set_segments(args.segments)
+        return e
+
+    eng = configured_engine()
+    eng_open = configured_engine() if args.split > 1 else eng  # opens run beside seals: own planner scratch
     if workload == "cfg5":
         w = workloads.build("cfg5", rank, world)  # strong split of the 8 Mi batch
     else:
@@ -413,24 +420,41 @@ def main():
     b.fill()
     torch.cuda.synchronize()
 
-    # One step = seal the batch then open it (both in place, on one stream).
+    # One step = seal the batch then open it (both in place).  With --split K the batch is K
+    # contiguous packet ranges: seal of range k runs on the step's stream, open of range k on a
+    # second stream once that seal is done, so open k overlaps seal k+1 and each launch's ramp-down
+    # and write drain hide behind the next one (the same packets, the same work).
     # Captured once into a HIP graph (torch.cuda.CUDAGraph drives HIP stream
     # capture) and replayed, so launch latency does not sit between steps.
+    ostream = torch.cuda.Stream()
+    parts = b.parts(args.split) if args.split > 1 else None
+
+    def enqueue(s_):
+        if parts is None:
+            b.seal(stream=s_)
+            b.open(stream=s_, counters_out=False)
+            return
+        ostream.wait_stream(s_)
+        for p in parts:
+            b.seal(stream=s_, part=p)
+            ev = torch.cuda.Event()
+            ev.record(s_)
+            ostream.wait_event(ev)
+            b.open(stream=ostream, counters_out=False, part=p, engine=eng_open)
+        s_.wait_stream(ostream)
+
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(side):
         for _ in range(max(args.warmup, 1)):
-            b.seal(stream=side)
-            b.open(stream=side, counters_out=False)
+            enqueue(side)
     torch.cuda.current_stream().wait_stream(side)
     torch.cuda.synchronize()
     graph = None
     if not args.no_graph:
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
-            s_ = torch.cuda.current_stream()
-            b.seal(stream=s_)
-            b.open(stream=s_, counters_out=False)
+            enqueue(torch.cuda.current_stream())
         graph.replay()
         torch.cuda.synchronize()
     stream = torch.cuda.current_stream()
@@ -439,8 +463,7 @@ def main():
         if graph is not None:
             graph.replay()
         else:
-            b.seal(stream=stream)
-            b.open(stream=stream, counters_out=False)
+            enqueue(stream)
 
     for _ in range(args.warmup):
         step()
@@ -529,7 +552,7 @@ def main():
                    "payload_bytes_per_packet": int(w.desc["len"][0]) if w.n else 0,
                    "mean_payload_bytes": round(payload / max(w.n, 1), 2), "wire_bytes_per_gpu": w.wire_bytes,
                    "sessions": int(w.meta.get("sessions", 1)), "parallelism": f"split{world} (no collective)",
-                   "kernel": kernel_label(args, eng, w),
+                   "kernel": kernel_label(args, eng, w), "split": args.split,
                    "wg_per_cu": args.wg_per_cu or "auto"},
         "mpkt_s": round(total_pkts / tmax / 1e6, 3),
         "seal_ms": round(seal_ms, 5),

@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define RG_ABI_VERSION 2
+#define RG_ABI_VERSION 3
 
 typedef struct rg_ctx rg_ctx;
 
@@ -293,6 +293,34 @@ int rg_sessions_endpoint(const rg_sessions *s, uint32_t slot, uint64_t *src_out)
  * and returns 1 when sent + KEEPALIVE_TIMEOUT < now (should_keepalive, lib.rs:201-203): the
  * caller then seals an empty payload (P = 0) for the session with rg_send_batch. */
 int rg_sessions_keepalive_due(rg_sessions *s, uint32_t slot);
+
+/* Device-resident variants of rg_send_batch / rg_recv_batch_ex: frames, descriptors and
+ * statuses in device memory, the session state on the host.  Work is enqueued on `stream`
+ * (hipStream_t) and the calls return without waiting for the GPU; the table keeps device
+ * mirrors of its keys, receivers and a receiver-id -> session table, refreshed (after the
+ * device work that reads them has drained) on the first device call after a session change.
+ *
+ * rg_send_batch_dev: slots[] and rekey_out[] are host arrays; desc[i].key_idx is ignored
+ * (the packet's session decides it).  Counters are reserved on the host in array order as
+ * rg_send_batch does; since the lengths are on the device, a frame with P % 16 != 0 still takes
+ * a counter and the kernel reports it RG_PKT_INVALID (nonces stay unique).  status (device,
+ * nullable) gets the per-packet statuses.  Two sends may be in flight; a third waits for the
+ * first one's seal. */
+int rg_send_batch_dev(rg_sessions *s, const uint32_t *slots, const rg_pkt_desc *desc, size_t n, uint8_t *buf,
+                      size_t buf_len, uint8_t *status, uint8_t *rekey_out, void *stream);
+/* rg_recv_batch_dev enqueues receiver resolution (rg_open_batch_dev_rx), the GPU open and
+ * the copy of (status, counter, session) per packet to pinned host memory; status (device)
+ * gets the GPU verdicts.  rg_recv_batch_dev_finish waits for that copy, runs the in-order
+ * anti-replay pass and decrypt_packet's side effects exactly as rg_recv_batch_ex (src, flags),
+ * writes the final statuses back to the device status array, and re-seals frames it rejected
+ * (they go back to ciphertext), all on the batch's stream; status_out / slots_out / flags_out
+ * are optional host arrays.  One device receive may be pending per table: finish it before
+ * the next rg_recv_batch_dev, rg_sessions_insert or rg_sessions_remove (RG_EINVAL otherwise).
+ * Replayed frames are decrypted and re-sealed (the device cannot consult the window first). */
+int rg_recv_batch_dev(rg_sessions *s, const rg_pkt_desc *desc, size_t n, uint8_t *buf, size_t buf_len,
+                      uint8_t *status, void *stream);
+int rg_recv_batch_dev_finish(rg_sessions *s, const uint64_t *src, uint8_t *status_out, uint32_t *slots_out,
+                             uint8_t *flags_out);
 
 /* ------------------------------------------------ synthetic workloads */
 /* Device fill of payload bytes: inner bytes [0, inner_len[i]) of packet i

@@ -68,6 +68,9 @@ SIGNATURES = {
     "rg_sessions_set_time": (None, [c_vp, c_u64]),
     "rg_sessions_endpoint": (c_int, [c_vp, c_u32, c_vp]),
     "rg_sessions_keepalive_due": (c_int, [c_vp, c_u32]),
+    "rg_send_batch_dev": (c_int, [c_vp, c_vp, c_vp, c_size, c_vp, c_size, c_vp, c_u8p, c_vp]),
+    "rg_recv_batch_dev": (c_int, [c_vp, c_vp, c_size, c_vp, c_size, c_vp, c_vp]),
+    "rg_recv_batch_dev_finish": (c_int, [c_vp, c_vp, c_u8p, c_vp, c_u8p]),
     "rg_synth_fill_dev": (c_int, [c_vp, c_vp, c_vp, c_size, c_u8p, c_size, c_u64, c_vp]),
 }
 

@@ -367,6 +367,33 @@ class Sessions:
                                      _vp(slots), _vp(fl)), "rg_recv_batch_ex")
         return (status[:n], slots[:n], fl[:n]) if flags else (status[:n], slots[:n])
 
+    def send_batch_dev(self, slots, desc, buf, status=None, stream=None):
+        """rg_send_batch_dev: device frames / descriptors (torch tensors), host slots; enqueued on
+        `stream`, returns the rekey flags (host) without waiting for the GPU."""
+        slots = np.ascontiguousarray(slots, np.uint32)
+        n = _ndesc(desc)
+        rekey = np.zeros(max(n, 1), np.uint8)
+        check(lib().rg_send_batch_dev(self._h, _vp(slots), _vp(desc), n, _vp(buf), _nbytes(buf), _vp(status),
+                                      _vp(rekey), _stream_handle(stream)), "rg_send_batch_dev")
+        return rekey[:n]
+
+    def recv_batch_dev(self, desc, buf, status, stream=None):
+        """rg_recv_batch_dev: enqueue the GPU half of a device-resident receive; finish it with
+        recv_batch_dev_finish."""
+        check(lib().rg_recv_batch_dev(self._h, _vp(desc), _ndesc(desc), _vp(buf), _nbytes(buf), _vp(status),
+                                      _stream_handle(stream)), "rg_recv_batch_dev")
+
+    def recv_batch_dev_finish(self, n: int, src=None):
+        """rg_recv_batch_dev_finish: the in-order anti-replay pass of the pending device receive.
+        Returns (status, slots, flags) as host arrays."""
+        status = np.zeros(max(n, 1), np.uint8)
+        slots = np.zeros(max(n, 1), np.uint32)
+        fl = np.zeros(max(n, 1), np.uint8)
+        srcs = None if src is None else np.ascontiguousarray(src, np.uint64)
+        check(lib().rg_recv_batch_dev_finish(self._h, _vp(srcs), _vp(status), _vp(slots), _vp(fl)),
+              "rg_recv_batch_dev_finish")
+        return status[:n], slots[:n], fl[:n]
+
     def set_time(self, now_ns: int):
         """The table's clock (Sessions::turn's state.now), monotonic nanoseconds."""
         lib().rg_sessions_set_time(self._h, int(now_ns))

@@ -835,6 +835,35 @@ constexpr uint64_t kKeepaliveTimeout = 10 * kNsPerSec; // KEEPALIVE_TIMEOUT, lib
 constexpr uint64_t kRejectAfterTime = 180 * kNsPerSec; // REJECT_AFTER_TIME, lib.rs:67
 } // namespace
 
+namespace {
+// Device half of the session table for rg_send_batch_dev / rg_recv_batch_dev: mirrors of the key
+// rows, the receivers and a receiver-id -> recv-row table, refreshed before the next device call
+// after a session change (once the device work that reads them has drained).
+struct SendStage { // one device send in flight per stage; two stages alternate
+    DevBuf d_desc, d_kidx, d_ctr;
+    HostBuf h_kidx, h_ctr;
+    hipEvent_t ev = nullptr; // the stage's seal has consumed its buffers
+};
+struct RecvStage { // the device receive between rg_recv_batch_dev and rg_recv_batch_dev_finish
+    DevBuf d_rdesc, d_ctr, d_key, d_idx, d_udesc, d_uctr;
+    HostBuf h_status, h_ctr, h_key, h_fix, h_idx;
+    hipEvent_t ev_meta = nullptr, ev_done = nullptr;
+    bool pending = false;
+    size_t n = 0;
+    hipStream_t st = nullptr;
+    uint8_t *buf = nullptr, *status = nullptr;
+    size_t buf_len = 0;
+};
+struct SessDev {
+    DevBuf keys, recv, rx;
+    uint32_t rx_cap = 0;
+    bool dirty = true;
+    SendStage send[2];
+    int send_next = 0;
+    RecvStage rv;
+};
+} // namespace
+
 struct rg_sessions {
     rg_ctx *ctx = nullptr;
     uint32_t cap = 0;
@@ -843,7 +872,86 @@ struct rg_sessions {
     std::vector<uint8_t> keys;       // rows [0,cap): send keys, [cap,2cap): recv keys
     std::vector<uint32_t> receivers; // remote ids for send rows
     std::unordered_map<uint32_t, uint32_t> by_local;
+    SessDev dev;
 };
+
+namespace {
+
+// The in-order tail of DecryptionKey::decrypt (prim.rs:414-437) and decrypt_packet
+// (rustyguard-core/src/lib.rs:655-679) for packet i of session `slot`, whose GPU verdict
+// `st` is RG_PKT_OK or RG_PKT_DECRYPT_ERR: would_accept comes first (Error::Rejected, also
+// for a frame too short or with a bad tag), then the AEAD's verdict; an accepted packet
+// advances the window (only authenticated counters do, RFC 6479 §3.4.3), may move the
+// endpoint (whitepaper §6.5) and may ask for a keepalive.  *undo: the GPU left plaintext in
+// a frame the reference would not have decrypted.
+uint8_t replay_step(rg_sessions *s, uint32_t slot, uint64_t ctr, uint8_t st, const uint64_t *src, size_t i,
+                    uint8_t *fl, bool *undo) {
+    Session &x = s->s[slot];
+    *undo = false;
+    *fl = 0;
+    if (!rg_antireplay_would_accept(&x.replay, ctr)) {
+        *undo = st == RG_PKT_OK;
+        return RG_PKT_REJECTED;
+    }
+    if (st != RG_PKT_OK) return st;
+    rg_antireplay_mark_seen(&x.replay, ctr);
+    uint8_t f = RG_RECV_AUTHENTICATED;
+    if (x.sent + kKeepaliveTimeout < s->now && !x.keepalive_pending) {
+        x.keepalive_pending = true;
+        f |= RG_RECV_KEEPALIVE;
+    }
+    if (src) {
+        x.endpoint = src[i];
+        x.has_endpoint = true;
+    }
+    *fl = f;
+    return RG_PKT_OK;
+}
+
+hipError_t sync_event(hipEvent_t e) { return e ? hipEventSynchronize(e) : hipSuccess; }
+
+hipError_t drain_device_work(SessDev &D) {
+    hipError_t e = hipSuccess;
+    for (auto &g : D.send)
+        if (e == hipSuccess) e = sync_event(g.ev);
+    if (e == hipSuccess) e = sync_event(D.rv.ev_meta);
+    if (e == hipSuccess) e = sync_event(D.rv.ev_done);
+    return e;
+}
+
+// refresh the device mirrors after session changes
+int sync_tables(rg_sessions *s) {
+    SessDev &D = s->dev;
+    if (!D.dirty) return RG_OK;
+    RG_HIP(drain_device_work(D), "session tables in use");
+    RG_HIP(D.keys.reserve(s->keys.size()), "alloc session keys");
+    RG_HIP(hipMemcpy(D.keys.p, s->keys.data(), s->keys.size(), hipMemcpyHostToDevice), "H2D session keys");
+    RG_HIP(D.recv.reserve((size_t)s->cap * 4), "alloc session receivers");
+    RG_HIP(hipMemcpy(D.recv.p, s->receivers.data(), (size_t)s->cap * 4, hipMemcpyHostToDevice),
+           "H2D session receivers");
+    std::vector<uint32_t> ids, rows;
+    for (uint32_t i = 0; i < s->cap; ++i)
+        if (s->s[i].used) {
+            ids.push_back(s->s[i].local_id);
+            rows.push_back(s->cap + i); // the session's recv-key row
+        }
+    uint32_t rx_cap = 2;
+    while (rx_cap < 2 * ids.size()) rx_cap <<= 1;
+    std::vector<rg_rx_entry> t(rx_cap);
+    int rc = rg_rx_table_build(ids.data(), rows.data(), ids.size(), t.data(), rx_cap);
+    if (rc) return rc;
+    RG_HIP(D.rx.reserve((size_t)rx_cap * sizeof(rg_rx_entry)), "alloc rx table");
+    RG_HIP(hipMemcpy(D.rx.p, t.data(), (size_t)rx_cap * sizeof(rg_rx_entry), hipMemcpyHostToDevice), "H2D rx table");
+    D.rx_cap = rx_cap;
+    D.dirty = false;
+    return RG_OK;
+}
+
+hipError_t ensure_event(hipEvent_t &e) {
+    return e ? hipSuccess : hipEventCreateWithFlags(&e, hipEventDisableTiming);
+}
+
+} // namespace
 
 extern "C" {
 
@@ -863,12 +971,28 @@ int rg_sessions_create(rg_ctx *ctx, uint32_t capacity, rg_sessions **out) {
 void rg_sessions_destroy(rg_sessions *s) {
     if (!s) return;
     std::fill(s->keys.begin(), s->keys.end(), 0); // zeroize, as prim.rs:227-231 / lib.rs:216-228
+    SessDev &D = s->dev;
+    (void)hipSetDevice(s->ctx->device);
+    (void)drain_device_work(D);
+    if (D.keys.p) (void)hipMemset(D.keys.p, 0, D.keys.cap);
+    D.keys.release(); D.recv.release(); D.rx.release();
+    for (auto &g : D.send) {
+        g.d_desc.release(); g.d_kidx.release(); g.d_ctr.release(); g.h_kidx.release(); g.h_ctr.release();
+        if (g.ev) (void)hipEventDestroy(g.ev);
+    }
+    RecvStage &R = D.rv;
+    R.d_rdesc.release(); R.d_ctr.release(); R.d_key.release(); R.d_idx.release(); R.d_udesc.release();
+    R.d_uctr.release(); R.h_status.release(); R.h_ctr.release(); R.h_key.release(); R.h_fix.release();
+    R.h_idx.release();
+    if (R.ev_meta) (void)hipEventDestroy(R.ev_meta);
+    if (R.ev_done) (void)hipEventDestroy(R.ev_done);
     delete s;
 }
 
 int rg_sessions_insert(rg_sessions *s, uint32_t local_id, uint32_t remote_id, const uint8_t send_key[32],
                        const uint8_t recv_key[32]) {
     if (!s || !send_key || !recv_key) return set_err(RG_EINVAL, "insert: bad args");
+    if (s->dev.rv.pending) return set_err(RG_EINVAL, "insert: a device receive batch is pending");
     if (s->by_local.count(local_id)) return set_err(RG_EINVAL, "insert: local id in use");
     for (uint32_t i = 0; i < s->cap; ++i) {
         Session &x = s->s[i];
@@ -882,6 +1006,7 @@ int rg_sessions_insert(rg_sessions *s, uint32_t local_id, uint32_t remote_id, co
         memcpy(&s->keys[((size_t)s->cap + i) * 32], recv_key, 32);
         s->receivers[i] = remote_id;
         s->by_local[local_id] = i;
+        s->dev.dirty = true;
         return (int)i;
     }
     return set_err(RG_EFULL, "insert: table full");
@@ -889,6 +1014,8 @@ int rg_sessions_insert(rg_sessions *s, uint32_t local_id, uint32_t remote_id, co
 
 int rg_sessions_remove(rg_sessions *s, uint32_t slot) {
     if (!s || slot >= s->cap || !s->s[slot].used) return set_err(RG_EINVAL, "remove: bad slot");
+    if (s->dev.rv.pending) return set_err(RG_EINVAL, "remove: a device receive batch is pending");
+    s->dev.dirty = true;
     s->by_local.erase(s->s[slot].local_id);
     s->s[slot] = Session();
     memset(&s->keys[(size_t)slot * 32], 0, 32);
@@ -1021,35 +1148,22 @@ int rg_recv_batch_ex(rg_sessions *s, const rg_pkt_desc *desc, size_t n, uint8_t 
     std::vector<uint64_t> undo_ctr;
     if (flags_out) memset(flags_out, 0, n);
     for (size_t i = 0; i < n; ++i) {
-        if (host_status[i] != 0xFF) {
-            status[i] = host_status[i];
-        } else if (status[i] == RG_PKT_OK) {
-            Session &x = s->s[slot_of[i]];
-            rg_antireplay *r = &x.replay;
-            if (rg_antireplay_would_accept(r, ctr[i])) {
-                rg_antireplay_mark_seen(r, ctr[i]);
-                // decrypt_packet after the AEAD (rustyguard-core/src/lib.rs:664-678): the endpoint
-                // moves only for an authenticated packet (whitepaper §6.5), and the first
-                // authenticated packet of a quiet session asks for a keepalive
-                uint8_t fl = RG_RECV_AUTHENTICATED;
-                if (x.sent + kKeepaliveTimeout < s->now && !x.keepalive_pending) {
-                    x.keepalive_pending = true;
-                    fl |= RG_RECV_KEEPALIVE;
-                }
-                if (src) {
-                    x.endpoint = src[i];
-                    x.has_endpoint = true;
-                }
-                if (flags_out) flags_out[i] = fl;
-            } else {
-                // a second copy of a counter accepted earlier in this batch, or one the window
-                // has moved past since: the reference rejects it before decrypting
-                // (prim.rs:420-423), so the GPU's plaintext is put back to ciphertext
-                status[i] = RG_PKT_REJECTED;
+        uint8_t st = host_status[i] != 0xFF ? host_status[i] : status[i];
+        // a frame that reached the session (GPU verdict, or too short for a tag) takes the
+        // in-order window check first: a second copy of a counter accepted earlier in this
+        // batch, or one the window has moved past since, is Rejected before decrypting
+        // (prim.rs:420-423), and a GPU plaintext there is put back to ciphertext
+        if (slot_of[i] != 0xFFFFFFFFu && (st == RG_PKT_OK || st == RG_PKT_DECRYPT_ERR)) {
+            uint8_t fl;
+            bool back;
+            st = replay_step(s, slot_of[i], ctr[i], st, src, i, &fl, &back);
+            if (flags_out) flags_out[i] = fl;
+            if (back) {
                 undo.push_back(rg_pkt_desc{d[i].offset, d[i].len - 32, d[i].key_idx});
                 undo_ctr.push_back(ctr[i]);
             }
         }
+        status[i] = st;
         if (slots_out) slots_out[i] = slot_of[i];
     }
     if (!undo.empty()) {
@@ -1063,6 +1177,156 @@ int rg_recv_batch_ex(rg_sessions *s, const rg_pkt_desc *desc, size_t n, uint8_t 
         for (uint8_t x : st2)
             if (x != RG_PKT_OK) return set_err(RG_EDEVICE, "recv_batch: restoring a replayed frame failed");
     }
+    return RG_OK;
+}
+
+int rg_send_batch_dev(rg_sessions *s, const uint32_t *slots, const rg_pkt_desc *desc, size_t n, uint8_t *buf,
+                      size_t buf_len, uint8_t *status, uint8_t *rekey_out, void *stream) {
+    if (!s || !slots || !desc || !buf) return set_err(RG_EINVAL, "send_batch_dev: bad args");
+    if (n > 0xFFFFFFFFull) return set_err(RG_EINVAL, "send_batch_dev: too many packets");
+    if (n == 0) return RG_OK;
+    int rc = check_ctx(s->ctx);
+    if (rc) return rc;
+    rc = sync_tables(s);
+    if (rc) return rc;
+    SessDev &D = s->dev;
+    SendStage &g = D.send[D.send_next];
+    D.send_next ^= 1;
+    RG_HIP(ensure_event(g.ev), "send event");
+    RG_HIP(hipEventSynchronize(g.ev), "send staging"); // the stage's previous batch has been sealed
+    RG_HIP(g.h_kidx.reserve(n * 4), "alloc send staging");
+    RG_HIP(g.h_ctr.reserve(n * 8), "alloc send staging");
+    RG_HIP(g.d_kidx.reserve(n * 4), "alloc send key rows");
+    RG_HIP(g.d_ctr.reserve(n * 8), "alloc send counters");
+    RG_HIP(g.d_desc.reserve(n * sizeof(rg_pkt_desc)), "alloc send descriptors");
+    uint32_t *kx = static_cast<uint32_t *>(g.h_kidx.p);
+    uint64_t *cx = static_cast<uint64_t *>(g.h_ctr.p);
+    // rg_send_batch's session checks, in array order; the lengths live on the device, so a
+    // frame with P % 16 != 0 takes its counter and the kernel reports it RG_PKT_INVALID
+    for (size_t i = 0; i < n; ++i) {
+        if (rekey_out) rekey_out[i] = 0;
+        const uint32_t slot = slots[i];
+        kx[i] = RG_KEY_SKIP; // the kernel reports RG_PKT_REJECTED
+        cx[i] = 0;
+        if (slot >= s->cap || !s->s[slot].used) continue;
+        Session &x = s->s[slot];
+        if (x.send_ctr >= RG_REJECT_AFTER_MESSAGES || x.started + kRejectAfterTime < s->now) continue;
+        cx[i] = x.send_ctr++; // EncryptionKey::encrypt, prim.rs:387-388
+        x.sent = s->now;      // force_encrypt, lib.rs:285
+        kx[i] = slot;
+        if (rekey_out && x.send_ctr >= RG_REKEY_AFTER_MESSAGES) rekey_out[i] = 1; // lib.rs:564-570
+    }
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    RG_HIP(hipMemcpyAsync(g.d_kidx.p, kx, n * 4, hipMemcpyHostToDevice, st), "H2D send key rows");
+    RG_HIP(hipMemcpyAsync(g.d_ctr.p, cx, n * 8, hipMemcpyHostToDevice, st), "H2D send counters");
+    auto *bd = static_cast<rg_pkt_desc *>(g.d_desc.p);
+    RG_HIP(rg::launch_bind_keys(desc, static_cast<const uint32_t *>(g.d_kidx.p), (uint32_t)n, bd, st), "bind launch");
+    rc = rg_seal_batch_dev(s->ctx, static_cast<const uint8_t *>(D.keys.p), static_cast<const uint32_t *>(D.recv.p),
+                           s->cap, bd, static_cast<const uint64_t *>(g.d_ctr.p), n, buf, buf_len, status, stream);
+    if (rc) return rc;
+    RG_HIP(hipEventRecord(g.ev, st), "send event record");
+    return RG_OK;
+}
+
+int rg_recv_batch_dev(rg_sessions *s, const rg_pkt_desc *desc, size_t n, uint8_t *buf, size_t buf_len,
+                      uint8_t *status, void *stream) {
+    if (!s || !desc || !buf || !status) return set_err(RG_EINVAL, "recv_batch_dev: bad args");
+    if (n > 0xFFFFFFFFull) return set_err(RG_EINVAL, "recv_batch_dev: too many packets");
+    RecvStage &R = s->dev.rv;
+    if (R.pending) return set_err(RG_EINVAL, "recv_batch_dev: finish the pending batch first");
+    int rc = check_ctx(s->ctx);
+    if (rc) return rc;
+    rc = sync_tables(s);
+    if (rc) return rc;
+    SessDev &D = s->dev;
+    RG_HIP(ensure_event(R.ev_meta), "recv event");
+    RG_HIP(ensure_event(R.ev_done), "recv event");
+    RG_HIP(hipEventSynchronize(R.ev_done), "recv staging"); // the previous batch's fix-ups are done
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    R.pending = true;
+    R.n = n;
+    R.st = st;
+    R.buf = buf;
+    R.buf_len = buf_len;
+    R.status = status;
+    if (n == 0) return RG_OK;
+    RG_HIP(R.d_rdesc.reserve(n * sizeof(rg_pkt_desc)), "alloc recv descriptors");
+    RG_HIP(R.d_ctr.reserve(n * 8), "alloc recv counters");
+    RG_HIP(R.d_key.reserve(n * 4), "alloc recv key rows");
+    RG_HIP(R.h_status.reserve(n), "alloc recv staging");
+    RG_HIP(R.h_ctr.reserve(n * 8), "alloc recv staging");
+    RG_HIP(R.h_key.reserve(n * 4), "alloc recv staging");
+    auto *rd = static_cast<rg_pkt_desc *>(R.d_rdesc.p);
+    RG_HIP(rg::launch_rx_resolve(desc, (uint32_t)n, buf, buf_len, static_cast<const rg_rx_entry *>(D.rx.p), D.rx_cap,
+                                 rd, static_cast<uint32_t *>(R.d_key.p), st),
+           "rx resolve launch");
+    rc = rg_open_batch_dev(s->ctx, static_cast<const uint8_t *>(D.keys.p), 2 * s->cap, rd, n, buf, buf_len, status,
+                           static_cast<uint64_t *>(R.d_ctr.p), stream);
+    if (rc) {
+        R.pending = false;
+        return rc;
+    }
+    RG_HIP(hipMemcpyAsync(R.h_status.p, status, n, hipMemcpyDeviceToHost, st), "D2H recv status");
+    RG_HIP(hipMemcpyAsync(R.h_ctr.p, R.d_ctr.p, n * 8, hipMemcpyDeviceToHost, st), "D2H recv counters");
+    RG_HIP(hipMemcpyAsync(R.h_key.p, R.d_key.p, n * 4, hipMemcpyDeviceToHost, st), "D2H recv key rows");
+    RG_HIP(hipEventRecord(R.ev_meta, st), "recv event record");
+    return RG_OK;
+}
+
+int rg_recv_batch_dev_finish(rg_sessions *s, const uint64_t *src, uint8_t *status_out, uint32_t *slots_out,
+                             uint8_t *flags_out) {
+    if (!s) return set_err(RG_EINVAL, "recv_batch_dev_finish: null");
+    RecvStage &R = s->dev.rv;
+    if (!R.pending) return set_err(RG_EINVAL, "recv_batch_dev_finish: no pending batch");
+    R.pending = false;
+    const size_t n = R.n;
+    if (n == 0) return RG_OK;
+    int rc = check_ctx(s->ctx);
+    if (rc) return rc;
+    RG_HIP(hipEventSynchronize(R.ev_meta), "recv metadata");
+    RG_HIP(R.h_fix.reserve(n), "alloc recv staging");
+    RG_HIP(R.h_idx.reserve(n * 4), "alloc recv staging");
+    const uint8_t *gs = static_cast<const uint8_t *>(R.h_status.p);
+    const uint64_t *cx = static_cast<const uint64_t *>(R.h_ctr.p);
+    const uint32_t *kx = static_cast<const uint32_t *>(R.h_key.p);
+    uint8_t *fx = static_cast<uint8_t *>(R.h_fix.p);
+    uint32_t *ix = static_cast<uint32_t *>(R.h_idx.p);
+    size_t m = 0;
+    bool changed = false;
+    for (size_t i = 0; i < n; ++i) {
+        uint8_t st = gs[i], fl = 0;
+        const uint32_t k = kx[i];
+        const uint32_t slot = k != RG_KEY_SKIP && k >= s->cap && k < 2 * s->cap ? k - s->cap : 0xFFFFFFFFu;
+        if (slot != 0xFFFFFFFFu && (st == RG_PKT_OK || st == RG_PKT_DECRYPT_ERR)) {
+            bool back;
+            const uint8_t st2 = replay_step(s, slot, cx[i], st, src, i, &fl, &back);
+            if (back) ix[m++] = (uint32_t)i;
+            changed |= st2 != st;
+            st = st2;
+        }
+        fx[i] = st;
+        if (status_out) status_out[i] = st;
+        if (slots_out) slots_out[i] = slot;
+        if (flags_out) flags_out[i] = fl;
+    }
+    hipStream_t st = R.st;
+    if (changed) RG_HIP(hipMemcpyAsync(R.status, fx, n, hipMemcpyHostToDevice, st), "H2D recv status");
+    if (m) {
+        // re-seal under the same key and nonce: ciphertext and tag come back byte for byte
+        RG_HIP(R.d_idx.reserve(m * 4), "alloc undo list");
+        RG_HIP(R.d_udesc.reserve(m * sizeof(rg_pkt_desc)), "alloc undo list");
+        RG_HIP(R.d_uctr.reserve(m * 8), "alloc undo list");
+        RG_HIP(hipMemcpyAsync(R.d_idx.p, ix, m * 4, hipMemcpyHostToDevice, st), "H2D undo list");
+        auto *ud = static_cast<rg_pkt_desc *>(R.d_udesc.p);
+        RG_HIP(rg::launch_undo_gather(static_cast<const rg_pkt_desc *>(R.d_rdesc.p),
+                                      static_cast<const uint64_t *>(R.d_ctr.p), static_cast<const uint32_t *>(R.d_idx.p),
+                                      (uint32_t)m, ud, static_cast<uint64_t *>(R.d_uctr.p), st),
+               "undo gather launch");
+        rc = rg_seal_batch_dev(s->ctx, static_cast<const uint8_t *>(s->dev.keys.p), nullptr, 2 * s->cap, ud,
+                               static_cast<const uint64_t *>(R.d_uctr.p), m, R.buf, R.buf_len, nullptr, st);
+        if (rc) return rc;
+    }
+    RG_HIP(hipEventRecord(R.ev_done, st), "recv event record");
     return RG_OK;
 }
 

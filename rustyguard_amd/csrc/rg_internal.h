@@ -242,6 +242,12 @@ __host__ __device__ __forceinline__ uint32_t rx_slot(uint32_t receiver, uint32_t
     return cap > 1 ? (receiver * 0x9E3779B1u) >> (32 - __builtin_ctz(cap)) : 0u;
 }
 hipError_t launch_general(GeneralJob *jobs, uint32_t njobs, uint8_t *arena, hipStream_t s);
+// device-resident session batches (rg_api.cpp): bind each packet to its key row; gather the
+// frames the host's anti-replay pass rejected into a re-seal list (len W -> P = W - 32)
+hipError_t launch_bind_keys(const rg_pkt_desc *in, const uint32_t *key_idx, uint32_t n, rg_pkt_desc *out,
+                            hipStream_t s);
+hipError_t launch_undo_gather(const rg_pkt_desc *rd, const uint64_t *ctr, const uint32_t *idx, uint32_t m,
+                              rg_pkt_desc *out, uint64_t *ctr_out, hipStream_t s);
 hipError_t launch_synth_fill(const rg_pkt_desc *desc, const uint32_t *inner_len, uint32_t n, uint8_t *buf,
                              uint64_t buf_len, uint64_t seed, hipStream_t s);
 

@@ -112,6 +112,47 @@ hipError_t launch_rx_resolve(const rg_pkt_desc *desc, uint32_t n, const uint8_t 
     return hipGetLastError();
 }
 
+// ------------------------------------------------- session device batches
+// rg_send_batch_dev: the caller's descriptors (offset, len) with the key row the
+// host chose for each packet (its session's send key, or RG_KEY_SKIP)
+__global__ __launch_bounds__(256) void bind_keys_kernel(const rg_pkt_desc *in, const uint32_t *key_idx, uint32_t n,
+                                                        rg_pkt_desc *out) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    rg_pkt_desc d = in[i];
+    d.key_idx = key_idx[i];
+    out[i] = d;
+}
+
+hipError_t launch_bind_keys(const rg_pkt_desc *in, const uint32_t *key_idx, uint32_t n, rg_pkt_desc *out,
+                            hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(bind_keys_kernel, dim3((n + 255) / 256), dim3(256), 0, s, in, key_idx, n, out);
+    return hipGetLastError();
+}
+
+// rg_recv_batch_dev_finish: frames opened on the GPU but rejected by the in-order
+// anti-replay pass go back to ciphertext by a re-seal under the same key and
+// nonce; their seal descriptors (P = W - 32) and counters from the open's outputs
+__global__ __launch_bounds__(256) void undo_gather_kernel(const rg_pkt_desc *rd, const uint64_t *ctr,
+                                                          const uint32_t *idx, uint32_t m, rg_pkt_desc *out,
+                                                          uint64_t *ctr_out) {
+    const uint32_t j = blockIdx.x * 256 + threadIdx.x;
+    if (j >= m) return;
+    const uint32_t i = idx[j];
+    rg_pkt_desc d = rd[i];
+    d.len -= 32;
+    out[j] = d;
+    ctr_out[j] = ctr[i];
+}
+
+hipError_t launch_undo_gather(const rg_pkt_desc *rd, const uint64_t *ctr, const uint32_t *idx, uint32_t m,
+                              rg_pkt_desc *out, uint64_t *ctr_out, hipStream_t s) {
+    if (m == 0) return hipSuccess;
+    hipLaunchKernelGGL(undo_gather_kernel, dim3((m + 255) / 256), dim3(256), 0, s, rd, ctr, idx, m, out, ctr_out);
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------------------- synth
 __global__ __launch_bounds__(256) void synth_fill_kernel(const rg_pkt_desc *desc, const uint32_t *inner_len,
                                                          uint32_t n, uint8_t *buf, uint64_t buf_len, uint64_t seed) {

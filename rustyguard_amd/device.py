@@ -31,13 +31,24 @@ class DeviceBatch:
         """Synthetic plaintext (see workloads.py) written on the device."""
         self.engine.synth_fill_dev(self.desc_seal, self.inner_len, self.buf, self.w.data_seed, stream=stream)
 
-    def seal(self, stream=None, with_header: bool = True, status: bool = True):
-        self.engine.seal_dev(self.keys, self.receivers if with_header else None, self.desc_seal, self.counters,
-                             self.buf, self.status if status else None, stream=stream)
+    def seal(self, stream=None, with_header: bool = True, status: bool = True, part=None, engine=None):
+        """Seal packets [a, b) when `part` = (a, b) (all of them by default), on `engine` (default: the
+        batch's).  Concurrent calls on different streams need different engines: an engine's planner
+        scratch is stream-ordered."""
+        a, b = part if part is not None else (0, self.w.n)
+        (engine or self.engine).seal_dev(self.keys, self.receivers if with_header else None, self.desc_seal[a:b],
+                                         self.counters[a:b], self.buf, self.status[a:b] if status else None,
+                                         stream=stream)
 
-    def open(self, stream=None, counters_out: bool = True):
-        self.engine.open_dev(self.keys, self.desc_open, self.buf, self.status,
-                             self.counters_out if counters_out else None, stream=stream)
+    def open(self, stream=None, counters_out: bool = True, part=None, engine=None):
+        a, b = part if part is not None else (0, self.w.n)
+        (engine or self.engine).open_dev(self.keys, self.desc_open[a:b], self.buf, self.status[a:b],
+                                         self.counters_out[a:b] if counters_out else None, stream=stream)
+
+    def parts(self, k: int):
+        """k contiguous packet ranges of near-equal size."""
+        n = self.w.n
+        return [(i * n // k, (i + 1) * n // k) for i in range(k)]
 
     def host_buf(self) -> np.ndarray:
         return self.buf.cpu().numpy()

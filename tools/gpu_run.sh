@@ -86,6 +86,14 @@ for s in "$@"; do
                 --kernel-trace --output-format csv -d gpurun_out/valu_$W -o p -- \
                 python3 bench.py --workload $W --steps 5 --warmup 2 --cpu-seconds 0 --no-cold ${RG_BENCH_FLAGS:-}
         done ;;
+    hbmcal)
+        # FETCH_SIZE / WRITE_SIZE / raw EA requests against known byte counts (1 GiB working set)
+        for k in rd_coal rd_frame wr_coal wr_frame wr_split; do
+            run hbmcal_fetch_$k 60 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/hbmcal/fetch_$k -o p -- tools/build/hbmcal $k
+            run hbmcal_write_$k 60 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/hbmcal/write_$k -o p -- tools/build/hbmcal $k
+            run hbmcal_ea_$k 60 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum --kernel-trace --output-format csv -d gpurun_out/hbmcal/ea_$k -o p -- tools/build/hbmcal $k
+        done
+        python3 tools/pmc_summary.py gpurun_out/hbmcal/* > gpurun_out/hbmcal_summary.txt 2>&1 || true ;;
     variants) each_variant bench_variant; summ gpurun_out/var_*.log ;;
     stamps_v) each_variant stamp_variant ;;
     pmc_clock) each_variant pmc_variant; python3 tools/pmc_clock.py gpurun_out/pmcclk_* ;;
