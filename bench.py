@@ -69,6 +69,8 @@ def parse():
     ap.add_argument("--plan", type=int, default=-1, help="size-class planner: 0 off, 1 on, 2 auto, -1 library default (auto)")
     ap.add_argument("--segments", type=int, default=0, help="segments per packet for the tile kernels (0 = auto)")
     ap.add_argument("--debug-mode", type=int, default=0, help="seal diagnostics (invalid output): 1 compute-only, 2 memory-only")
+    ap.add_argument("--frame-shift", type=int, default=0,
+                    help="diagnostics: add this many bytes (multiple of 16) to every frame offset")
     ap.add_argument("--split", type=int, default=1,
                     help="sub-batches per step: seal of part k+1 overlaps open of part k on a second stream")
     ap.add_argument("--no-graph", action="store_true", help="launch eagerly instead of replaying a captured HIP graph")
@@ -416,6 +418,10 @@ def main():
         w = workloads.build("cfg5", rank, world)  # strong split of the 8 Mi batch
     else:
         w = workloads.build(workload)
+    if args.frame_shift:  # layout experiment: every frame moved by the same 16-B multiple
+        assert args.frame_shift % 16 == 0
+        w.desc["offset"] += np.uint64(args.frame_shift)
+        w.buf_bytes += args.frame_shift
     b = DeviceBatch(eng, w)
     b.fill()
     torch.cuda.synchronize()

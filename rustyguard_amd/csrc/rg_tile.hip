@@ -365,7 +365,7 @@ __global__ __launch_bounds__(512) void tile_kernel(SealArgs sa, OpenArgs oa, Til
         const uint32_t b1 = 4 * c1 < nb ? 4 * c1 : nb;
         const uint32_t snb = b1 - b0;     // blocks of this segment
         const uint32_t segC = c1 - c0;
-        // ---- tile addressing: buffer descriptor based at the lowest frame of the tile
+        // ---- tile addressing: buffer descriptor based at the 128-byte line of the lowest frame
         uint64_t lo = work ? d.offset : ~0ull;
 #pragma unroll
         for (int m = 32; m >= 1; m >>= 1) {
@@ -374,14 +374,30 @@ __global__ __launch_bounds__(512) void tile_kernel(SealArgs sa, OpenArgs oa, Til
         }
         lo = uniform_u64(lo);
         if (lo == ~0ull) lo = 0;
+        lo &= ~127ull;
         const uint64_t span_cap = buf_len - lo;
         const uint32_t nrec = span_cap > kOOB ? kOOB : (uint32_t)span_cap;
         const v4i rsrc = make_rsrc(buf + lo, nrec);
         const bool addressable = work && d.offset - lo + 16 + (uint64_t)P <= nrec;
-        // segment payload base relative to the descriptor (kOOB if unusable)
-        const uint32_t my_base = addressable ? (uint32_t)(d.offset - lo) + 16 + 64 * c0 : kOOB;
         const uint32_t myC = addressable ? segC : 0;
-        uint32_t Wl = (myC + G - 1) / G;
+        // Window phase: windows are PPW 16-byte pieces that start SH pieces before the segment's
+        // first payload block.  When every lane's segment starts at the same phase inside a
+        // PPW-piece line (fixed-stride frames: payload at +16 of a 128-byte aligned frame gives
+        // SH = 1), SH is that phase and every window is whole 128-byte lines: each line is
+        // fetched and written once.  Otherwise SH = 0 (windows follow the payload; lines at
+        // window seams are fetched by two windows).
+        const uint32_t ph = (uint32_t)((d.offset + 16 + 64ull * c0) >> 4) & (PPW - 1);
+        uint32_t ph_lo = myC ? ph : PPW, ph_hi = myC ? ph : 0u;
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) {
+            ph_lo = min(ph_lo, (uint32_t)__shfl_xor((int)ph_lo, m));
+            ph_hi = max(ph_hi, (uint32_t)__shfl_xor((int)ph_hi, m));
+        }
+        const uint32_t SH = uniform_u32(ph_lo == ph_hi ? ph_lo : 0u);
+        // window base of the segment relative to the descriptor (kOOB if unusable): the payload
+        // base minus SH pieces, never below the tile's line base (SH > 0 is the lane's own phase)
+        const uint32_t my_base = addressable ? (uint32_t)(d.offset - lo) + 16 + 64 * c0 - 16 * SH : kOOB;
+        uint32_t Wl = myC ? (SH + snb + PPW - 1) / PPW : 0u;
 #pragma unroll
         for (int m = 32; m >= 1; m >>= 1) {
             const uint32_t o = __shfl_xor(Wl, m);
@@ -389,8 +405,9 @@ __global__ __launch_bounds__(512) void tile_kernel(SealArgs sa, OpenArgs oa, Til
         }
         const uint32_t W = uniform_u32(Wl);
         // DMA/store address table: instruction q serves lane pq = q*PKT_PER_INST + lane/PPW,
-        // piece k = (lane % PPW) ^ swz(pq)
-        uint32_t tb[PPW], tlim[PPW];
+        // piece k = (lane % PPW) ^ swz(pq) of each window; that piece is payload block
+        // PPW w + k - SH of the segment, valid iff tlo <= PPW w < thi
+        uint32_t tb[PPW], tlo[PPW], thi[PPW];
 #pragma unroll
         for (uint32_t q = 0; q < PPW; ++q) {
             const uint32_t pq = q * Cfg::PKT_PER_INST + lane / PPW;
@@ -398,7 +415,8 @@ __global__ __launch_bounds__(512) void tile_kernel(SealArgs sa, OpenArgs oa, Til
             const uint32_t b = __shfl(my_base, pq);
             const uint32_t blocks = __shfl(myC == 0 ? 0u : snb, pq);
             tb[q] = b == kOOB ? kOOB : b + 16 * k;
-            tlim[q] = blocks > k ? blocks - k : 0; // piece valid in window w iff w*PPW < tlim
+            tlo[q] = SH > k ? SH - k : 0u;
+            thi[q] = blocks + SH > k ? blocks + SH - k : 0u;
         }
         // ---- key and one-time Poly1305 key (block 0)
         const uint32_t n1 = (uint32_t)ctr, n2 = (uint32_t)(ctr >> 32);
@@ -411,7 +429,7 @@ __global__ __launch_bounds__(512) void tile_kernel(SealArgs sa, OpenArgs oa, Til
         Acc acc = {0, 0, 0, 0, 0};
 
         auto voff_of = [&](uint32_t q, uint32_t w) -> uint32_t {
-            return (tb[q] != kOOB && w * PPW < tlim[q]) ? tb[q] + w * PPW * 16 : kOOB;
+            return (tb[q] != kOOB && w * PPW >= tlo[q] && w * PPW < thi[q]) ? tb[q] + w * PPW * 16 : kOOB;
         };
         auto issue_dma = [&](uint32_t w) {
             const uint32_t lbase = lds_wave + (w & 1) * Cfg::BUF;
@@ -449,61 +467,52 @@ __global__ __launch_bounds__(512) void tile_kernel(SealArgs sa, OpenArgs oa, Til
         constexpr bool TRACK = decltype(track_tag)::value;
         uint32_t ksc[16];
         if (Cmax > 0) stream_block(stm, c0 + 1, ksc);
+        // Window schedule (wave-uniform): DMA(0), DMA(1) up front; before chunk c, wait for the
+        // highest window it touches; after it, each window the next chunk no longer touches is
+        // stored and its buffer refilled with the window two ahead.  Issue order is therefore
+        // D0 D1 S0 D2 S1 D3 ..., so the ops younger than D(w) when it is awaited are none, or
+        // S(w-1) and D(w+1) once window w-1 has been released.
+        int have = -1;     // highest window whose DMA has been awaited
+        uint32_t low = 0;  // lowest window still held in LDS
+        if (W > 0) {
+            issue_dma(0);
+            if (W > 1) issue_dma(1);
+        }
         for (uint32_t c = 0; c < Cmax; ++c) {
-            const uint32_t w = c / G, cl = c % G;
-            if (cl == 0) { // window boundary (wave-uniform)
-                if constexpr (STAMP) {
-                    const uint64_t t = stamp();
-                    t_chunk += t - t_mark;
-                    t_mark = t;
-                }
-                if (w > 0) store_window(w - 1);
-                if constexpr (STAMP) {
-                    const uint64_t t = stamp();
-                    t_store += t - t_mark;
-                    t_mark = t;
-                }
-                const bool more = w + 1 < W;
-                if (w == 0) {
-                    issue_dma(0);
-                    if (more) issue_dma(1);
-                } else if (more) {
-                    issue_dma(w + 1);
-                }
-                if constexpr (STAMP) {
-                    const uint64_t t = stamp();
-                    t_issue += t - t_mark;
-                    t_mark = t;
-                }
-                if (w == 0) {
-                    if (more) wait_vm<PPW>();
-                    else wait_vm<0>();
-                } else {
-                    // wait for DMA(w); younger: stores(w-1) and DMA(w+1)
-                    if (more) wait_vm<2 * PPW>();
-                    else wait_vm<PPW>();
-                }
-                if constexpr (STAMP) {
-                    const uint64_t t = stamp();
-                    t_wait += t - t_mark;
-                    t_mark = t;
-                }
+            const uint32_t g0 = 4 * c + SH; // window-sequence piece of the chunk's first block
+            const uint32_t need = min((g0 + 3) / PPW, W - 1);
+            if constexpr (STAMP) {
+                const uint64_t t = stamp();
+                t_chunk += t - t_mark;
+                t_mark = t;
             }
-            uint4 *win = lds4 + (w & 1) * (Cfg::BUF / 16);
+            while (have < (int)need) {
+                ++have;
+                const uint32_t w = (uint32_t)have;
+                const uint32_t younger = w == 0 ? (W > 1 ? PPW : 0u) : (low >= w ? (w + 1 < W ? 2 * PPW : PPW) : 0u);
+                if (younger == 0) wait_vm<0>();
+                else if (younger == PPW) wait_vm<PPW>();
+                else wait_vm<2 * PPW>();
+            }
+            if constexpr (STAMP) {
+                const uint64_t t = stamp();
+                t_wait += t - t_mark;
+                t_mark = t;
+            }
             // blocks of this chunk that belong to the segment (0..4)
             const uint32_t cnt4 = c < myC ? (snb - 4 * c < 4 ? snb - 4 * c : 4) : 0;
-            const uint32_t sl0 = lane * PPW + ((4 * cl + 0) ^ f);
-            const uint32_t sl1 = lane * PPW + ((4 * cl + 1) ^ f);
-            const uint32_t sl2 = lane * PPW + ((4 * cl + 2) ^ f);
-            const uint32_t sl3 = lane * PPW + ((4 * cl + 3) ^ f);
-            const uint4 m0 = win[sl0], m1 = win[sl1], m2 = win[sl2], m3 = win[sl3];
+            auto slot_of = [&](uint32_t g) -> uint32_t {
+                return ((g / PPW) & 1) * (Cfg::BUF / 16) + lane * PPW + ((g % PPW) ^ f);
+            };
+            const uint32_t sl0 = slot_of(g0), sl1 = slot_of(g0 + 1), sl2 = slot_of(g0 + 2), sl3 = slot_of(g0 + 3);
+            const uint4 m0 = lds4[sl0], m1 = lds4[sl1], m2 = lds4[sl2], m3 = lds4[sl3];
             if (c + 1 == Cmax) { // last chunk: no next keystream block to overlap with
                 const uint4 x0 = xor4(m0, ksc + 0), x1 = xor4(m1, ksc + 4), x2 = xor4(m2, ksc + 8),
                             x3 = xor4(m3, ksc + 12);
-                win[sl0] = x0;
-                win[sl1] = x1;
-                win[sl2] = x2;
-                win[sl3] = x3;
+                lds4[sl0] = x0;
+                lds4[sl1] = x1;
+                lds4[sl2] = x2;
+                lds4[sl3] = x3;
                 acc_block_pred(acc, OPEN ? m0 : x0, r, cnt4 > 0);
                 acc_block_pred(acc, OPEN ? m1 : x1, r, cnt4 > 1);
                 acc_block_pred(acc, OPEN ? m2 : x2, r, cnt4 > 2);
@@ -514,37 +523,55 @@ __global__ __launch_bounds__(512) void tile_kernel(SealArgs sa, OpenArgs oa, Til
                     acc_mul_pred(pw, r, cnt4 > 2);
                     acc_mul_pred(pw, r, cnt4 > 3);
                 }
-                break;
-            }
-            // XOR + write-back after double round 0, Poly1305 blocks after 1, 3, 5, 7
-            uint4 x0, x1, x2, x3;
-            uint32_t ksn[16];
-            stream_block_hooked(stm, c0 + c + 2, ksn, [&](int dr) {
-                if (dr == 0) {
-                    x0 = xor4(m0, ksc + 0);
-                    x1 = xor4(m1, ksc + 4);
-                    x2 = xor4(m2, ksc + 8);
-                    x3 = xor4(m3, ksc + 12);
-                    win[sl0] = x0; // pieces outside the payload are never stored
-                    win[sl1] = x1;
-                    win[sl2] = x2;
-                    win[sl3] = x3;
-                }
-                if (dr == 1) acc_block_pred(acc, OPEN ? m0 : x0, r, cnt4 > 0);
-                if (dr == 3) acc_block_pred(acc, OPEN ? m1 : x1, r, cnt4 > 1);
-                if (dr == 5) acc_block_pred(acc, OPEN ? m2 : x2, r, cnt4 > 2);
-                if (dr == 7) acc_block_pred(acc, OPEN ? m3 : x3, r, cnt4 > 3);
-                if (dr % 2 == 1) pin_acc(acc);
-                if constexpr (TRACK) {
-                    if (dr == 2) acc_mul_pred(pw, r, cnt4 > 0);
-                    if (dr == 4) acc_mul_pred(pw, r, cnt4 > 1);
-                    if (dr == 6) acc_mul_pred(pw, r, cnt4 > 2);
-                    if (dr == 8) acc_mul_pred(pw, r, cnt4 > 3);
-                    if (dr % 2 == 0 && dr > 0) pin_acc(pw);
-                }
-            });
+            } else {
+                // XOR + write-back after double round 0, Poly1305 blocks after 1, 3, 5, 7
+                uint4 x0, x1, x2, x3;
+                uint32_t ksn[16];
+                stream_block_hooked(stm, c0 + c + 2, ksn, [&](int dr) {
+                    if (dr == 0) {
+                        x0 = xor4(m0, ksc + 0);
+                        x1 = xor4(m1, ksc + 4);
+                        x2 = xor4(m2, ksc + 8);
+                        x3 = xor4(m3, ksc + 12);
+                        lds4[sl0] = x0; // pieces outside the payload are never stored
+                        lds4[sl1] = x1;
+                        lds4[sl2] = x2;
+                        lds4[sl3] = x3;
+                    }
+                    if (dr == 1) acc_block_pred(acc, OPEN ? m0 : x0, r, cnt4 > 0);
+                    if (dr == 3) acc_block_pred(acc, OPEN ? m1 : x1, r, cnt4 > 1);
+                    if (dr == 5) acc_block_pred(acc, OPEN ? m2 : x2, r, cnt4 > 2);
+                    if (dr == 7) acc_block_pred(acc, OPEN ? m3 : x3, r, cnt4 > 3);
+                    if (dr % 2 == 1) pin_acc(acc);
+                    if constexpr (TRACK) {
+                        if (dr == 2) acc_mul_pred(pw, r, cnt4 > 0);
+                        if (dr == 4) acc_mul_pred(pw, r, cnt4 > 1);
+                        if (dr == 6) acc_mul_pred(pw, r, cnt4 > 2);
+                        if (dr == 8) acc_mul_pred(pw, r, cnt4 > 3);
+                        if (dr % 2 == 0 && dr > 0) pin_acc(pw);
+                    }
+                });
 #pragma unroll
-            for (int t = 0; t < 16; ++t) ksc[t] = ksn[t];
+                for (int t = 0; t < 16; ++t) ksc[t] = ksn[t];
+            }
+            if constexpr (STAMP) {
+                const uint64_t t = stamp();
+                t_chunk += t - t_mark;
+                t_mark = t;
+            }
+            // release the windows the next chunk does not touch (all of them after the last)
+            const uint32_t next_low = c + 1 < Cmax ? (g0 + 4) / PPW : W;
+            if (c + 1 == Cmax && (int)W - 1 > have) wait_vm<0>(); // never store a window in flight
+            while (low < next_low) {
+                store_window(low);
+                if (low + 2 < W) issue_dma(low + 2);
+                ++low;
+            }
+            if constexpr (STAMP) {
+                const uint64_t t = stamp();
+                t_store += t - t_mark;
+                t_mark = t;
+            }
         }
         };
         const bool track = K > 1 && seg > 0; // wave-uniform
@@ -555,7 +582,6 @@ __global__ __launch_bounds__(512) void tile_kernel(SealArgs sa, OpenArgs oa, Til
             t_chunk += t - t_mark;
             t_mark = t;
         }
-        if (W > 0) store_window(W - 1);
         wait_vm<0>(); // this tile's stores drained before the tail touches the frames
         if (work && !addressable) {
             // frame outside the tile's 32-bit buffer window (tiles of far-apart

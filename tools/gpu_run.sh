@@ -75,9 +75,9 @@ for s in "$@"; do
         # separate passes: FETCH_SIZE and WRITE_SIZE do not fit one pass; never combined with tracing domains
         W=${RG_WORKLOAD:-cfg2}
         run pmc_fetch_$W 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch_$W -o p -- \
-            python3 bench.py --workload $W --steps 5 --warmup 2 --cpu-seconds 0 --no-cold
+            python3 bench.py --workload $W --steps 5 --warmup 2 --cpu-seconds 0 --no-cold ${RG_BENCH_FLAGS:-}
         run pmc_write_$W 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write_$W -o p -- \
-            python3 bench.py --workload $W --steps 5 --warmup 2 --cpu-seconds 0 --no-cold ;;
+            python3 bench.py --workload $W --steps 5 --warmup 2 --cpu-seconds 0 --no-cold ${RG_BENCH_FLAGS:-} ;;
     valu)
         # issue counters of the transport kernels (one pass: 8 SQ + 2 GRBM), per BASELINE config
         for W in ${RG_WORKLOADS:-cfg2 cfg3 cfg4}; do
