@@ -88,8 +88,13 @@ def parse():
 
 
 def kernel_label(args, eng, w) -> str:
-    k = eng.kernel_for(w.n)
+    k = eng.last_kernel()  # the family the timed launches actually ran
+    if k < 0:
+        k = eng.kernel_for(w.n)
     plan = ({0: "off", 1: "on"}).get(args.plan, "auto")
+    if k == 3:
+        return (f"flattened chunk stream (units of equal work cut inside the kernel, chunks dealt evenly "
+                f"over 64 lanes), planner {plan}")
     if k == 0:
         return (f"pipelined lanes ({eng.lanes_per_packet(w.n)} lane(s)/packet without plan, 3 chunks in flight, "
                 f"Poly1305 in keystream rounds), planner {plan}")

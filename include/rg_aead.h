@@ -158,10 +158,18 @@ int rg_set_wg_per_cu(rg_ctx *ctx, int wg_per_cu);
  * 0 = pipelined lane kernel (one packet -- or one of lanes_per_packet
  * contiguous segments -- per lane, 3 chunks in flight, Poly1305 folded
  * into the keystream rounds); 1/2 = LDS-staged tiles (one packet (segment) per
- * lane, coalesced LDS-DMA windows of that many 64-byte chunks). */
+ * lane, coalesced LDS-DMA windows of that many 64-byte chunks); 3 = flattened
+ * chunk stream (a wave takes a run of whole packets of equal total work and
+ * deals their 64-byte chunks evenly over its lanes; Poly1305 partial sums are
+ * combined per packet in LDS). */
 int rg_set_staged(rg_ctx *ctx, int kernel);
-/* The kernel family a batch of n packets runs on (0, 1 or 2; see above). */
+/* The kernel family a batch of n packets runs on (0, 1 or 2; see above).  In automatic mode a
+ * small batch whose sizes are mixed (the last planned batch of the same planner -- the device API's,
+ * or a host pipeline slot's -- held more than one size class) runs family 3 instead, the flattened
+ * chunk stream (rg_set_staged(ctx, 3) forces it); every 32nd such call re-plans on family 0. */
 int rg_get_kernel(rg_ctx *ctx, size_t n);
+/* The family the most recent batched launch on this context ran (-1 before any). */
+int rg_last_kernel(rg_ctx *ctx);
 /* A device-side planner can first sort the batch into size classes so that
  * every 64-lane tile holds packets of similar length (both kernel families;
  * the pipelined kernel then also picks segments per class by an estimated

@@ -40,6 +40,7 @@ SIGNATURES = {
     "rg_open_batch_dev_rx": (c_int, [c_vp, c_vp, ctypes.c_uint32, c_vp, ctypes.c_uint32, c_vp, c_size, c_vp, c_size,
                                      c_vp, c_vp, c_vp, c_vp]),
     "rg_get_kernel": (c_int, [c_vp, c_size]),
+    "rg_last_kernel": (c_int, [c_vp]),
     "rg_set_plan": (c_int, [c_vp, c_int]),
     "rg_set_segments": (c_int, [c_vp, c_int]),
     "rg_set_debug_buffer": (c_int, [c_vp, c_vp]),

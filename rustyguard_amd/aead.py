@@ -120,6 +120,10 @@ class Engine:
         """The kernel family a batch of n packets runs on (rg_get_kernel)."""
         return check(self._L.rg_get_kernel(self._h, n), "rg_get_kernel")
 
+    def last_kernel(self) -> int:
+        """The kernel family the most recent batched launch ran (rg_last_kernel; -1 before any)."""
+        return self._L.rg_last_kernel(self._h)
+
     def set_plan(self, mode):
         """Size-class planner before the batched kernels: 0/False off, 1/True on, 2 auto (default)."""
         check(self._L.rg_set_plan(self._h, int(mode)), "rg_set_plan")

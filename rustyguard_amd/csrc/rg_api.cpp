@@ -155,6 +155,7 @@ struct rg_ctx {
     int staged_g = -1; // -1 auto, 0 pipelined lane kernel, 1/2 LDS-staged tile windows of G chunks
     int plan = 2;     // size-class planner: 0 off (array order), 1 always, 2 auto (skip for single-class batches)
     int segments = 0; // segments per packet: 0 = automatic, else 1 / 2 / 4
+    int last_kernel = -1; // kernel family of the latest batched launch (-1: none yet)
     PlanBuf plan_dev; // planner lists of the device API (calls on one ctx are stream-ordered)
     uint64_t *dbg = nullptr; // diagnostics buffer (device), stamp builds only
     int pipe_max_wg[2] = {0, 0}; // [seal, open] resident workgroups per CU of the pipelined kernel
@@ -311,6 +312,11 @@ int rg_get_kernel(rg_ctx *ctx, size_t n) {
     return n < (size_t)(ctx->cus > 0 ? ctx->cus : 256) * 512 ? 0 : 2;
 }
 
+int rg_last_kernel(rg_ctx *ctx) {
+    if (!ctx) return set_err(RG_EINVAL, "null context");
+    return ctx->last_kernel;
+}
+
 static rg::Launch launch_cfg(rg_ctx *ctx, size_t n, bool open) {
     rg::Launch L;
     L.lanes = rg_get_lanes_per_packet(ctx, n);
@@ -405,9 +411,25 @@ static hipError_t launch_flat_any(rg_ctx *ctx, const rg::SealArgs *sa, const rg:
     return rg::launch_flat(sa, oa, ctx->plan != 0, static_cast<uint4 *>(ctx->d_junk.p), ctx->cus, st);
 }
 
+// Automatic choice between the two small-batch kernels: when the last planned batch of this planner
+// held more than one size class (mixed sizes, e.g. IMIX), the flattened chunk stream runs -- it
+// balances mixed sizes inside the kernel, without a planner pass; every 32nd call goes back to the
+// planned pipelined kernel, whose planner refreshes the class count (a uniform batch returns there).
+static int pick_family(rg_ctx *ctx, int g, PlanBuf &pb) {
+    if (ctx->staged_g >= 0 || g != 0 || ctx->plan != 2 || !pb.h_classes) return g;
+    const uint32_t cls = *pb.h_classes;
+    if (cls >= 2 && cls != ~0u && (pb.calls % 32) != 0) {
+        ++pb.calls;
+        return 3;
+    }
+    return g;
+}
+
 static hipError_t launch_seal_any(rg_ctx *ctx, const rg::SealArgs &a0, PlanBuf &pb, hipStream_t st) {
     rg::SealArgs a = a0;
-    const rg::Launch L = launch_cfg(ctx, a.n, false);
+    rg::Launch L = launch_cfg(ctx, a.n, false);
+    L.staged_g = pick_family(ctx, L.staged_g, pb);
+    ctx->last_kernel = L.staged_g;
     // stamps: debug mode 3, or any diagnostic mode of the pipelined kernel
     a.dbg = L.debug_mode == 3 || (L.staged_g == 0 && L.debug_mode != 0) ? ctx->dbg : nullptr;
     if (L.staged_g == 3) return launch_flat_any(ctx, &a, nullptr, st);
@@ -417,7 +439,9 @@ static hipError_t launch_seal_any(rg_ctx *ctx, const rg::SealArgs &a0, PlanBuf &
 
 static hipError_t launch_open_any(rg_ctx *ctx, const rg::OpenArgs &a0, PlanBuf &pb, hipStream_t st) {
     rg::OpenArgs a = a0;
-    const rg::Launch L = launch_cfg(ctx, a.n, true);
+    rg::Launch L = launch_cfg(ctx, a.n, true);
+    L.staged_g = pick_family(ctx, L.staged_g, pb);
+    ctx->last_kernel = L.staged_g;
     a.dbg = L.debug_mode == 3 ? ctx->dbg : nullptr;
     if (L.staged_g == 3) return launch_flat_any(ctx, nullptr, &a, st);
     if (L.staged_g == 0) return launch_pipe_any(ctx, nullptr, &a, pb, L, st);

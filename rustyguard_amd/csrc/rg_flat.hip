@@ -59,7 +59,10 @@ __device__ __forceinline__ uint32_t flat_work(const rg_pkt_desc &d, bool open) {
 // -------------------------------------------------------------- LDS image
 // One per wave, one record set per packet of the sub-unit, laid out so that a
 // lane moving on to the next packet issues all its LDS reads at once.
-constexpr uint32_t kFlatMaxPk = 256;
+#ifndef RG_FLAT_MAX_PK
+#define RG_FLAT_MAX_PK 128 // packets per sub-unit (phase A holds their key loads in registers)
+#endif
+constexpr uint32_t kFlatMaxPk = RG_FLAT_MAX_PK;
 struct FlatLds {
     uint4 rec[kFlatMaxPk + 1];    // {offset lo, offset hi, nb | kLiveBit, cs}; rec[m].w = D
     uint32_t kr[kFlatMaxPk][16];  // key[8], counter lo/hi, r[4] (unclamped), desc len, desc key_idx
@@ -87,6 +90,9 @@ struct FChunk {
 // clamped inside the payload (always readable)
 __device__ __forceinline__ void fload(FChunk &c, const uint4 *pl, uint32_t t, uint32_t last) {
     const uint32_t b = 4 * t;
+#ifdef RG_FLAT_ABL_NOLOAD // diagnostics only: no payload loads (output invalid)
+    c.q0.x ^= b; c.q1.y ^= b; c.q2.z ^= b; c.q3.w ^= last; return;
+#endif
     c.q0 = pl[min(b + 0, last)];
     c.q1 = pl[min(b + 1, last)];
     c.q2 = pl[min(b + 2, last)];
@@ -113,8 +119,16 @@ __device__ __forceinline__ void fcur_from(FCur &p, const uint4 &rc, uint8_t *buf
 __device__ __forceinline__ bool fcur_next(FCur &p, const FlatLds &L, uint8_t *buf, uint32_t m) {
     if (++p.t < p.c) return false;
     uint32_t k = p.k + 1;
+    // one 16-byte LDS read on the common path (the next packet has chunks); packets without
+    // chunks (P = 0) are skipped by the rare loop
     uint4 rc = L.rec[k < m ? k : m];
-    while (k < m && (rc.z & ~kLiveBit) == 0) rc = L.rec[++k < m ? k : m];
+    asm volatile("" ::"v"(rc.x), "v"(rc.y), "v"(rc.z)); // all fields now: one ds_read_b128
+    if (k < m && (rc.z & ~kLiveBit) == 0) {
+        do {
+            ++k;
+            rc = L.rec[k < m ? k : m];
+        } while (k < m && (rc.z & ~kLiveBit) == 0);
+    }
     if (k < m) fcur_from(p, rc, buf, k, 0);
     else p.k = m; // past the sub-unit (keeps pl: loads stay readable)
     return true;
@@ -152,6 +166,7 @@ struct FLane {
     Mul pr;
     uint32_t pe;
     int pb;
+    uint32_t rn[4]; // seal: r of the compute cursor's packet, kept from its key read for the pk switch
 };
 
 // one square-and-multiply step of the carry power (pb is wave-uniform)
@@ -185,6 +200,9 @@ __device__ __forceinline__ void flat_step(FLane &s, FChunk &b, uint32_t j, FlatL
     if (active && s.cur.live) cnt = min(4u, s.cur.nb - 4 * s.cur.t);
     uint32_t ks[16];
     stream_block_hooked(s.st, s.cur.t + 1, ks, [&](int dr) {
+#ifdef RG_FLAT_ABL_NOPOLY // diagnostics only: no Poly1305 absorption (output invalid)
+        if (dr < 100) return;
+#endif
         if constexpr (OPEN) {
             if (dr == 1) acc_block_pred(s.h, b.q0, s.r, cnt > 0);
             if (dr == 3) acc_block_pred(s.h, b.q1, s.r, cnt > 1);
@@ -206,10 +224,15 @@ __device__ __forceinline__ void flat_step(FLane &s, FChunk &b, uint32_t j, FlatL
     });
     const FChunk x = {xor4(b.q0, ks + 0), xor4(b.q1, ks + 4), xor4(b.q2, ks + 8), xor4(b.q3, ks + 12)};
     uint4 *dst = const_cast<uint4 *>(s.cur.pl) + 4 * s.cur.t;
-    *(cnt > 0 ? dst + 0 : junk + 0) = x.q0;
-    *(cnt > 1 ? dst + 1 : junk + 1) = x.q1;
-    *(cnt > 2 ? dst + 2 : junk + 2) = x.q2;
-    *(cnt > 3 ? dst + 3 : junk + 3) = x.q3;
+#ifdef RG_FLAT_ABL_NOSTORE // diagnostics only: ciphertext not stored (output invalid)
+    if (s.cur.k == 0xFFFFFFFFu)
+#endif
+    {
+        *(cnt > 0 ? dst + 0 : junk + 0) = x.q0;
+        *(cnt > 1 ? dst + 1 : junk + 1) = x.q1;
+        *(cnt > 2 ? dst + 2 : junk + 2) = x.q2;
+        *(cnt > 3 ? dst + 3 : junk + 3) = x.q3;
+    }
     if constexpr (OPEN) {
         if (active && s.cur.t + 1 == s.cur.c) { // the packet's last chunk: its final piece
             if (s.cur.live) put_h(L, s.cur.k, s.h, lane);
@@ -219,8 +242,7 @@ __device__ __forceinline__ void flat_step(FLane &s, FChunk &b, uint32_t j, FlatL
         if (active && s.pk != s.cur.k) { // the pending packet ended in this lane: final piece
             if (s.pk < m) put_h(L, s.pk, s.h, lane);
             s.h = Acc{0, 0, 0, 0, 0};
-            const FKey q = fkey(L, s.cur.k);
-            s.r = make_mul(q.r[0], q.r[1], q.r[2], q.r[3]);
+            s.r = make_mul(s.rn[0], s.rn[1], s.rn[2], s.rn[3]); // r of cur.k, read at its switch
             s.pk = s.cur.k;
         }
         s.pi = x;
@@ -236,6 +258,9 @@ __device__ __forceinline__ void flat_step(FLane &s, FChunk &b, uint32_t j, FlatL
         const FKey q = fkey(L, s.cur.k);
         s.st = make_stream(q.key, 0u, q.n1, q.n2);
         if constexpr (OPEN) s.r = make_mul(q.r[0], q.r[1], q.r[2], q.r[3]);
+        else {
+            s.rn[0] = q.r[0]; s.rn[1] = q.r[1]; s.rn[2] = q.r[2]; s.rn[3] = q.r[3];
+        }
     }
 }
 
@@ -572,9 +597,11 @@ template <bool OPEN> __global__ __launch_bounds__(64 * kFlatWaves) void flat_ker
                 const FKey q = fkey(L, s.cur.k);
                 s.st = make_stream(q.key, 0u, q.n1, q.n2);
                 s.r = make_mul(q.r[0], q.r[1], q.r[2], q.r[3]);
+                s.rn[0] = q.r[0]; s.rn[1] = q.r[1]; s.rn[2] = q.r[2]; s.rn[3] = q.r[3];
             } else {
                 s.st = make_stream(Key8{{0, 0, 0, 0, 0, 0, 0, 0}}, 0u, 0u, 0u);
                 s.r = make_mul(0, 0, 0, 0);
+                s.rn[0] = s.rn[1] = s.rn[2] = s.rn[3] = 0;
             }
             s.h = Acc{0, 0, 0, 0, 0};
             s.pi = FChunk{};

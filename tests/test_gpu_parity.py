@@ -842,3 +842,33 @@ def test_aead_with_aad_reference_handshake_snapshot(engine):
     bad[31] ^= 1
     with pytest.raises(aead.DecryptionError):
         engine.chacha20poly1305_dec(key, nonce, bytes(bad), bytearray(), tag)
+
+
+def test_auto_routes_mixed_small_batches_to_flat():
+    """Automatic kernel choice (rg_get_kernel / rg_last_kernel): the first IMIX batch runs the planned
+    pipelined kernel, whose planner sees several size classes; the next ones run the flattened chunk
+    stream until the 32nd call re-plans.  Every route gives the same bytes."""
+    import torch
+
+    from rustyguard_amd.device import DeviceBatch
+
+    eng = aead.Engine(0)
+    w = workloads.imix(5000)
+    b = DeviceBatch(eng, w)
+    outs, fams = [], []
+    for _ in range(3):
+        b.fill()
+        b.seal()
+        fams.append(eng.last_kernel())
+        torch.cuda.synchronize()
+        outs.append(b.buf.cpu().numpy().copy())
+        b.open()
+        fams.append(eng.last_kernel())
+        torch.cuda.synchronize()
+        assert (b.status.cpu().numpy()[: w.n] == 0).all()
+    assert fams[0] == 0 and fams[1:] == [3] * 5  # the seal's planner already saw the mix
+    assert all(np.array_equal(outs[0], o) for o in outs[1:])
+    b.fill()
+    ref = b.host_buf()
+    oracle.seal_batch(w.keys, w.receivers, w.desc, w.counters, ref)
+    assert np.array_equal(outs[0], ref)
