@@ -538,7 +538,7 @@ def main():
     pmc = load_traffic(workload)
     traffic = None
     # only counters of the kernel family this run used (a kernel change makes them stale)
-    if pmc and pmc.get(dominant) and pmc[dominant].get("family") == eng.kernel_for(w.n):
+    if pmc and pmc.get(dominant) and pmc[dominant].get("family") == eng.last_kernel():
         traffic = pmc[dominant].get("hbm_bytes_per_launch")
 
     out = {

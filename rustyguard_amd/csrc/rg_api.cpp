@@ -201,6 +201,9 @@ int rg_create(int device, rg_ctx **out) {
         if (e == hipSuccess) e = rg::prepare_tile_kernels();
         if (e == hipSuccess) e = rg::prepare_pipe_kernels(c->pipe_max_wg);
         if (e == hipSuccess) e = rg::prepare_flat_kernels();
+        // the flattened kernel's store sink, allocated now: the automatic choice may first pick that
+        // kernel inside a stream capture (HIP graph), where allocation is not permitted
+        if (e == hipSuccess) e = c->d_junk.reserve(rg::flat_junk_bytes(c->cus));
         if (e != hipSuccess) {
             delete c;
             return set_err(RG_EDEVICE, "kernel setup", e);
@@ -414,11 +417,15 @@ static hipError_t launch_flat_any(rg_ctx *ctx, const rg::SealArgs *sa, const rg:
 // Automatic choice between the two small-batch kernels: when the last planned batch of this planner
 // held more than one size class (mixed sizes, e.g. IMIX), the flattened chunk stream runs -- it
 // balances mixed sizes inside the kernel, without a planner pass; every 32nd call goes back to the
-// planned pipelined kernel, whose planner refreshes the class count (a uniform batch returns there).
-static int pick_family(rg_ctx *ctx, int g, PlanBuf &pb) {
+// planned pipelined kernel, whose planner refreshes the class count (a uniform batch returns there),
+// except inside a stream capture: a captured graph replays one route, and it should be the fast one.
+static int pick_family(rg_ctx *ctx, int g, PlanBuf &pb, hipStream_t st) {
     if (ctx->staged_g >= 0 || g != 0 || ctx->plan != 2 || !pb.h_classes) return g;
     const uint32_t cls = *pb.h_classes;
-    if (cls >= 2 && cls != ~0u && (pb.calls % 32) != 0) {
+    if (cls < 2 || cls == ~0u) return g;
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cap) != hipSuccess) cap = hipStreamCaptureStatusNone;
+    if ((pb.calls % 32) != 0 || cap != hipStreamCaptureStatusNone) {
         ++pb.calls;
         return 3;
     }
@@ -428,7 +435,7 @@ static int pick_family(rg_ctx *ctx, int g, PlanBuf &pb) {
 static hipError_t launch_seal_any(rg_ctx *ctx, const rg::SealArgs &a0, PlanBuf &pb, hipStream_t st) {
     rg::SealArgs a = a0;
     rg::Launch L = launch_cfg(ctx, a.n, false);
-    L.staged_g = pick_family(ctx, L.staged_g, pb);
+    L.staged_g = pick_family(ctx, L.staged_g, pb, st);
     ctx->last_kernel = L.staged_g;
     // stamps: debug mode 3, or any diagnostic mode of the pipelined kernel
     a.dbg = L.debug_mode == 3 || (L.staged_g == 0 && L.debug_mode != 0) ? ctx->dbg : nullptr;
@@ -440,7 +447,7 @@ static hipError_t launch_seal_any(rg_ctx *ctx, const rg::SealArgs &a0, PlanBuf &
 static hipError_t launch_open_any(rg_ctx *ctx, const rg::OpenArgs &a0, PlanBuf &pb, hipStream_t st) {
     rg::OpenArgs a = a0;
     rg::Launch L = launch_cfg(ctx, a.n, true);
-    L.staged_g = pick_family(ctx, L.staged_g, pb);
+    L.staged_g = pick_family(ctx, L.staged_g, pb, st);
     ctx->last_kernel = L.staged_g;
     a.dbg = L.debug_mode == 3 ? ctx->dbg : nullptr;
     if (L.staged_g == 3) return launch_flat_any(ctx, nullptr, &a, st);

@@ -872,3 +872,28 @@ def test_auto_routes_mixed_small_batches_to_flat():
     ref = b.host_buf()
     oracle.seal_batch(w.keys, w.receivers, w.desc, w.counters, ref)
     assert np.array_equal(outs[0], ref)
+
+
+def test_flat_first_launch_inside_graph_capture():
+    """The flattened kernel's first launch on a context may happen inside a stream capture (the bench
+    captures its step into a HIP graph): nothing may be allocated there."""
+    import torch
+
+    from rustyguard_amd.device import DeviceBatch
+
+    eng = aead.Engine(0)
+    eng.set_staged(3)
+    w = workloads.imix(3000)
+    b = DeviceBatch(eng, w)
+    b.fill()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        b.seal()
+    g.replay()
+    torch.cuda.synchronize()
+    got = b.host_buf()
+    b.fill()
+    ref = b.host_buf()
+    oracle.seal_batch(w.keys, w.receivers, w.desc, w.counters, ref)
+    assert np.array_equal(got, ref)

@@ -30,6 +30,8 @@ def kind_of(name: str):
     if "staged_kernel<" in name or "tile_kernel<" in name:
         args = name.split("<", 1)[1].split(">", 1)[0].split(",")
         return "open" if args[1].strip() == "true" else "seal"
+    if "flat_kernel<" in name:
+        return "open" if name.split("<", 1)[1].startswith("true") else "seal"
     if "pipe_seal_kernel" in name:
         return "seal"
     if "pipe_open_kernel" in name:
@@ -41,19 +43,29 @@ def family_of(name: str) -> int:
     """rg_get_kernel value of a transport kernel: 0 pipelined lanes, 1/2 tile window."""
     if "pipe_" in name:
         return 0
+    if "flat_kernel<" in name:
+        return 3
     return int(name.split("<", 1)[1].split(",", 1)[0])
 
 
 def counter_means(d: str):
-    out = collections.defaultdict(lambda: collections.defaultdict(list))
+    """Per-dispatch means of each counter for seal and open, over the dispatches of the kernel family
+    that ran most often (automatic choice may route the first call of a run elsewhere)."""
+    out = collections.defaultdict(lambda: collections.defaultdict(lambda: collections.defaultdict(list)))
     names = {}
     for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
             k = kind_of(r["Kernel_Name"])
             if k:
-                out[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
-                names[k] = r["Kernel_Name"]
-    return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in out.items()}, names
+                fam = family_of(r["Kernel_Name"])
+                out[k][fam][r["Counter_Name"]].append(float(r["Counter_Value"]))
+                names[(k, fam)] = r["Kernel_Name"]
+    means, picked = {}, {}
+    for k, fams in out.items():
+        fam = max(fams, key=lambda x: max(len(v) for v in fams[x].values()))
+        means[k] = {c: sum(v) / len(v) for c, v in fams[fam].items()}
+        picked[k] = names[(k, fam)]
+    return means, picked
 
 
 def main():
