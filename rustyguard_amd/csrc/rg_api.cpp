@@ -162,10 +162,10 @@ struct rg_ctx {
     std::mutex mu;
     Slot slots[3]; // host pipeline: up to three slices in flight (H2D of one beside D2H of another)
     DevBuf d_keys, d_recv;
-    DevBuf d_general;  // per-message drop-in arena
+    DevBuf d_general;  // per-message drop-in arena: [job][aad][payload][tag]
+    HostBuf h_general; // its pinned host image (one H2D and one D2H per call)
     DevBuf d_rx_desc;  // rg_open_batch_dev_rx: resolved descriptors
     DevBuf d_mac_keys; // rg_mac_verify_batch_dev: per-key BLAKE2s states
-    DevBuf d_jobs;
     DevBuf d_junk; // flattened kernel: sink of the stores that are not payload (never read)
 };
 
@@ -238,7 +238,7 @@ void rg_destroy(rg_ctx *ctx) {
     ctx->d_general.release();
     ctx->d_rx_desc.release();
     ctx->d_mac_keys.release();
-    ctx->d_jobs.release();
+    ctx->h_general.release();
     ctx->d_junk.release();
     delete ctx;
 }
@@ -761,11 +761,16 @@ static int general_one(rg_ctx *ctx, bool dec, const uint8_t key[32], const uint8
         return set_err(RG_EINVAL, "aead: bad args");
     if (len > (64ull << 32)) return set_err(RG_EINVAL, "aead: message too long for a 32-bit block counter");
     std::lock_guard<std::mutex> g(ctx->mu);
+    // one pinned image of the device arena: the inputs are packed into it on the host, moved by one
+    // H2D copy, and the results come back by one D2H copy (pageable copies of each piece cost tens of
+    // microseconds apiece)
+    const size_t job_bytes = (sizeof(rg::GeneralJob) + 15) & ~15ull;
     const size_t aad_off = 0, pay_off = (aad_len + 15) & ~15ull, tag_off = pay_off + ((len + 15) & ~15ull);
-    const size_t arena = tag_off + 16;
+    const size_t arena = job_bytes + tag_off + 16;
     RG_HIP(ctx->d_general.reserve(arena), "alloc arena");
-    RG_HIP(ctx->d_jobs.reserve(sizeof(rg::GeneralJob)), "alloc job");
+    RG_HIP(ctx->h_general.reserve(arena), "alloc pinned arena");
     uint8_t *d = static_cast<uint8_t *>(ctx->d_general.p);
+    uint8_t *h = static_cast<uint8_t *>(ctx->h_general.p);
     rg::GeneralJob job;
     memset(&job, 0, sizeof job);
     memcpy(job.key, key, 32);
@@ -782,17 +787,22 @@ static int general_one(rg_ctx *ctx, bool dec, const uint8_t key[32], const uint8
     job.payload_off = pay_off;
     job.payload_len = len;
     job.tag_off = tag_off;
+    memcpy(h, &job, sizeof job);
+    uint8_t *hb = h + job_bytes; // arena base as the kernel sees it; padding zeroed (pad16)
+    memset(hb, 0, tag_off + 16);
+    if (aad_len) memcpy(hb + aad_off, aad, aad_len);
+    if (len) memcpy(hb + pay_off, payload, len);
+    if (dec) memcpy(hb + tag_off, tag, 16);
     hipStream_t st = ctx->slots[0].stream;
-    if (aad_len) RG_HIP(hipMemcpyAsync(d + aad_off, aad, aad_len, hipMemcpyHostToDevice, st), "H2D aad");
-    if (len) RG_HIP(hipMemcpyAsync(d + pay_off, payload, len, hipMemcpyHostToDevice, st), "H2D payload");
-    if (dec) RG_HIP(hipMemcpyAsync(d + tag_off, tag, 16, hipMemcpyHostToDevice, st), "H2D tag");
-    RG_HIP(hipMemcpyAsync(ctx->d_jobs.p, &job, sizeof job, hipMemcpyHostToDevice, st), "H2D job");
-    RG_HIP(rg::launch_general(static_cast<rg::GeneralJob *>(ctx->d_jobs.p), 1, d, st), "general launch");
-    RG_HIP(hipMemcpyAsync(&job, ctx->d_jobs.p, sizeof job, hipMemcpyDeviceToHost, st), "D2H job");
+    RG_HIP(hipMemcpyAsync(d, h, arena, hipMemcpyHostToDevice, st), "H2D arena");
+    RG_HIP(rg::launch_general(reinterpret_cast<rg::GeneralJob *>(d), 1, d + job_bytes, st), "general launch");
+    RG_HIP(hipMemcpyAsync(h, d, arena, hipMemcpyDeviceToHost, st), "D2H arena");
     RG_HIP(hipStreamSynchronize(st), "general sync");
+    memcpy(&job, h, sizeof job);
+    memset(h, 0, sizeof job); // the key does not stay in the pinned image
     if (dec && job.status != RG_PKT_OK) return RG_PKT_DECRYPT_ERR; // payload untouched
-    if (len) RG_HIP(hipMemcpy(payload, d + pay_off, len, hipMemcpyDeviceToHost), "D2H payload");
-    if (!dec) RG_HIP(hipMemcpy(tag, d + tag_off, 16, hipMemcpyDeviceToHost), "D2H tag");
+    if (len) memcpy(payload, hb + pay_off, len);
+    if (!dec) memcpy(tag, hb + tag_off, 16);
     return RG_OK;
 }
 

@@ -10,61 +10,95 @@
 namespace rg {
 
 // --------------------------------------------------------------- general
-// One lane per message, byte-granular: any nonce, any AAD, any length.  Used
-// by the per-message CryptoPrimatives drop-in (handshake-sized messages).
-__device__ void poly_bytes(Acc &h, const Mul &r, const uint8_t *p, uint64_t len) {
-    for (uint64_t off = 0; off < len; off += 16) {
-        uint32_t w[4] = {0, 0, 0, 0};
-        for (int b = 0; b < 16; ++b)
-            if (off + b < len) w[b >> 2] |= (uint32_t)p[off + b] << (8 * (b & 3));
-        acc_add(h, w[0], w[1], w[2], w[3], 1); // zero-padded to 16 (RFC 8439 §2.8 pad16)
-        acc_mul(h, r);
+// One wave per message: any nonce, any AAD, any length.  Used by the
+// per-message CryptoPrimatives drop-in (handshake-sized messages).  The host
+// packs each message into a job arena at 16-byte aligned offsets with zeroed
+// padding, so everything moves as 16-byte vectors: the lanes generate the
+// keystream blocks in parallel (lane b: blocks b + 1, b + 65, ...), lane 0
+// runs the Poly1305 Horner chain (RFC 8439 §2.8, pad16 of AAD and text).
+__device__ __forceinline__ uint4 mask_tail(uint4 v, uint64_t valid) { // keep bytes [0, valid) of 16
+    if (valid >= 16) return v;
+    uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int64_t keep = (int64_t)valid - 4 * q;
+        w[q] = keep >= 4 ? w[q] : keep <= 0 ? 0u : (w[q] & (0xFFFFFFFFu >> (32 - 8 * keep)));
+    }
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+__device__ void poly_vec(Acc &h, const Mul &r, const uint4 *p, uint64_t len) {
+    const uint64_t nb = (len + 15) / 16;
+    for (uint64_t b0 = 0; b0 < nb; b0 += 8) { // eight loads in flight, then the Horner chain
+        uint4 m[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) m[q] = p[min(b0 + q, nb - 1)];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            if (b0 + q >= nb) break;
+            const uint4 v = mask_tail(m[q], len - 16 * (b0 + q)); // zero-padded to 16 (pad16)
+            acc_add(h, v.x, v.y, v.z, v.w, 1);
+            acc_mul(h, r);
+        }
     }
 }
 
-__global__ void general_kernel(GeneralJob *jobs, uint32_t njobs, uint8_t *arena) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+// lanes XOR the keystream into the text: 64-byte chunk c uses block c + 1
+__device__ void xor_stream(const Key8 &key, const uint32_t nonce[3], uint4 *pl, uint64_t len, uint32_t lane) {
+    const uint64_t chunks = (len + 63) / 64;
+    for (uint64_t c = lane; c < chunks; c += 64) {
+        uint32_t ks[16];
+        chacha_block(key, (uint32_t)c + 1, nonce[0], nonce[1], nonce[2], ks);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint64_t off = 64 * c + 16 * q;
+            if (off >= len) break;
+            const uint4 x = xor4(pl[off / 16], ks + 4 * q);
+            pl[off / 16] = mask_tail(x, len - off); // bytes past the text stay zero
+        }
+    }
+}
+
+__global__ __launch_bounds__(64) void general_kernel(GeneralJob *jobs, uint32_t njobs, uint8_t *arena) {
+    const uint32_t i = blockIdx.x, lane = threadIdx.x;
     if (i >= njobs) return;
     GeneralJob &j = jobs[i];
     Key8 key;
     for (int t = 0; t < 8; ++t) key.k[t] = j.key[t];
     if (j.xchacha) key = hchacha20(key, j.hnonce); // XChaCha20-Poly1305 subkey (prim.rs:202-224)
-    uint32_t ks[16];
-    chacha_block(key, 0, j.nonce[0], j.nonce[1], j.nonce[2], ks);
-    const Mul r = make_mul(ks[0], ks[1], ks[2], ks[3]);
-    const uint32_t s0 = ks[4], s1 = ks[5], s2 = ks[6], s3 = ks[7];
-    uint8_t *pl = arena + j.payload_off;
+    const uint32_t nonce[3] = {j.nonce[0], j.nonce[1], j.nonce[2]};
+    uint4 *pl = reinterpret_cast<uint4 *>(arena + j.payload_off);
     const uint64_t len = j.payload_len;
-    Acc h = {0, 0, 0, 0, 0};
-    poly_bytes(h, r, arena + j.aad_off, j.aad_len);
+    __shared__ uint32_t verdict;
     if (!j.decrypt) {
-        for (uint64_t off = 0; off < len; off += 64) {
-            chacha_block(key, (uint32_t)(off / 64) + 1, j.nonce[0], j.nonce[1], j.nonce[2], ks);
-            for (int b = 0; b < 64 && off + b < len; ++b) pl[off + b] ^= (uint8_t)(ks[b >> 2] >> (8 * (b & 3)));
+        xor_stream(key, nonce, pl, len, lane);
+        __threadfence_block();
+        __syncthreads(); // every lane's ciphertext visible to lane 0
+    }
+    if (lane == 0) {
+        uint32_t ks[16];
+        chacha_block(key, 0, nonce[0], nonce[1], nonce[2], ks); // one-time Poly1305 key
+        const Mul r = make_mul(ks[0], ks[1], ks[2], ks[3]);
+        Acc h = {0, 0, 0, 0, 0};
+        poly_vec(h, r, reinterpret_cast<const uint4 *>(arena + j.aad_off), j.aad_len);
+        poly_vec(h, r, pl, len);
+        acc_add(h, (uint32_t)j.aad_len, (uint32_t)(j.aad_len >> 32), (uint32_t)len, (uint32_t)(len >> 32), 1);
+        acc_mul(h, r);
+        uint32_t tag[4];
+        acc_finish(h, ks[4], ks[5], ks[6], ks[7], tag);
+        uint4 *tp = reinterpret_cast<uint4 *>(arena + j.tag_off);
+        if (!j.decrypt) {
+            *tp = make_uint4(tag[0], tag[1], tag[2], tag[3]);
+            verdict = RG_PKT_OK;
+        } else {
+            const uint4 want = *tp;
+            const uint32_t diff = (tag[0] ^ want.x) | (tag[1] ^ want.y) | (tag[2] ^ want.z) | (tag[3] ^ want.w);
+            verdict = diff == 0 ? RG_PKT_OK : RG_PKT_DECRYPT_ERR;
         }
+        j.status = verdict;
     }
-    poly_bytes(h, r, pl, len);
-    acc_add(h, (uint32_t)j.aad_len, (uint32_t)(j.aad_len >> 32), (uint32_t)len, (uint32_t)(len >> 32), 1);
-    acc_mul(h, r);
-    uint32_t tag[4];
-    acc_finish(h, s0, s1, s2, s3, tag);
-    uint8_t *tp = arena + j.tag_off;
-    if (!j.decrypt) {
-        for (int b = 0; b < 16; ++b) tp[b] = (uint8_t)(tag[b >> 2] >> (8 * (b & 3)));
-        j.status = RG_PKT_OK;
-        return;
-    }
-    uint32_t diff = 0;
-    for (int b = 0; b < 16; ++b) diff |= (uint32_t)(tp[b] ^ (uint8_t)(tag[b >> 2] >> (8 * (b & 3))));
-    if (diff != 0) {
-        j.status = RG_PKT_DECRYPT_ERR;
-        return;
-    }
-    for (uint64_t off = 0; off < len; off += 64) {
-        chacha_block(key, (uint32_t)(off / 64) + 1, j.nonce[0], j.nonce[1], j.nonce[2], ks);
-        for (int b = 0; b < 64 && off + b < len; ++b) pl[off + b] ^= (uint8_t)(ks[b >> 2] >> (8 * (b & 3)));
-    }
-    j.status = RG_PKT_OK;
+    __syncthreads();
+    if (j.decrypt && verdict == RG_PKT_OK) xor_stream(key, nonce, pl, len, lane); // text only if authentic
 }
 
 // ------------------------------------------------------------ receivers
@@ -181,7 +215,7 @@ __global__ __launch_bounds__(256) void synth_fill_kernel(const rg_pkt_desc *desc
 // ---------------------------------------------------------------- launch
 hipError_t launch_general(GeneralJob *jobs, uint32_t njobs, uint8_t *arena, hipStream_t s) {
     if (njobs == 0) return hipSuccess;
-    hipLaunchKernelGGL(general_kernel, dim3((njobs + 63) / 64), dim3(64), 0, s, jobs, njobs, arena);
+    hipLaunchKernelGGL(general_kernel, dim3(njobs), dim3(64), 0, s, jobs, njobs, arena);
     return hipGetLastError();
 }
 
