@@ -41,6 +41,16 @@ __device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x) {
     x += dpp0<0x143, 0xC>(x);
     return x;
 }
+// inclusive prefix maximum over the 64 lanes (values >= 0; the same DPP steps)
+__device__ __forceinline__ uint32_t wave_scan_max(uint32_t x) {
+    x = max(x, dpp0<0x111>(x));
+    x = max(x, dpp0<0x112>(x));
+    x = max(x, dpp0<0x114>(x));
+    x = max(x, dpp0<0x118>(x));
+    x = max(x, dpp0<0x142, 0xA>(x));
+    x = max(x, dpp0<0x143, 0xC>(x));
+    return x;
+}
 // value of lane - 1 (0 for lane 0): wave_shr:1
 __device__ __forceinline__ uint32_t wave_shr1(uint32_t x) { return dpp0<0x138>(x); }
 // value of lane 63, wave-uniform

@@ -38,12 +38,13 @@
 
 namespace rg {
 
-// floor(a / b) for a < 2^53, b > 0: a double estimate corrected to the exact quotient
-// (a 64-bit integer division is a long software loop on the GPU)
+// floor(a / b) for a < 2^50, b > 0: a * rcp(b) in double (v_rcp_f64, a few ulp) corrected to the
+// exact quotient (a 64-bit integer division is a long software loop on the GPU, an IEEE double
+// division a dozen dependent instructions)
 __device__ __forceinline__ uint64_t fdiv(uint64_t a, uint64_t b) {
-    uint64_t q = (uint64_t)((double)a / (double)b);
-    if (q * b > a) --q;
-    if ((q + 1) * b <= a) ++q;
+    uint64_t q = (uint64_t)((double)a * __builtin_amdgcn_rcp((double)b));
+    while (q * b > a) --q;
+    while ((q + 1) * b <= a) ++q;
     return q;
 }
 
@@ -368,46 +369,75 @@ template <bool OPEN> __global__ __launch_bounds__(64 * kFlatWaves) void flat_ker
             const uint32_t f1 = (uint32_t)min((uint64_t)NU, fdiv(((uint64_t)g + 1) * kFlatGroup * NU + n - 1, n));
             const uint32_t kg = f1 - f0, j = u - f0;
             const uint32_t gb = g * kFlatGroup, gn = min(kFlatGroup, n - gb);
+#ifdef RG_FLAT_PRO_STAMPS2
+            if (dbg && mk[4] == 0) mk[4] = __builtin_amdgcn_s_memtime();
+#endif
             // coalesced: lane l holds packets l + 64 q of the group (q = 0..15)
             rg_pkt_desc d[16];
-            uint32_t w[16];
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
                 const uint32_t i = lane + 64 * q;
                 d[q] = desc[gb + (i < gn ? i : 0)];
             }
-            // inclusive prefix E of the work in packet order (q-major), one wave scan per q
-            // inclusive prefix E of the work in packet order (q-major), one DPP wave scan per round;
-            // group totals stay below 2^24 (1024 packets of at most 16386 blocks), so 32 bits suffice
-            uint32_t base = 0;
+#ifdef RG_FLAT_PRO_STAMPS2
+            {
+                uint32_t acc = 0;
+#pragma unroll
+                for (int q = 0; q < 16; ++q) acc ^= d[q].len; // forces every load to land
+                if (dbg && mk[5] == 0) mk[5] = __builtin_amdgcn_s_memtime() + (acc == 0x7FFFFFFFu);
+            }
+#endif
+            // The work prefix in packet order, lane-contiguous: the per-packet work goes through LDS
+            // (the key-record area, written only later) from the coalesced order (lane + 64 q) to
+            // lane l holding packets 16 l .. 16 l + 15; each lane sums its 16 serially and one DPP
+            // wave scan of the lane totals places them (one scan instead of one per round).  Group
+            // totals stay below 2^24 (1024 packets of at most 16386 blocks), so 32 bits suffice.
+            uint32_t *const tw = &L.kr[0][0];
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
                 const uint32_t i = lane + 64 * q;
-                const uint32_t wq = i < gn ? (A.balance ? flat_work(d[q], OPEN) : 1u) : 0u;
-                const uint32_t x = wave_scan_incl(wq);
-                w[q] = base + x; // E of packet i
-                base += lane63(x);
+                tw[i] = i < gn ? (A.balance ? flat_work(d[q], OPEN) : 1u) : 0u;
             }
-            const uint32_t total = base;
+            wave_sync();
+            uint32_t e[16];
+            {
+                const uint4 *t4 = reinterpret_cast<const uint4 *>(tw) + 4 * lane;
+                const uint4 a0 = t4[0], a1 = t4[1], a2 = t4[2], a3 = t4[3];
+                e[0] = a0.x; e[1] = a0.y; e[2] = a0.z; e[3] = a0.w;
+                e[4] = a1.x; e[5] = a1.y; e[6] = a1.z; e[7] = a1.w;
+                e[8] = a2.x; e[9] = a2.y; e[10] = a2.z; e[11] = a2.w;
+                e[12] = a3.x; e[13] = a3.y; e[14] = a3.z; e[15] = a3.w;
+            }
+            wave_sync(); // the reads are done before anything rewrites the area
+#pragma unroll
+            for (int q = 1; q < 16; ++q) e[q] += e[q - 1];
+            const uint32_t lsum = e[15];
+            const uint32_t lx = wave_scan_incl(lsum) - lsum; // work of the lanes before this one
+#pragma unroll
+            for (int q = 0; q < 16; ++q) e[q] += lx; // E_i, inclusive, of packet 16 lane + q
+            const uint32_t total = lane63(lx + lsum);
 #ifdef RG_FLAT_PRO_STAMPS
             if (dbg && mk[2] == 0) mk[2] = __builtin_amdgcn_s_memtime();
 #endif
             // targets j total / kg and (j + 1) total / kg without a 64-bit division
-            const uint32_t tq = total / kg, tr = total % kg;
-            const uint32_t t2[2] = {2 * (tq * j + tr * j / kg), 2 * (tq * (j + 1) + tr * (j + 1) / kg)};
+            const uint32_t t2[2] = {2 * (uint32_t)fdiv((uint64_t)total * j, kg),
+                                    2 * (uint32_t)fdiv((uint64_t)total * (j + 1), kg)};
             // a packet belongs to the unit its work midpoint (E_{i-1} + E_i) / 2 falls in; the midpoints
             // rise with i, so a cut is the number of packets whose midpoint lies below the target
-            uint32_t cut[2] = {0, 0};
-            uint32_t prev63 = 0; // E of the packet before round q
+            uint32_t c0 = 0, c1 = 0;
+            {
+                const uint32_t sh = wave_shr1(e[15]);
+                uint32_t prev = lane ? sh : 0u; // E of the packet before 16 lane
 #pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const uint32_t i = lane + 64 * q;
-                const uint32_t sh = wave_shr1(w[q]);
-                const uint32_t mid2 = w[q] + (lane ? sh : prev63);
-                prev63 = lane63(w[q]);
-                cut[0] += (uint32_t)__popcll(__ballot(i < gn && mid2 < t2[0]));
-                cut[1] += (uint32_t)__popcll(__ballot(i < gn && mid2 < t2[1]));
+                for (int q = 0; q < 16; ++q) {
+                    const uint32_t i = 16 * lane + q;
+                    const uint32_t mid2 = e[q] + prev;
+                    prev = e[q];
+                    c0 += (i < gn && mid2 < t2[0]) ? 1u : 0u;
+                    c1 += (i < gn && mid2 < t2[1]) ? 1u : 0u;
+                }
             }
+            uint32_t cut[2] = {lane63(wave_scan_incl(c0)), lane63(wave_scan_incl(c1))};
             if (j == 0) cut[0] = 0;
             if (j + 1 == kg) cut[1] = gn;
 #ifdef RG_FLAT_PRO_STAMPS
@@ -441,37 +471,9 @@ template <bool OPEN> __global__ __launch_bounds__(64 * kFlatWaves) void flat_ker
             }
             staged = 0;
             wave_sync();
-            uint32_t run = 0;
-#pragma unroll
-            for (uint32_t q = 0; q < kFlatMaxPk / 64; ++q) {
-                if (64 * q >= m) break; // wave-uniform
-                const uint32_t k = lane + 64 * q;
-                const uint32_t c = k < m ? (L.rec[k].z + 3) >> 2 : 0u;
-                const uint32_t x = wave_scan_incl(c);
-                if (k < m) L.rec[k].w = run + x - c;
-                run += lane63(x);
-            }
-            const uint32_t D = run;
-            // statuses of the descriptor checks, kept for phase A in registers
-            uint8_t dst[kFlatMaxPk / 64];
-            wave_sync();
-            if (lane == 0) L.rec[m] = make_uint4(0, 0, 0, D);
-            RG_FLAT_MARK(2);
-            // ---- the lane's chunk range and start packet
-            const uint32_t c_lo = (uint32_t)(((uint64_t)lane * D) >> 6), c_hi = (uint32_t)(((uint64_t)(lane + 1) * D) >> 6);
-            FLane s;
-            s.nsteps = c_hi - c_lo;
-            uint32_t kstart = m;
-            {
-                uint32_t lo = 0, hi = m; // last k with cs[k] <= c_lo
-                while (hi - lo > 1) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if (L.rec[mid].w <= c_lo) lo = mid;
-                    else hi = mid;
-                }
-                kstart = lo;
-            }
-            // ---- phase A loads (issued ahead of the chunk prefetch so that their waits stay exact)
+            // ---- phase A loads, issued first so that their latency hides behind the chunk-count scan
+            // and the range search (and ahead of the chunk prefetch, so that their waits stay exact)
+            uint8_t dst[kFlatMaxPk / 64]; // statuses of the descriptor checks, kept for phase A
             uint4 ka[kFlatMaxPk / 64], kb[kFlatMaxPk / 64], hx[kFlatMaxPk / 64], tg[kFlatMaxPk / 64];
             uint32_t rcv[kFlatMaxPk / 64], dlen[kFlatMaxPk / 64], dkey[kFlatMaxPk / 64];
             uint64_t doff[kFlatMaxPk / 64];
@@ -517,6 +519,58 @@ template <bool OPEN> __global__ __launch_bounds__(64 * kFlatWaves) void flat_ker
                     tg[q] = *(go ? reinterpret_cast<const uint4 *>(fr + dlen[q] - 16) : safe);
                 }
             }
+            uint32_t run = 0;
+            uint32_t csr[kFlatMaxPk / 64]; // chunk start of packet lane + 64 q
+#pragma unroll
+            for (uint32_t q = 0; q < kFlatMaxPk / 64; ++q) {
+                csr[q] = 0xFFFFFFFFu;
+                if (64 * q >= m) break; // wave-uniform
+                const uint32_t k = lane + 64 * q;
+                const uint32_t c = k < m ? (L.rec[k].z + 3) >> 2 : 0u;
+                const uint32_t x = wave_scan_incl(c);
+                if (k < m) L.rec[k].w = csr[q] = run + x - c;
+                run += lane63(x);
+            }
+            const uint32_t D = run;
+            // The lane's first packet kstart = last k with cs[k] <= c_lo(lane) and, with chunks, its last
+            // packet kend = last k with cs[k] < c_hi(lane), c_lo(l) = floor(l D / 64) = c_hi(l - 1):
+            // packet k qualifies for every lane from ceil(64 cs[k] / D) (resp. ceil(64 (cs[k] + 1) / D) - 1)
+            // on, so each packet marks that lane (LDS max) and a running max over the lanes reads off
+            // the answer -- no dependent LDS search per lane.  The carry slots serve as scratch here.
+            uint32_t *const mk_lo = &L.ck[0];
+            uint32_t *const mk_hi = &L.ch[0][0];
+            mk_lo[lane] = 0u;
+            mk_hi[5 * lane] = 0u;
+            wave_sync();
+            if (D) {
+                const double rD = __builtin_amdgcn_rcp((double)D);
+                auto fl = [&](uint32_t a) -> uint32_t { // floor(a / D), a < 2^31: estimate, then exact
+                    uint32_t t = (uint32_t)((double)a * rD);
+                    t = (uint64_t)t * D > a ? t - 1 : t;
+                    return (uint64_t)(t + 1) * D <= a ? t + 1 : t;
+                };
+#pragma unroll
+                for (uint32_t q = 0; q < kFlatMaxPk / 64; ++q) {
+                    if (64 * q >= m) break; // wave-uniform
+                    const uint32_t k = lane + 64 * q;
+                    if (k >= m) continue;
+                    const uint32_t l0 = fl(64 * csr[q] + D - 1);
+                    const uint32_t l1 = fl(64 * (csr[q] + 1) + D - 1) - 1;
+                    if (l0 < 64) atomicMax(&mk_lo[l0], k);
+                    if (l1 < 64) atomicMax(&mk_hi[5 * l1], k);
+                }
+            }
+            wave_sync();
+            const uint32_t kstart_scan = wave_scan_max(mk_lo[lane]);
+            const uint32_t kend_scan = wave_scan_max(mk_hi[5 * lane]);
+            wave_sync(); // the scratch reads are done before the slots are used again
+            if (lane == 0) L.rec[m] = make_uint4(0, 0, 0, D);
+            RG_FLAT_MARK(2);
+            // ---- the lane's chunk range and start packet
+            const uint32_t c_lo = (uint32_t)(((uint64_t)lane * D) >> 6), c_hi = (uint32_t)(((uint64_t)(lane + 1) * D) >> 6);
+            FLane s;
+            s.nsteps = c_hi - c_lo;
+            const uint32_t kstart = D ? kstart_scan : m - 1;
             // ---- the lane's first three chunks
             FChunk b0, b1, b2;
             if (s.nsteps) {
@@ -612,13 +666,7 @@ template <bool OPEN> __global__ __launch_bounds__(64 * kFlatWaves) void flat_ker
                 s.pe = 0;
                 uint32_t kend = 0;
                 if (s.nsteps) {
-                    uint32_t lo = 0, hi = m; // last k with cs[k] <= c_hi - 1
-                    while (hi - lo > 1) {
-                        const uint32_t mid = (lo + hi) >> 1;
-                        if (L.rec[mid].w <= c_hi - 1) lo = mid;
-                        else hi = mid;
-                    }
-                    kend = lo;
+                    kend = kend_scan;
                     const uint4 rc = L.rec[kend];
                     const uint32_t nbe = rc.z & ~kLiveBit, tend = c_hi - rc.w; // chunks of kend through the lane
                     if (4 * tend < nbe) s.pe = nbe - 4 * tend;
