@@ -38,14 +38,13 @@
 
 namespace rg {
 
-// floor(a / b) for a < 2^50, b > 0: a * rcp(b) in double (v_rcp_f64, a few ulp) corrected to the
-// exact quotient (a 64-bit integer division is a long software loop on the GPU, an IEEE double
-// division a dozen dependent instructions)
+// floor(a / b) for a < 2^46, b > 0: a * rcp(b) in double (v_rcp_f64 is good to a few ulp, so the
+// estimate is off by at most one) and one branch-free correction (a 64-bit integer division is a
+// long software loop on the GPU, an IEEE double division a dozen dependent instructions)
 __device__ __forceinline__ uint64_t fdiv(uint64_t a, uint64_t b) {
     uint64_t q = (uint64_t)((double)a * __builtin_amdgcn_rcp((double)b));
-    while (q * b > a) --q;
-    while ((q + 1) * b <= a) ++q;
-    return q;
+    q = q * b > a ? q - 1 : q;
+    return (q + 1) * b <= a ? q + 1 : q;
 }
 
 // ------------------------------------------------------ unit boundaries
@@ -335,9 +334,9 @@ __device__ __forceinline__ uint32_t flat_stage(FlatLds &L, uint32_t k, const rg_
 
 template <bool OPEN> __global__ __launch_bounds__(64 * kFlatWaves) void flat_kernel(FlatArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t flat_lds[];
-    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t lane = threadIdx.x & 63, wv = uniform_u32(threadIdx.x >> 6);
     FlatLds &L = reinterpret_cast<FlatLds *>(flat_lds)[wv];
-    const uint32_t wid = blockIdx.x * kFlatWaves + wv, nw = gridDim.x * kFlatWaves;
+    const uint32_t wid = uniform_u32(blockIdx.x * kFlatWaves + wv), nw = gridDim.x * kFlatWaves;
     const uint32_t n = OPEN ? A.oa.n : A.sa.n;
     uint8_t *const buf = OPEN ? A.oa.buf : A.sa.buf;
     const uint64_t buf_len = OPEN ? A.oa.buf_len : A.sa.buf_len;
@@ -357,6 +356,9 @@ template <bool OPEN> __global__ __launch_bounds__(64 * kFlatWaves) void flat_ker
     if (dbg && lane == 0) dbg[8ull * wid + 6] = 0xABCD0000ull + wv;
 #endif
     const uint32_t NU = A.units;
+#ifdef RG_FLAT_PRO_STAMPS2
+    if (dbg && mk[6] == 0) mk[6] = __builtin_amdgcn_s_memtime() + (NU == 0xFFFFFFFFu) + (n == 0xFFFFFFFFu);
+#endif
     for (uint32_t u = wid; u < NU; u += nw) {
         // ---- this unit's packets [s, e) and, when it is read from a group, its first sub-unit staged
         uint32_t s0, e0, staged = 0;
@@ -364,9 +366,19 @@ template <bool OPEN> __global__ __launch_bounds__(64 * kFlatWaves) void flat_ker
             // Units of group g (kFlatGroup packets): those whose nominal start u n / NU falls in it;
             // inside the group the cut points split its work evenly (midpoint rule).  No global
             // pass: the wave reads the group's descriptors (16 per lane) and scans them itself.
-            const uint32_t g = (uint32_t)fdiv((uint64_t)u * n, (uint64_t)NU * kFlatGroup);
-            const uint32_t f0 = (uint32_t)fdiv((uint64_t)g * kFlatGroup * NU + n - 1, n);
-            const uint32_t f1 = (uint32_t)min((uint64_t)NU, fdiv(((uint64_t)g + 1) * kFlatGroup * NU + n - 1, n));
+            // (wave-uniform values, pinned to scalar registers so that every test on them below is a
+            // scalar branch rather than an exec-masked one)
+            uint32_t g, f0, f1;
+            if (NU <= 1024u) { // every operand below 2^31 (n <= 2^10 NU): 32-bit divisions
+                const uint32_t gu = kFlatGroup * NU;
+                g = uniform_u32(u * n / gu);
+                f0 = uniform_u32((g * gu + n - 1) / n);
+                f1 = uniform_u32(min(NU, ((g + 1) * gu + n - 1) / n));
+            } else {
+                g = uniform_u32((uint32_t)fdiv((uint64_t)u * n, (uint64_t)NU * kFlatGroup));
+                f0 = uniform_u32((uint32_t)fdiv((uint64_t)g * kFlatGroup * NU + n - 1, n));
+                f1 = uniform_u32((uint32_t)min((uint64_t)NU, fdiv(((uint64_t)g + 1) * kFlatGroup * NU + n - 1, n)));
+            }
             const uint32_t kg = f1 - f0, j = u - f0;
             const uint32_t gb = g * kFlatGroup, gn = min(kFlatGroup, n - gb);
 #ifdef RG_FLAT_PRO_STAMPS2
@@ -420,8 +432,8 @@ template <bool OPEN> __global__ __launch_bounds__(64 * kFlatWaves) void flat_ker
             if (dbg && mk[2] == 0) mk[2] = __builtin_amdgcn_s_memtime();
 #endif
             // targets j total / kg and (j + 1) total / kg without a 64-bit division
-            const uint32_t t2[2] = {2 * (uint32_t)fdiv((uint64_t)total * j, kg),
-                                    2 * (uint32_t)fdiv((uint64_t)total * (j + 1), kg)};
+            const uint32_t t2[2] = {uniform_u32(2 * (uint32_t)fdiv((uint64_t)total * j, kg)),
+                                    uniform_u32(2 * (uint32_t)fdiv((uint64_t)total * (j + 1), kg))};
             // a packet belongs to the unit its work midpoint (E_{i-1} + E_i) / 2 falls in; the midpoints
             // rise with i, so a cut is the number of packets whose midpoint lies below the target
             uint32_t c0 = 0, c1 = 0;
