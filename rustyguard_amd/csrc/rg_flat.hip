@@ -67,12 +67,12 @@ struct FlatLds {
     uint4 rec[kFlatMaxPk + 1];    // {offset lo, offset hi, nb | kLiveBit, cs}; rec[m].w = D
     uint32_t kr[kFlatMaxPk][16];  // key[8], counter lo/hi, r[4] (unclamped), desc len, desc key_idx
     uint32_t sw[kFlatMaxPk][4];   // seal: s; open: tag - s (mod 2^128)
-    uint32_t hs[kFlatMaxPk][8];   // final piece's Horner sum h0..h4, [5] its lane (64: none), [6] kFail
-    uint32_t ck[64];              // lane's carry: packet, ~0 (none) or kNoChunks
-    uint32_t ch[64][5];           // lane's carry value h r^after
+    uint32_t hs[kFlatMaxPk][8];   // [6] kFail (open: the tag did not verify)
+    unsigned long long ps[kFlatMaxPk][5]; // sum of the packet's Horner pieces, radix 2^32 limbs (LDS atomics)
+    uint32_t ck[64];              // scratch: the lanes' first-packet markers
+    uint32_t ch[64][5];           // scratch: the lanes' last-packet markers (stride 5)
 };
 constexpr uint32_t kLiveBit = 0x80000000u, kFail = 2u;
-constexpr uint32_t kNoChunks = 0xFFFFFFFEu;
 constexpr uint32_t kFlatWaves = 4; // one per SIMD (two per SIMD, with half-size units, measured slower)
 static_assert(kFlatWaves * sizeof(FlatLds) <= kLdsPerCu, "flat LDS image");
 
@@ -182,10 +182,15 @@ __device__ __forceinline__ void pow_step(FLane &s) {
     --s.pb;
 }
 
-__device__ __forceinline__ void put_h(FlatLds &L, uint32_t k, const Acc &h, uint32_t lane) {
-    uint4 *o = reinterpret_cast<uint4 *>(L.hs[k]);
-    o[0] = make_uint4(h.h0, h.h1, h.h2, h.h3);
-    o[1] = make_uint4(h.h4, lane, 0u, 0u);
+// a piece of packet k's Poly1305 sum (its final piece, or a carry h r^after of an earlier lane): the
+// limbs are added into the packet's 64-bit slots by LDS atomics, so phase F reads one sum per
+// packet instead of walking the lanes before it (each limb < 2^32, at most 64 pieces)
+__device__ __forceinline__ void add_h(FlatLds &L, uint32_t k, const Acc &h) {
+    atomicAdd(&L.ps[k][0], (unsigned long long)h.h0);
+    atomicAdd(&L.ps[k][1], (unsigned long long)h.h1);
+    atomicAdd(&L.ps[k][2], (unsigned long long)h.h2);
+    atomicAdd(&L.ps[k][3], (unsigned long long)h.h3);
+    atomicAdd(&L.ps[k][4], (unsigned long long)h.h4);
 }
 
 // One step of phase C over chunk j of the lane (in buffer b).  Seal absorbs the
@@ -235,12 +240,12 @@ __device__ __forceinline__ void flat_step(FLane &s, FChunk &b, uint32_t j, FlatL
     }
     if constexpr (OPEN) {
         if (active && s.cur.t + 1 == s.cur.c) { // the packet's last chunk: its final piece
-            if (s.cur.live) put_h(L, s.cur.k, s.h, lane);
+            if (s.cur.live) add_h(L, s.cur.k, s.h);
             s.h = Acc{0, 0, 0, 0, 0};
         }
     } else {
         if (active && s.pk != s.cur.k) { // the pending packet ended in this lane: final piece
-            if (s.pk < m) put_h(L, s.pk, s.h, lane);
+            if (s.pk < m) add_h(L, s.pk, s.h);
             s.h = Acc{0, 0, 0, 0, 0};
             s.r = make_mul(s.rn[0], s.rn[1], s.rn[2], s.rn[3]); // r of cur.k, read at its switch
             s.pk = s.cur.k;
@@ -642,7 +647,11 @@ template <bool OPEN> __global__ __launch_bounds__(64 * kFlatWaves) void flat_ker
                 } else {
                     *reinterpret_cast<uint4 *>(L.sw[k]) = make_uint4(ks[4], ks[5], ks[6], ks[7]);
                 }
-                put_h(L, k, Acc{0, 0, 0, 0, 0}, 64);
+                {
+                    unsigned long long *z = L.ps[k];
+                    z[0] = z[1] = z[2] = z[3] = z[4] = 0ull;
+                    L.hs[k][6] = 0u;
+                }
                 if (st == 0xFF) {
                     L.rec[k].z |= kLiveBit;
                     if constexpr (!OPEN) {
@@ -714,7 +723,7 @@ template <bool OPEN> __global__ __launch_bounds__(64 * kFlatWaves) void flat_ker
                         ck = s.pk;
                         after = s.cur.nb - 4 * s.cur.t;
                     } else {
-                        put_h(L, s.pk, s.h, lane);
+                        add_h(L, s.pk, s.h);
                     }
                 }
             } else {
@@ -726,34 +735,35 @@ template <bool OPEN> __global__ __launch_bounds__(64 * kFlatWaves) void flat_ker
             // carry = h r^after for the packet the next lane continues (the power was computed during
             // phase C; after == s.pe whenever there is a carry)
             while (s.pb >= 0) pow_step(s);
-            Acc cv = s.h;
-            if (ck != ~0u) acc_mul_gen(cv, make_gen(s.px));
+            if (ck != ~0u) {
+                Acc cv = s.h;
+                acc_mul_gen(cv, make_gen(s.px));
+                add_h(L, ck, cv);
+            }
             (void)after;
-            L.ck[lane] = s.nsteps ? ck : kNoChunks;
-            L.ch[lane][0] = cv.h0; L.ch[lane][1] = cv.h1; L.ch[lane][2] = cv.h2; L.ch[lane][3] = cv.h3;
-            L.ch[lane][4] = cv.h4;
             wave_sync();
             RG_FLAT_MARK(5);
             // ---- phase F: tags
             bool any_fail = false;
             for (uint32_t k = lane; k < m; k += 64) {
                 const uint4 rc = L.rec[k];
-                const uint4 h03 = reinterpret_cast<const uint4 *>(L.hs[k])[0];
-                const uint4 h4l = reinterpret_cast<const uint4 *>(L.hs[k])[1];
+                const unsigned long long *ps = L.ps[k];
+                const unsigned long long p0 = ps[0], p1 = ps[1], p2 = ps[2], p3 = ps[3], p4 = ps[4];
                 const uint4 swk = *reinterpret_cast<const uint4 *>(L.sw[k]);
                 const uint4 r03 = make_uint4(L.kr[k][10], L.kr[k][11], L.kr[k][12], L.kr[k][13]);
                 if (!(rc.z & kLiveBit)) continue;
-                Acc h = {h03.x, h03.y, h03.z, h03.w, h4l.x};
-                // the packet's other pieces: the carries of the lanes just before its final lane
-                // (lanes without chunks sit between them when D < 64 and pass through)
-                for (int l = (int)h4l.y - 1; l >= 0; --l) {
-                    const uint32_t c = L.ck[l]; // read with the value: one LDS round trip per lane
-                    const Acc cv = {L.ch[l][0], L.ch[l][1], L.ch[l][2], L.ch[l][3], L.ch[l][4]};
-                    if (c == kNoChunks) continue;
-                    if (c != k) break;
-                    acc_add_acc(h, cv);
-                    acc_fold(h);
-                }
+                // the sum of the packet's pieces, carried into 32-bit limbs and partially reduced
+                Acc h;
+                unsigned long long t = p0;
+                h.h0 = (uint32_t)t;
+                t = (t >> 32) + p1;
+                h.h1 = (uint32_t)t;
+                t = (t >> 32) + p2;
+                h.h2 = (uint32_t)t;
+                t = (t >> 32) + p3;
+                h.h3 = (uint32_t)t;
+                h.h4 = (uint32_t)((t >> 32) + p4);
+                acc_fold(h);
                 const uint32_t P = (rc.z & ~kLiveBit) * 16;
                 const Mul r = make_mul(r03.x, r03.y, r03.z, r03.w);
                 acc_add(h, 0, 0, P, 0, 1); // le64(aad_len = 0) || le64(P), RFC 8439 §2.8
