@@ -260,6 +260,9 @@ __device__ __forceinline__ void flat_step(FLane &s, FChunk &b, uint32_t j, FlatL
     }
     fload(b, s.f.pl, s.f.t, s.f.nb ? s.f.nb - 1 : 0);
     if (active && fcur_next(s.cur, L, buf, m) && s.cur.k < m) {
+#ifdef RG_FLAT_ABL_NOSWITCH // diagnostics only: the stream is not re-keyed at a packet switch (output invalid)
+        if (s.cur.k != 0xFFFFFFFFu) return;
+#endif
         const FKey q = fkey(L, s.cur.k);
         s.st = make_stream(q.key, 0u, q.n1, q.n2);
         if constexpr (OPEN) s.r = make_mul(q.r[0], q.r[1], q.r[2], q.r[3]);
