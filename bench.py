@@ -80,6 +80,8 @@ def parse():
     ap.add_argument("--e2e", action="store_true", help="also time the pinned host->GPU->host path")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch/validate the ranks, print each rank's plan as JSON and exit before any GPU work")
+    ap.add_argument("--forged", type=float, default=0.0,
+                    help="also time the open with this fraction of forged tags (0 = skip)")
     ap.add_argument("--no-cold", dest="cold", action="store_false",
                     help="skip the cold-cache pass (profiling runs: keeps per-kernel averages to the step's regime)")
     ap.add_argument("--no-verify", dest="verify", action="store_false",
@@ -270,6 +272,39 @@ def launch_ranks(n: int) -> int:
 
 
 MALL_BYTES = 256 * 2**20  # MI355X Infinity Cache (memory-side, in front of HBM)
+
+
+def forged_open_timing(w, b, stream, frac: float, verify: bool):
+    """Open time when a fraction of the batch carries forged tags (last tag byte flipped after the
+    seal): the open kernels decrypt speculatively and a forged frame costs a second keystream pass
+    to restore it, so this prices that DoS property.  Reported beside the step."""
+    import torch
+
+    rng = np.random.default_rng(7)
+    k = max(1, int(round(frac * w.n)))
+    pick = np.sort(rng.choice(w.n, size=k, replace=False))
+    pos = (w.desc["offset"][pick] + np.uint64(16) + w.desc["len"][pick].astype(np.uint64) + np.uint64(15))
+    idx = torch.from_numpy(pos.astype(np.int64)).to(b.buf.device)
+    reps = 5
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(reps)]
+    for e in evs:
+        b.seal(stream=stream)
+        with torch.cuda.stream(stream):
+            b.buf[idx] ^= 1
+        e[0].record(stream)
+        b.open(stream=stream, counters_out=False)
+        e[1].record(stream)
+    torch.cuda.synchronize()
+    st = b.status[: w.n].cpu().numpy()
+    if verify:
+        bad = np.zeros(w.n, bool)
+        bad[pick] = True
+        assert (st[bad] == 1).all() and (st[~bad] == 0).all(), "forged-batch statuses"
+    b.seal(stream=stream)  # leave the batch sealed and valid
+    torch.cuda.synchronize()
+    open_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / reps
+    return {"forged_frac": round(k / w.n, 4), "open_ms": round(open_ms, 5),
+            "open_gib_s": round(w.payload_bytes / (open_ms / 1e3) / 2**30, 3)}
 
 
 def cold_cache_timing(eng, w, b, stream, verify: bool):
@@ -518,6 +553,7 @@ def main():
     if args.verify:
         assert (b.status[: w.n] == 0).all().item(), "open failed in the kernel-timing pass"
     cold = cold_cache_timing(eng, w, b, stream, args.verify) if args.cold and w.buf_bytes < MALL_BYTES else None
+    forged = forged_open_timing(w, b, stream, args.forged, args.verify) if args.forged > 0 else None
     if args.verify:
         strict_check(w, b, stream)
 
@@ -589,6 +625,8 @@ def main():
                                      "rates measured by tools/microbench.hip; one-time-key block per packet"}
     if cold:
         out["cold_cache"] = cold
+    if forged:
+        out["forged_open"] = forged
     if args.e2e and rank == 0:
         out["e2e"] = e2e_host(eng, w, b)
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
