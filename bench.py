@@ -300,7 +300,7 @@ def forged_open_timing(w, b, stream, frac: float, verify: bool):
         bad = np.zeros(w.n, bool)
         bad[pick] = True
         assert (st[bad] == 1).all() and (st[~bad] == 0).all(), "forged-batch statuses"
-    b.seal(stream=stream)  # leave the batch sealed and valid
+    b.fill(stream=stream)  # back to the synthetic plaintext the later checks start from
     torch.cuda.synchronize()
     open_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / reps
     return {"forged_frac": round(k / w.n, 4), "open_ms": round(open_ms, 5),
