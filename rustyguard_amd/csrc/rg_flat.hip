@@ -73,7 +73,10 @@ struct FlatLds {
     uint32_t ch[64][5];           // scratch: the lanes' last-packet markers (stride 5)
 };
 constexpr uint32_t kLiveBit = 0x80000000u, kFail = 2u;
-constexpr uint32_t kFlatWaves = 4; // one per SIMD (two per SIMD, with half-size units, measured slower)
+#ifndef RG_FLAT_WAVES
+#define RG_FLAT_WAVES 4 // waves per workgroup, one workgroup per CU: one wave per SIMD
+#endif
+constexpr uint32_t kFlatWaves = RG_FLAT_WAVES;
 static_assert(kFlatWaves * sizeof(FlatLds) <= kLdsPerCu, "flat LDS image");
 
 __device__ __forceinline__ void wave_sync() {
