@@ -81,6 +81,48 @@ def main():
                  "seal_open_rx_ms": round(ms_rx, 4), "resolve_overhead_us": round((ms_rx - ms_open) * 1e3, 2),
                  "note": "medians of 7 alternating repetitions of 10 steps; the rx_resolve kernel itself is in the "
                          "rocprofv3 kernel stats"}
+    # ------------------------------------------------------------ sessions
+    # the device-resident session layer on config-2 geometry (64 Ki x 1504 B, one session): B seals
+    # with rg_send_batch_dev (fresh counters every round), A receives with rg_recv_batch_dev; the host
+    # half (rg_recv_batch_dev_finish: in-order anti-replay pass, flags, status write-back) is timed
+    # on its own
+    import time
+
+    w = workloads.build("cfg2")
+    b = DeviceBatch(eng, w)
+    b.fill()
+    rng = np.random.default_rng(9)
+    k1, k2 = rng.integers(0, 256, 32, dtype=np.uint8).tobytes(), rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
+    sa, sb = aead.Sessions(eng, 4), aead.Sessions(eng, 4)
+    slot_a = sa.insert(0x1111, 0x2222, k1, k2)
+    slot_b = sb.insert(0x2222, 0x1111, k2, k1)
+    slots = np.full(w.n, slot_b, np.uint32)
+    t_send, t_gpu, t_fin = [], [], []
+    for it in range(12):
+        b.fill()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        sb.send_batch_dev(slots, b.desc_seal, b.buf, b.status)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        sa.recv_batch_dev(b.desc_open, b.buf, b.status)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        st, sl, fl = sa.recv_batch_dev_finish(w.n)
+        torch.cuda.synchronize()
+        t3 = time.perf_counter()
+        assert (st == 0).all() and (sl == slot_a).all()
+        if it >= 2:
+            t_send.append(t1 - t0)
+            t_gpu.append(t2 - t1)
+            t_fin.append(t3 - t2)
+    med = lambda x: float(np.median(x)) * 1e3  # noqa: E731
+    out["sessions"] = {"workload": "cfg2 geometry, one session", "packets": w.n,
+                       "send_batch_dev_ms": round(med(t_send), 4), "recv_batch_dev_ms": round(med(t_gpu), 4),
+                       "recv_finish_ms": round(med(t_fin), 4),
+                       "recv_mpkt_s": round(w.n / (med(t_gpu) + med(t_fin)) / 1e3, 2),
+                       "note": "wall-clock medians of 10 rounds, each call followed by a device sync; finish is "
+                               "the host's in-order anti-replay pass plus the status write-back"}
     print(json.dumps(out))
 
 
