@@ -20,6 +20,7 @@ from rustyguard_amd.device import DeviceBatch  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--workload", default="cfg3")
 ap.add_argument("--plan", type=int, default=1)
+ap.add_argument("--per-wave", action="store_true", help="also dump each wave's total with its unit's m and D")
 args = ap.parse_args()
 eng = Engine(0)
 eng.set_staged(3)
@@ -65,3 +66,30 @@ for op in ("seal", "open"):
     out["start_spread_cyc"] = int(start.max())
     res[op] = out
     print(op, json.dumps(out), flush=True)
+    if args.per_wave and op == "seal":
+        # the unit each wave ran (wave id = unit id: one unit per wave), by the kernel's cut rule
+        P = w.desc["len"].astype(np.int64)
+        n = len(P)
+        NU, G = len(d), 1024
+        chunks = ((P + 15) // 16 + 3) // 4
+        work = 1 + chunks
+        rows = []
+        raw = dbg.cpu().numpy().reshape(-1, 8).astype(np.int64)
+        for u in range(NU):
+            g = u * n // (G * NU)
+            f0 = (g * G * NU + n - 1) // n
+            f1 = min(NU, ((g + 1) * G * NU + n - 1) // n)
+            kg, j, gb = f1 - f0, u - f0, g * G
+            gn = min(G, n - gb)
+            E = np.cumsum(work[gb:gb + gn])
+            tot = int(E[-1])
+            mid2 = E + np.concatenate([[0], E[:-1]])
+            c0 = 0 if j == 0 else int((mid2 < 2 * (tot * j // kg)).sum())
+            c1 = gn if j + 1 == kg else int((mid2 < 2 * (tot * (j + 1) // kg)).sum())
+            m, D = c1 - c0, int(chunks[gb + c0:gb + c1].sum())
+            r = raw[u]
+            rows.append({"wave": u, "m": m, "D": D, "total": int(r[7] - r[0]) if r[0] else None})
+        rows.sort(key=lambda x: -(x["total"] or 0))
+        with open("gpurun_out/flat_per_wave.json", "w") as fo:
+            json.dump(rows, fo)
+        print("slowest", rows[:12], flush=True)
