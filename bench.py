@@ -537,9 +537,13 @@ def main():
 
     # per-kernel timing for the roofline: seal -> open pairs on the step's batch
     # (the same work and cache state as a step), one HIP event pair around each
-    # launch on the launch stream, averaged over the pairs
+    # launch on the launch stream, averaged over the pairs.  The stream is first held
+    # by a spin kernel while every pair is enqueued, so that the GPU runs them back to
+    # back: an event then brackets the kernel, not the host's time to submit it.
     reps = max(args.steps, 10)
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(reps)]
+    with torch.cuda.stream(stream):
+        torch.cuda._sleep(int(2e7))  # ~10 ms of GPU clock cycles: longer than enqueueing the pairs
     for e in evs:
         e[0].record(stream)
         b.seal(stream=stream)
