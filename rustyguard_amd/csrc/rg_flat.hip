@@ -176,7 +176,7 @@ struct FLane {
 __device__ __forceinline__ void pow_step(FLane &s) {
     if (s.pb < 0) return;
     Acc sq = s.px;
-    acc_mul_gen(sq, make_gen(s.px));
+    acc_sqr_gen(sq);
     Acc xr = sq;
     acc_mul(xr, s.pr);
     const bool bit = (s.pe >> s.pb) & 1u;
@@ -286,7 +286,7 @@ __device__ __forceinline__ Acc flat_pow_mul(Acc h, const Mul &r, uint32_t e) {
     Acc x = {1, 0, 0, 0, 0};
     for (int b = (int)bits - 1; b >= 0; --b) {
         Acc sq = x;
-        acc_mul_gen(sq, make_gen(x));
+        acc_sqr_gen(sq);
         Acc xr = sq;
         acc_mul(xr, r);
         const bool bit = (e >> b) & 1u;

@@ -235,7 +235,7 @@ __device__ __forceinline__ Acc combine_segments(Acc h, const Mul &r, uint32_t af
         Acc x = {1, 0, 0, 0, 0};
         for (int b = (int)bits - 1; b >= 0; --b) {
             Acc sq = x;
-            acc_mul_gen(sq, make_gen(x));
+            acc_sqr_gen(sq);
             Acc xr = sq;
             acc_mul(xr, r);
             const bool bit = (after >> b) & 1u;
