@@ -15,6 +15,14 @@ namespace rg {
 // through uint32_t so that a set bit 31 is never sign-extended into a 64-bit
 // value (byte offsets past 2 GiB).
 __device__ __forceinline__ uint32_t uniform_u32(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+
+// orders a wave's own LDS accesses across lanes (the compiler sees one lane; the hardware runs a
+// wave's LDS instructions in order)
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 __device__ __forceinline__ uint64_t uniform_u64(uint64_t v) {
     return ((uint64_t)uniform_u32((uint32_t)(v >> 32)) << 32) | (uint64_t)uniform_u32((uint32_t)v);
 }

@@ -79,12 +79,6 @@ constexpr uint32_t kLiveBit = 0x80000000u, kFail = 2u;
 constexpr uint32_t kFlatWaves = RG_FLAT_WAVES;
 static_assert(kFlatWaves * sizeof(FlatLds) <= kLdsPerCu, "flat LDS image");
 
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
 struct FChunk {
     uint4 q0, q1, q2, q3;
 };

@@ -46,7 +46,8 @@ template <int NT> __device__ __forceinline__ uint4 ld16(const uint4 *p) {
     } else return *p;
 }
 template <int NT> __device__ __forceinline__ void st16(uint4 *p, const uint4 &x) {
-    if constexpr (NT & 2) {
+    if constexpr (NT & 4) return; // diagnostics: payload stores dropped
+    else if constexpr (NT & 2) {
         const v4u v = {x.x, x.y, x.z, x.w};
         __builtin_nontemporal_store(v, reinterpret_cast<v4u *>(p));
     } else *p = x;
@@ -78,6 +79,83 @@ __device__ __forceinline__ void absorb_chunk(Acc &h, const Chunk &c, const Mul &
     acc_block_pred(h, c.q3, r, cnt > 3);
 }
 
+// ------------------------------------------------------------- block stores
+// When all 64 lanes of a wave hold valid packets of one size (one lane per
+// packet), the 64-byte frame blocks leave through a wave-private LDS ring: a
+// lane-per-frame store instruction puts one 16-byte piece into each of 64
+// frames (64 cache lines per instruction, each 64-byte block completed by four
+// instructions), whereas from the ring each store instruction writes whole
+// 64-byte blocks of 16 frames, four lanes per block.  Step t puts its block t
+// into ring set t & 1 and stores block t - 1, read back at the start of the
+// step, so the LDS round trip hides behind the keystream rounds.  Frame p's
+// 128 bytes hold piece j of set s in slot 4 (s ^ ((p >> 2) & 1)) + (j ^ (p & 3)):
+// conflict-free for the frame-major ds_write_b128 (8-lane groups, 128-byte
+// rows) and the block-major ds_read_b128 (16-lane groups, 256-byte rows).
+#ifndef RG_PIPE_LINES
+#define RG_PIPE_LINES 1
+#endif
+constexpr uint32_t kPipeLinesFlag = 4u; // launch flag bit (bits 0-1: log2 lanes per packet)
+constexpr uint32_t kRingBytes = 64u * 128u; // per wave
+// (plain vector types: HIP's uint4 has no assignment in a qualified address space)
+typedef __attribute__((address_space(3))) v4u lds_u4;
+typedef __attribute__((address_space(1))) v4u glb_u4;
+__device__ __forceinline__ v4u to_v4(const uint4 &a) { return v4u{a.x, a.y, a.z, a.w}; }
+__device__ __forceinline__ uint4 from_v4(const v4u &a) { return make_uint4(a.x, a.y, a.z, a.w); }
+struct Ring {
+    lds_u4 *wr;    // this lane's frame record (slot index added per piece)
+    lds_u4 *rd;    // block-major read base: frame lane / 4, piece lane % 4 (set 0)
+    glb_u4 *fr[4]; // frame 16 q + lane / 4, piece lane % 4 (bytes 16 (lane % 4) of block 0)
+    uint32_t wsw, rsw; // lane's slot swizzles: writes (p = lane), reads (set bit only)
+};
+
+__device__ __forceinline__ Ring make_ring(uint8_t *frame) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t pipe_lds[];
+    const uint32_t lane = threadIdx.x & 63;
+    lds_u4 *base = (lds_u4 *)(pipe_lds + (threadIdx.x >> 6) * kRingBytes);
+    Ring R;
+    R.wr = base + 8 * lane;
+    R.wsw = (((lane >> 2) & 1u) << 2) | (lane & 3u);
+    // reads: frame p = 16 q + lane / 4, piece w = lane % 4 -> slot 4 (s ^ ((p >> 2) & 1)) + (w ^ (p & 3))
+    R.rsw = ((lane >> 4) & 1u) << 2;
+    R.rd = base + 8 * (lane >> 2) + ((lane & 3u) ^ ((lane >> 2) & 3u));
+    const uint64_t f = reinterpret_cast<uint64_t>(frame);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t src = 16 * q + (lane >> 2);
+        const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)f, (int)src), hi = (uint32_t)__shfl((int)(uint32_t)(f >> 32), (int)src);
+        R.fr[q] = (glb_u4 *)((((uint64_t)hi << 32) | lo) + 16 * (lane & 3u));
+    }
+    return R;
+}
+
+// block (4 pieces) of this lane's frame into set s
+__device__ __forceinline__ void ring_put(const Ring &R, uint32_t s, const uint4 &a, const uint4 &b, const uint4 &c,
+                                         const uint4 &d) {
+    const uint32_t sw = R.wsw ^ (s << 2);
+    R.wr[sw ^ 0] = to_v4(a);
+    R.wr[sw ^ 1] = to_v4(b);
+    R.wr[sw ^ 2] = to_v4(c);
+    R.wr[sw ^ 3] = to_v4(d);
+}
+
+struct Ring4 {
+    v4u v[4];
+};
+// set s read back block-major: v[q] = piece lane % 4 of frame 16 q + lane / 4
+__device__ __forceinline__ Ring4 ring_get(const Ring &R, uint32_t s) {
+    const lds_u4 *r = R.rd + (R.rsw ^ (s << 2));
+    Ring4 o;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) o.v[q] = r[128 * q];
+    return o;
+}
+
+// store block b of the 64 frames from a read-back set
+__device__ __forceinline__ void ring_store(const Ring &R, const Ring4 &x, uint32_t b) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) R.fr[q][4 * b] = x.v[q];
+}
+
 // One step: keystream block t+1 -- with the previous chunk's four Poly1305
 // blocks (pi, always a full chunk) absorbed in its rounds when ABSORB -- XORed
 // into chunk t (buf) and stored; then chunk t+kDepth is requested into buf.  Full
@@ -92,11 +170,20 @@ __device__ __forceinline__ void absorb_chunk(Acc &h, const Chunk &c, const Mul &
 // steps were measured at 1.66x the algorithmic write bytes (profiles/).
 // MODE (seal diagnostics, rg_set_debug_mode): 0 normal; 1 compute only (no
 // payload loads or stores, loop-carried fake data); 2 memory only (no
-// keystream and no Poly1305); 4/5/6 non-temporal loads / stores / both.
-template <bool OPEN, bool ABSORB, bool TAIL, int MODE = 0>
+// keystream and no Poly1305); 4/5/6 non-temporal loads / stores / both; 7 no payload stores.
+// LINES: the frame blocks go through the wave's LDS ring (block t - 1 is read
+// back before the rounds and stored after them; block t goes into the ring).
+template <bool OPEN, bool ABSORB, bool TAIL, int MODE = 0, bool LINES = false>
 __device__ __forceinline__ void pipe_step(uint4 *pl, const Stream &st, const Mul &r, Acc &h, Chunk &pi, Chunk &buf,
-                                          uint4 &prev, bool &have_prev, uint32_t t, uint32_t nb, uint32_t c0) {
+                                          uint4 &prev, bool &have_prev, uint32_t t, uint32_t nb, uint32_t c0,
+                                          const Ring &R) {
     uint32_t ks[16];
+    constexpr bool FLUSH = LINES && ABSORB && !TAIL;
+    Ring4 fl;
+    if constexpr (FLUSH) {
+        wave_sync(); // block t - 1 was put by every lane
+        fl = ring_get(R, (t - 1) & 1u);
+    }
     if constexpr (MODE == 2) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) ks[i] = t * 16 + i;
@@ -117,8 +204,13 @@ __device__ __forceinline__ void pipe_step(uint4 *pl, const Stream &st, const Mul
         buf.q0.x += t; buf.q1.y ^= t; buf.q2.z += h.h0; buf.q3.w ^= t; // fake next chunk, loop-carried
         return;
     }
-    constexpr int NT = MODE >= 4 ? MODE - 3 : 0;
-    if constexpr (TAIL) {
+    constexpr int NT = MODE == 7 ? 4 : MODE >= 4 ? MODE - 3 : 0;
+    if constexpr (LINES && !TAIL) {
+        ring_put(R, t & 1u, prev, x.q0, x.q1, x.q2); // prev: the header before the first chunk
+        if constexpr (FLUSH) ring_store(R, fl, t - 1);
+        prev = x.q3;
+        have_prev = true;
+    } else if constexpr (TAIL) {
         const uint32_t cnt = nb & 3u;
         if (have_prev) st16<NT>(dst - 1, prev);
         st16<NT>(dst + 0, x.q0); // cnt >= 1
@@ -145,37 +237,44 @@ __device__ __forceinline__ void pipe_step(uint4 *pl, const Stream &st, const Mul
 // inside the loop is unconditional; chunk c always lives in buffer c % kDepth.
 // head / has_head: the DataHeader a seal writes in front of the payload (only
 // the lane whose segment starts the payload has one).
-template <bool OPEN, int MODE = 0>
+// LINES (a wave of valid packets of one size, has_head set): blocks through the LDS ring.
+template <bool OPEN, int MODE = 0, bool LINES = false>
 __device__ __forceinline__ Acc pipe_pass(uint4 *pl, const Stream &st, const Mul &r, uint32_t nb, uint32_t c0,
-                                         Chunk &b0, Chunk &b1, Chunk &b2, uint4 head, bool has_head) {
+                                         Chunk &b0, Chunk &b1, Chunk &b2, uint4 head, bool has_head,
+                                         const Ring &R) {
     const uint32_t F = nb >> 2, bl = nb & 3u; // full chunks, blocks in the partial last chunk
     Acc h = {0, 0, 0, 0, 0};
     Chunk pi = {};
     uint4 prev = head; // block still to be stored just in front of the current chunk
     bool have_prev = has_head;
     uint32_t pending = 0; // blocks of pi not yet absorbed
+    if constexpr (LINES) wave_sync(); // the previous packet's last read-back is done
     if (F > 0) {
-        pipe_step<OPEN, false, false, MODE>(pl, st, r, h, pi, b0, prev, have_prev, 0, nb, c0);
+        pipe_step<OPEN, false, false, MODE, LINES>(pl, st, r, h, pi, b0, prev, have_prev, 0, nb, c0, R);
         uint32_t t = 1;
         // whole rounds of kDepth steps only: a step that may be skipped would
         // leave the waitcnt pass a path without its memory operations
         // (vmcnt(0) at the next one); the remainder steps run after the loop
         if constexpr (kDepth == 3) {
             for (; t + 2 < F; t += 3) {
-                pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0);
-                pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b2, prev, have_prev, t + 1, nb, c0);
-                pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b0, prev, have_prev, t + 2, nb, c0);
+                pipe_step<OPEN, true, false, MODE, LINES>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R);
+                pipe_step<OPEN, true, false, MODE, LINES>(pl, st, r, h, pi, b2, prev, have_prev, t + 1, nb, c0, R);
+                pipe_step<OPEN, true, false, MODE, LINES>(pl, st, r, h, pi, b0, prev, have_prev, t + 2, nb, c0, R);
             }
-            if (t < F) pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0);
-            if (t + 1 < F) pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b2, prev, have_prev, t + 1, nb, c0);
+            if (t < F) pipe_step<OPEN, true, false, MODE, LINES>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R);
+            if (t + 1 < F) pipe_step<OPEN, true, false, MODE, LINES>(pl, st, r, h, pi, b2, prev, have_prev, t + 1, nb, c0, R);
         } else {
             for (; t + 1 < F; t += 2) {
-                pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0);
-                pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b0, prev, have_prev, t + 1, nb, c0);
+                pipe_step<OPEN, true, false, MODE, LINES>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R);
+                pipe_step<OPEN, true, false, MODE, LINES>(pl, st, r, h, pi, b0, prev, have_prev, t + 1, nb, c0, R);
             }
-            if (t < F) pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0);
+            if (t < F) pipe_step<OPEN, true, false, MODE, LINES>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R);
         }
         pending = 4;
+        if constexpr (LINES) { // the last full block
+            wave_sync();
+            ring_store(R, ring_get(R, (F - 1) & 1u), F - 1);
+        }
     }
     if (bl > 0) {
         // chunk F lives in b(F % kDepth); select by value (a reference select
@@ -183,11 +282,11 @@ __device__ __forceinline__ Acc pipe_pass(uint4 *pl, const Stream &st, const Mul 
         const uint32_t k = F % kDepth;
         Chunk bp = {k == 1 ? b1.q0 : k == 2 ? b2.q0 : b0.q0, k == 1 ? b1.q1 : k == 2 ? b2.q1 : b0.q1,
                     k == 1 ? b1.q2 : k == 2 ? b2.q2 : b0.q2, k == 1 ? b1.q3 : k == 2 ? b2.q3 : b0.q3};
-        if (F > 0) pipe_step<OPEN, true, true, MODE>(pl, st, r, h, pi, bp, prev, have_prev, F, nb, c0);
-        else pipe_step<OPEN, false, true, MODE>(pl, st, r, h, pi, bp, prev, have_prev, F, nb, c0);
+        if (F > 0) pipe_step<OPEN, true, true, MODE, LINES>(pl, st, r, h, pi, bp, prev, have_prev, F, nb, c0, R);
+        else pipe_step<OPEN, false, true, MODE, LINES>(pl, st, r, h, pi, bp, prev, have_prev, F, nb, c0, R);
         pending = bl;
     }
-    if (have_prev && MODE != 1) st16<(MODE >= 4 ? MODE - 3 : 0)>(pl + 4 * F - 1, prev);
+    if (have_prev && MODE != 1) st16<(MODE == 7 ? 4 : MODE >= 4 ? MODE - 3 : 0)>(pl + 4 * F - 1, prev);
     absorb_chunk(h, pi, r, pending); // the last chunk's blocks
     return h;
 }
@@ -280,10 +379,14 @@ __device__ __forceinline__ Acc combine_segments(Acc h, const Mul &r, uint32_t af
 // segment j; lane 0 writes header, tag and status.
 template <int MODE>
 __device__ __forceinline__ void pipe_seal_packet(const SealArgs &a, uint32_t i, const rg_pkt_desc &d, uint32_t j,
-                                                 uint32_t G) {
+                                                 uint32_t G, bool lines_ok) {
     const uint32_t P = d.len;
     const bool valid = d.key_idx < a.nkeys && (P & 15u) == 0 && (d.offset & 15u) == 0 && P <= kMaxPayload &&
                        d.offset <= a.buf_len && P + 32 <= a.buf_len - d.offset;
+    // block stores through the LDS ring: every lane of the wave a valid packet of one size
+    bool lines = false;
+    if constexpr (MODE == 0)
+        lines = lines_ok && G == 1 && __ballot(valid && P == uniform_u32(P)) == ~0ull;
     if (!valid) {
         if (a.status && j == 0) a.status[i] = d.key_idx == RG_KEY_SKIP ? RG_PKT_REJECTED : RG_PKT_INVALID;
         return;
@@ -300,7 +403,7 @@ __device__ __forceinline__ void pipe_seal_packet(const SealArgs &a, uint32_t i, 
         b1 = b0;
         b2 = b0;
     } else {
-        constexpr int NT = MODE >= 4 ? MODE - 3 : 0;
+        constexpr int NT = MODE >= 4 && MODE != 7 ? MODE - 3 : 0;
         load_chunk<NT>(b0, pl, 0, sg.nb ? sg.nb - 1 : 0);
         load_chunk<NT>(b1, pl, 1, sg.nb ? sg.nb - 1 : 0);
         if constexpr (kDepth == 3) load_chunk<NT>(b2, pl, 2, sg.nb ? sg.nb - 1 : 0);
@@ -316,8 +419,14 @@ __device__ __forceinline__ void pipe_seal_packet(const SealArgs &a, uint32_t i, 
     // DataHeader {4, receiver, counter} (rustyguard-core/src/lib.rs:286-290), stored by segment 0
     // together with the first payload blocks
     const bool head = a.receivers != nullptr && j == 0;
-    const uint4 hdr = make_uint4(4u, head ? a.receivers[d.key_idx] : 0u, n1, n2);
-    Acc h = pipe_pass<false, MODE>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, hdr, head);
+    uint4 hdr = make_uint4(4u, head ? a.receivers[d.key_idx] : 0u, n1, n2);
+    Acc h;
+    if (lines) { // wave-uniform
+        if (!head) hdr = *reinterpret_cast<const uint4 *>(frame); // block 0 is stored whole: header unchanged
+        h = pipe_pass<false, MODE, true>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, hdr, true, make_ring(frame));
+    } else {
+        h = pipe_pass<false, MODE, false>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, hdr, head, Ring{});
+    }
     RG_MARK(3, h.h4);
     h = combine_segments(h, r, sg.after, G);
     RG_MARK(5, h.h4);
@@ -335,7 +444,7 @@ __device__ __forceinline__ void pipe_seal_packet(const SealArgs &a, uint32_t i, 
 // (constant-time compare, identical on every lane of the group) makes each
 // lane re-apply its segment's keystream, so the frame is left unchanged.
 __device__ __forceinline__ void pipe_open_packet(const OpenArgs &a, uint32_t i, const rg_pkt_desc &d, uint32_t j,
-                                                 uint32_t G) {
+                                                 uint32_t G, bool lines_ok) {
     const uint32_t W = d.len;
     uint32_t st;
     if (d.key_idx == RG_KEY_SKIP) st = RG_PKT_REJECTED;
@@ -373,6 +482,8 @@ __device__ __forceinline__ void pipe_open_packet(const OpenArgs &a, uint32_t i, 
             if (W < 32) st = RG_PKT_DECRYPT_ERR;
         }
     }
+    // block stores through the LDS ring: every lane of the wave a data packet of one size
+    const bool lines = lines_ok && G == 1 && __ballot(st == 0xFF && W == uniform_u32(W)) == ~0ull;
     if (st != 0xFF) {
         if (j == 0) {
             a.status[i] = (uint8_t)st;
@@ -385,14 +496,18 @@ __device__ __forceinline__ void pipe_open_packet(const OpenArgs &a, uint32_t i, 
     uint32_t ks[16];
     stream_block(stm, 0, ks);
     const Mul r = make_mul(ks[0], ks[1], ks[2], ks[3]);
-    Acc h = pipe_pass<true>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, make_uint4(0, 0, 0, 0), false);
+    Acc h;
+    if (lines) h = pipe_pass<true, 0, true>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, hdr, true, make_ring(frame)); // header unchanged
+    else h = pipe_pass<true, 0, false>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, make_uint4(0, 0, 0, 0), false, Ring{});
     h = combine_segments(h, r, sg.after, G);
     uint32_t tag[4];
     pipe_tag(h, r, P, ks + 4, tag);
     const uint32_t diff = (tag[0] ^ want.x) | (tag[1] ^ want.y) | (tag[2] ^ want.z) | (tag[3] ^ want.w);
     if (diff != 0) {
         // restore this lane's segment: plaintext ^ keystream = ciphertext
-        // (callers never read the buffer on Err, but the frame is left as it came)
+        // (callers never read the buffer on Err, but the frame is left as it came); with block stores
+        // other lanes wrote this frame: their stores complete and this lane's cached lines go first
+        if (lines) __threadfence();
         for (uint32_t c = 0; 4 * c < sg.nb; ++c) {
             stream_block(stm, sg.c0 + c + 1, ks);
             const uint32_t cnt = chunk_blocks(sg.nb, c);
@@ -524,20 +639,23 @@ __device__ __forceinline__ void pipe_walk(uint32_t n, uint32_t lg0, const PipePl
     }
 }
 
-template <int MODE> __global__ __launch_bounds__(256) void pipe_seal_kernel(SealArgs a, uint32_t lg, PipePlan pp) {
+// flags: bits 0-1 log2 lanes per packet (without a plan), kPipeLinesFlag: the LDS ring is reserved
+template <int MODE> __global__ __launch_bounds__(256) void pipe_seal_kernel(SealArgs a, uint32_t flags, PipePlan pp) {
     const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
     uint64_t marks[2] = {0, 0};
-    pipe_walk(a.n, lg, pp, a.desc, a.dbg != nullptr, marks, [=](uint32_t i, const rg_pkt_desc &d, uint32_t j, uint32_t G) {
-        pipe_seal_packet<MODE>(a, i, d, j, G);
+    const bool lines = RG_PIPE_LINES && (flags & kPipeLinesFlag) != 0;
+    pipe_walk(a.n, flags & 3u, pp, a.desc, a.dbg != nullptr, marks, [=](uint32_t i, const rg_pkt_desc &d, uint32_t j, uint32_t G) {
+        pipe_seal_packet<MODE>(a, i, d, j, G, lines);
     });
     if (a.dbg) pipe_stamp(a.dbg, t0, r0, marks);
 }
 
-__global__ __launch_bounds__(256) void pipe_open_kernel(OpenArgs a, uint32_t lg, PipePlan pp) {
+__global__ __launch_bounds__(256) void pipe_open_kernel(OpenArgs a, uint32_t flags, PipePlan pp) {
     const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
     uint64_t marks[2] = {0, 0};
-    pipe_walk(a.n, lg, pp, a.desc, a.dbg != nullptr, marks, [=](uint32_t i, const rg_pkt_desc &d, uint32_t j, uint32_t G) {
-        pipe_open_packet(a, i, d, j, G);
+    const bool lines = RG_PIPE_LINES && (flags & kPipeLinesFlag) != 0;
+    pipe_walk(a.n, flags & 3u, pp, a.desc, a.dbg != nullptr, marks, [=](uint32_t i, const rg_pkt_desc &d, uint32_t j, uint32_t G) {
+        pipe_open_packet(a, i, d, j, G, lines);
     });
     if (a.dbg) pipe_stamp(a.dbg, t0, r0, marks);
 }
@@ -567,22 +685,24 @@ hipError_t launch_pipe(const SealArgs *sa, const OpenArgs *oa, const Launch &L, 
     } else {
         pipe_grid((uint64_t)n << lg, L, blocks, lds);
     }
-    if (sa && L.debug_mode == 1) hipLaunchKernelGGL(pipe_seal_kernel<1>, dim3(blocks), dim3(256), lds, s, *sa, lg, pp);
-    else if (sa && L.debug_mode == 2) hipLaunchKernelGGL(pipe_seal_kernel<2>, dim3(blocks), dim3(256), lds, s, *sa, lg, pp);
-    else if (sa && L.debug_mode == 4) hipLaunchKernelGGL(pipe_seal_kernel<4>, dim3(blocks), dim3(256), lds, s, *sa, lg, pp);
-    else if (sa && L.debug_mode == 5) hipLaunchKernelGGL(pipe_seal_kernel<5>, dim3(blocks), dim3(256), lds, s, *sa, lg, pp);
-    else if (sa && L.debug_mode == 6) hipLaunchKernelGGL(pipe_seal_kernel<6>, dim3(blocks), dim3(256), lds, s, *sa, lg, pp);
-    else if (sa) hipLaunchKernelGGL(pipe_seal_kernel<0>, dim3(blocks), dim3(256), lds, s, *sa, lg, pp);
-    else hipLaunchKernelGGL(pipe_open_kernel, dim3(blocks), dim3(256), lds, s, *oa, lg, pp);
+    const uint32_t fl = lg | (lds >= 4 * kRingBytes ? kPipeLinesFlag : 0u);
+    if (sa && L.debug_mode == 1) hipLaunchKernelGGL(pipe_seal_kernel<1>, dim3(blocks), dim3(256), lds, s, *sa, fl, pp);
+    else if (sa && L.debug_mode == 2) hipLaunchKernelGGL(pipe_seal_kernel<2>, dim3(blocks), dim3(256), lds, s, *sa, fl, pp);
+    else if (sa && L.debug_mode == 4) hipLaunchKernelGGL(pipe_seal_kernel<4>, dim3(blocks), dim3(256), lds, s, *sa, fl, pp);
+    else if (sa && L.debug_mode == 5) hipLaunchKernelGGL(pipe_seal_kernel<5>, dim3(blocks), dim3(256), lds, s, *sa, fl, pp);
+    else if (sa && L.debug_mode == 6) hipLaunchKernelGGL(pipe_seal_kernel<6>, dim3(blocks), dim3(256), lds, s, *sa, fl, pp);
+    else if (sa && L.debug_mode == 7) hipLaunchKernelGGL(pipe_seal_kernel<7>, dim3(blocks), dim3(256), lds, s, *sa, fl, pp);
+    else if (sa) hipLaunchKernelGGL(pipe_seal_kernel<0>, dim3(blocks), dim3(256), lds, s, *sa, fl, pp);
+    else hipLaunchKernelGGL(pipe_open_kernel, dim3(blocks), dim3(256), lds, s, *oa, fl, pp);
     return hipGetLastError();
 }
 
 hipError_t prepare_pipe_kernels(int max_wg[2]) {
-    const void *f[7] = {(const void *)pipe_seal_kernel<0>, (const void *)pipe_open_kernel,
+    const void *f[8] = {(const void *)pipe_seal_kernel<0>, (const void *)pipe_open_kernel,
                         (const void *)pipe_seal_kernel<1>, (const void *)pipe_seal_kernel<2>,
                         (const void *)pipe_seal_kernel<4>, (const void *)pipe_seal_kernel<5>,
-                        (const void *)pipe_seal_kernel<6>};
-    for (int w = 0; w < 7; ++w) {
+                        (const void *)pipe_seal_kernel<6>, (const void *)pipe_seal_kernel<7>};
+    for (int w = 0; w < 8; ++w) {
         hipError_t e = hipFuncSetAttribute(f[w], hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsPerCu);
         if (e != hipSuccess) return e;
         int nb = 0;
