@@ -299,7 +299,7 @@ int rg_set_debug_buffer(rg_ctx *ctx, void *dev_ptr) {
 
 int rg_set_debug_mode(rg_ctx *ctx, int mode) {
     if (!ctx) return set_err(RG_EINVAL, "null context");
-    if (mode < 0 || mode > 7) return set_err(RG_EINVAL, "debug mode must be 0..7");
+    if (mode < 0 || mode > 8) return set_err(RG_EINVAL, "debug mode must be 0..8");
     ctx->debug_mode = mode;
     return RG_OK;
 }

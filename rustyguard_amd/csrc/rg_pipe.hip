@@ -79,33 +79,45 @@ __device__ __forceinline__ void absorb_chunk(Acc &h, const Chunk &c, const Mul &
     acc_block_pred(h, c.q3, r, cnt > 3);
 }
 
-// ------------------------------------------------------------- block stores
+// ------------------------------------------------------------- line stores
 // When all 64 lanes of a wave hold valid packets of one size (one lane per
-// packet), the 64-byte frame blocks leave through a wave-private LDS ring: a
-// lane-per-frame store instruction puts one 16-byte piece into each of 64
-// frames (64 cache lines per instruction, each 64-byte block completed by four
-// instructions), whereas from the ring each store instruction writes whole
-// 64-byte blocks of 16 frames, four lanes per block.  Step t puts its block t
-// into ring set t & 1 and stores block t - 1, read back at the start of the
-// step, so the LDS round trip hides behind the keystream rounds.  Frame p's
-// 128 bytes hold piece j of set s in slot 4 (s ^ ((p >> 2) & 1)) + (j ^ (p & 3)):
-// conflict-free for the frame-major ds_write_b128 (8-lane groups, 128-byte
-// rows) and the block-major ds_read_b128 (16-lane groups, 256-byte rows).
+// packet), the frames leave through a wave-private LDS ring in whole 128-byte
+// lines: a lane-per-frame store instruction puts one 16-byte piece into each
+// of 64 frames (64 cache lines per instruction, a line completed by eight
+// instructions over two steps, and measured 1.29x the algorithmic write bytes
+// at config 5), whereas from the ring each store instruction writes whole
+// lines of 8 frames, eight lanes per line.  Step t puts its 64-byte block t
+// (pieces 4t .. 4t+3 of the frame: the header, payload blocks, the tag)
+// into ring set t & 3; steps 2k+2 and 2k+3 store line k (blocks 2k, 2k+1) of
+// frames 0-31 and 32-63, read back at the start of the step so that the LDS
+// round trip hides behind the keystream rounds.  Every step issues the same
+// LDS and store instructions (no parity branch: the vmcnt waits stay exact).
+// Frame p's 256 bytes hold piece j of set s in slot (4 s + j) ^ g(p & 7),
+// g = {0, 1, 10, 11, 4, 5, 14, 15}: conflict-free for the frame-major
+// ds_write_b128 (8-lane groups, 128-byte rows) and the line-major
+// ds_read_b128 (16-lane groups, 256-byte rows).
 #ifndef RG_PIPE_LINES
 #define RG_PIPE_LINES 1
 #endif
-constexpr uint32_t kPipeLinesFlag = 4u; // launch flag bit (bits 0-1: log2 lanes per packet)
-constexpr uint32_t kRingBytes = 64u * 128u; // per wave
+// open absorbs each chunk's ciphertext in its own step (loaded three steps ahead), so no loaded
+// chunk is copied into a second register set (a copy of a load in flight makes the wave wait for it)
+#ifndef RG_PIPE_OPEN_CUR
+#define RG_PIPE_OPEN_CUR 1
+#endif
+constexpr bool PIPE_OPEN_CUR = RG_PIPE_OPEN_CUR != 0;
+constexpr uint32_t kPipeLinesFlag = 4u;      // launch flag bit (bits 0-1: log2 lanes per packet)
+constexpr uint32_t kRingBytes = 64u * 256u; // per wave
 // (plain vector types: HIP's uint4 has no assignment in a qualified address space)
 typedef __attribute__((address_space(3))) v4u lds_u4;
 typedef __attribute__((address_space(1))) v4u glb_u4;
 __device__ __forceinline__ v4u to_v4(const uint4 &a) { return v4u{a.x, a.y, a.z, a.w}; }
-__device__ __forceinline__ uint4 from_v4(const v4u &a) { return make_uint4(a.x, a.y, a.z, a.w); }
+__device__ __forceinline__ uint32_t ring_g(uint32_t p) { return (p & 1u) ^ (((p >> 1) & 1u) * 10u) ^ (((p >> 2) & 1u) * 4u); }
+
 struct Ring {
-    lds_u4 *wr;    // this lane's frame record (slot index added per piece)
-    lds_u4 *rd;    // block-major read base: frame lane / 4, piece lane % 4 (set 0)
-    glb_u4 *fr[4]; // frame 16 q + lane / 4, piece lane % 4 (bytes 16 (lane % 4) of block 0)
-    uint32_t wsw, rsw; // lane's slot swizzles: writes (p = lane), reads (set bit only)
+    lds_u4 *wr;       // this lane's frame record
+    lds_u4 *rd;       // line-major reads: frame lane / 8 (+ 8 q + 32 h), slot base
+    glb_u4 *fr[2][4]; // frame 32 h + 8 q + lane / 8, byte 16 (lane % 8) of line 0
+    uint32_t gw, gr;  // slot swizzles: this lane's frame (writes), frame lane / 8 (reads)
 };
 
 __device__ __forceinline__ Ring make_ring(uint8_t *frame) {
@@ -113,25 +125,26 @@ __device__ __forceinline__ Ring make_ring(uint8_t *frame) {
     const uint32_t lane = threadIdx.x & 63;
     lds_u4 *base = (lds_u4 *)(pipe_lds + (threadIdx.x >> 6) * kRingBytes);
     Ring R;
-    R.wr = base + 8 * lane;
-    R.wsw = (((lane >> 2) & 1u) << 2) | (lane & 3u);
-    // reads: frame p = 16 q + lane / 4, piece w = lane % 4 -> slot 4 (s ^ ((p >> 2) & 1)) + (w ^ (p & 3))
-    R.rsw = ((lane >> 4) & 1u) << 2;
-    R.rd = base + 8 * (lane >> 2) + ((lane & 3u) ^ ((lane >> 2) & 3u));
+    R.wr = base + 16 * lane;
+    R.gw = ring_g(lane);
+    R.rd = base + 16 * (lane >> 3);
+    R.gr = ring_g(lane >> 3);
     const uint64_t f = reinterpret_cast<uint64_t>(frame);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const uint32_t src = 16 * q + (lane >> 2);
-        const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)f, (int)src), hi = (uint32_t)__shfl((int)(uint32_t)(f >> 32), (int)src);
-        R.fr[q] = (glb_u4 *)((((uint64_t)hi << 32) | lo) + 16 * (lane & 3u));
-    }
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int src = 32 * h + 8 * q + (int)(lane >> 3);
+            const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)f, src), hi = (uint32_t)__shfl((int)(uint32_t)(f >> 32), src);
+            R.fr[h][q] = (glb_u4 *)((((uint64_t)hi << 32) | lo) + 16 * (lane & 7u));
+        }
     return R;
 }
 
-// block (4 pieces) of this lane's frame into set s
-__device__ __forceinline__ void ring_put(const Ring &R, uint32_t s, const uint4 &a, const uint4 &b, const uint4 &c,
+// block t (4 pieces) of this lane's frame into set t & 3
+__device__ __forceinline__ void ring_put(const Ring &R, uint32_t t, const uint4 &a, const uint4 &b, const uint4 &c,
                                          const uint4 &d) {
-    const uint32_t sw = R.wsw ^ (s << 2);
+    const uint32_t sw = (4 * (t & 3u)) ^ R.gw;
     R.wr[sw ^ 0] = to_v4(a);
     R.wr[sw ^ 1] = to_v4(b);
     R.wr[sw ^ 2] = to_v4(c);
@@ -141,19 +154,26 @@ __device__ __forceinline__ void ring_put(const Ring &R, uint32_t s, const uint4 
 struct Ring4 {
     v4u v[4];
 };
-// set s read back block-major: v[q] = piece lane % 4 of frame 16 q + lane / 4
-__device__ __forceinline__ Ring4 ring_get(const Ring &R, uint32_t s) {
-    const lds_u4 *r = R.rd + (R.rsw ^ (s << 2));
+// half h of line k read back: v[q] = piece lane % 8 of line k of frame 32 h + 8 q + lane / 8
+__device__ __forceinline__ Ring4 ring_get(const Ring &R, uint32_t k, uint32_t h) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t set = (2 * k + ((lane >> 2) & 1u)) & 3u;
+    const lds_u4 *r = R.rd + 512 * h + ((4 * set + (lane & 3u)) ^ R.gr);
     Ring4 o;
 #pragma unroll
     for (int q = 0; q < 4; ++q) o.v[q] = r[128 * q];
     return o;
 }
 
-// store block b of the 64 frames from a read-back set
-__device__ __forceinline__ void ring_store(const Ring &R, const Ring4 &x, uint32_t b) {
+// store it (MASK: pieces of block 2k+1 only when that block is in the ring, i.e. 2k+1 < nblk)
+template <bool MASK = false>
+__device__ __forceinline__ void ring_store(const Ring &R, const Ring4 &x, uint32_t k, uint32_t h, uint32_t nblk = 0) {
+    if constexpr (MASK) {
+        const uint32_t lane = threadIdx.x & 63;
+        if (((lane >> 2) & 1u) && 2 * k + 1 >= nblk) return;
+    }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) R.fr[q][4 * b] = x.v[q];
+    for (int q = 0; q < 4; ++q) (h ? R.fr[1][q] : R.fr[0][q])[8 * k] = x.v[q];
 }
 
 // One step: keystream block t+1 -- with the previous chunk's four Poly1305
@@ -170,26 +190,35 @@ __device__ __forceinline__ void ring_store(const Ring &R, const Ring4 &x, uint32
 // steps were measured at 1.66x the algorithmic write bytes (profiles/).
 // MODE (seal diagnostics, rg_set_debug_mode): 0 normal; 1 compute only (no
 // payload loads or stores, loop-carried fake data); 2 memory only (no
-// keystream and no Poly1305); 4/5/6 non-temporal loads / stores / both; 7 no payload stores.
-// LINES: the frame blocks go through the wave's LDS ring (block t - 1 is read
-// back before the rounds and stored after them; block t goes into the ring).
-template <bool OPEN, bool ABSORB, bool TAIL, int MODE = 0, bool LINES = false>
+// keystream and no Poly1305); 4/5/6 non-temporal loads / stores / both; 7 no payload stores;
+// 8 block stores all to block 0 of the frames (cache-resident: store issue without HBM writes).
+// LINES: the frame blocks go through the wave's LDS ring (block t goes into
+// the ring; with FLUSH, half t & 1 of line (t - 2) / 2 is read back before the
+// rounds and stored after them).
+template <bool OPEN, bool ABSORB, bool TAIL, int MODE = 0, bool LINES = false, bool FLUSH = false>
 __device__ __forceinline__ void pipe_step(uint4 *pl, const Stream &st, const Mul &r, Acc &h, Chunk &pi, Chunk &buf,
                                           uint4 &prev, bool &have_prev, uint32_t t, uint32_t nb, uint32_t c0,
                                           const Ring &R) {
     uint32_t ks[16];
-    constexpr bool FLUSH = LINES && ABSORB && !TAIL;
+    static_assert(!FLUSH || (LINES && ABSORB && !TAIL), "flush steps");
     Ring4 fl;
     if constexpr (FLUSH) {
         wave_sync(); // block t - 1 was put by every lane
-        fl = ring_get(R, (t - 1) & 1u);
+        fl = ring_get(R, (t - 2) >> 1, t & 1u);
     }
     if constexpr (MODE == 2) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) ks[i] = t * 16 + i;
         h.h0 ^= pi.q0.x ^ pi.q1.y ^ pi.q2.z ^ pi.q3.w;
     } else stream_block_hooked(st, c0 + t + 1, ks, [&](int dr) {
-        if constexpr (ABSORB) {
+        if constexpr (OPEN && PIPE_OPEN_CUR) { // this chunk's ciphertext (TAIL: its nb % 4 blocks)
+            const uint32_t bl = TAIL ? nb & 3u : 4u;
+            if (dr == 1) acc_block_pred(h, buf.q0, r, bl > 0);
+            if (dr == 3) acc_block_pred(h, buf.q1, r, bl > 1);
+            if (dr == 5) acc_block_pred(h, buf.q2, r, bl > 2);
+            if (dr == 7) acc_block_pred(h, buf.q3, r, bl > 3);
+            if (dr % 2 == 1) pin_acc(h);
+        } else if constexpr (ABSORB) {
             if (dr == 1) acc_block(h, pi.q0, r);
             if (dr == 3) acc_block(h, pi.q1, r);
             if (dr == 5) acc_block(h, pi.q2, r);
@@ -206,8 +235,8 @@ __device__ __forceinline__ void pipe_step(uint4 *pl, const Stream &st, const Mul
     }
     constexpr int NT = MODE == 7 ? 4 : MODE >= 4 ? MODE - 3 : 0;
     if constexpr (LINES && !TAIL) {
-        ring_put(R, t & 1u, prev, x.q0, x.q1, x.q2); // prev: the header before the first chunk
-        if constexpr (FLUSH) ring_store(R, fl, t - 1);
+        ring_put(R, t, prev, x.q0, x.q1, x.q2); // prev: the header before the first chunk
+        if constexpr (FLUSH) ring_store(R, fl, MODE == 8 ? 0u : (t - 2) >> 1, t & 1u);
         prev = x.q3;
         have_prev = true;
     } else if constexpr (TAIL) {
@@ -226,7 +255,7 @@ __device__ __forceinline__ void pipe_step(uint4 *pl, const Stream &st, const Mul
         prev = x.q3;
         have_prev = true;
     }
-    pi = OPEN ? buf : x;
+    if constexpr (!(OPEN && PIPE_OPEN_CUR)) pi = OPEN ? buf : x;
     if constexpr (!TAIL) load_chunk<NT>(buf, pl, t + kDepth, nb - 1);
 }
 
@@ -255,26 +284,38 @@ __device__ __forceinline__ Acc pipe_pass(uint4 *pl, const Stream &st, const Mul 
         // whole rounds of kDepth steps only: a step that may be skipped would
         // leave the waitcnt pass a path without its memory operations
         // (vmcnt(0) at the next one); the remainder steps run after the loop
-        if constexpr (kDepth == 3) {
-            for (; t + 2 < F; t += 3) {
-                pipe_step<OPEN, true, false, MODE, LINES>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R);
-                pipe_step<OPEN, true, false, MODE, LINES>(pl, st, r, h, pi, b2, prev, have_prev, t + 1, nb, c0, R);
-                pipe_step<OPEN, true, false, MODE, LINES>(pl, st, r, h, pi, b0, prev, have_prev, t + 2, nb, c0, R);
+        if constexpr (LINES) {
+            static_assert(kDepth == 3, "line stores: three chunk buffers");
+            // step 1 has no complete line yet; steps 2.. each store half a line
+            if (F > 1) pipe_step<OPEN, true, false, MODE, true>(pl, st, r, h, pi, b1, prev, have_prev, 1, nb, c0, R);
+            for (t = 2; t + 2 < F; t += 3) {
+                pipe_step<OPEN, true, false, MODE, true, true>(pl, st, r, h, pi, b2, prev, have_prev, t, nb, c0, R);
+                pipe_step<OPEN, true, false, MODE, true, true>(pl, st, r, h, pi, b0, prev, have_prev, t + 1, nb, c0, R);
+                pipe_step<OPEN, true, false, MODE, true, true>(pl, st, r, h, pi, b1, prev, have_prev, t + 2, nb, c0, R);
             }
-            if (t < F) pipe_step<OPEN, true, false, MODE, LINES>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R);
-            if (t + 1 < F) pipe_step<OPEN, true, false, MODE, LINES>(pl, st, r, h, pi, b2, prev, have_prev, t + 1, nb, c0, R);
+            if (t < F) pipe_step<OPEN, true, false, MODE, true, true>(pl, st, r, h, pi, b2, prev, have_prev, t, nb, c0, R);
+            if (t + 1 < F) pipe_step<OPEN, true, false, MODE, true, true>(pl, st, r, h, pi, b0, prev, have_prev, t + 1, nb, c0, R);
+            // the halves not stored yet: m = F - 2 .. 2 ceil(F / 2) - 1 (k = m / 2, h = m % 2); a
+            // last line of one block stores its first four pieces only
+            wave_sync();
+            for (uint32_t m = F >= 2 ? F - 2 : 0; m < 2 * ((F + 1) >> 1); ++m)
+                ring_store<true>(R, ring_get(R, m >> 1, m & 1u), MODE == 8 ? 0u : m >> 1, m & 1u, F);
+        } else if constexpr (kDepth == 3) {
+            for (; t + 2 < F; t += 3) {
+                pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R);
+                pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b2, prev, have_prev, t + 1, nb, c0, R);
+                pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b0, prev, have_prev, t + 2, nb, c0, R);
+            }
+            if (t < F) pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R);
+            if (t + 1 < F) pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b2, prev, have_prev, t + 1, nb, c0, R);
         } else {
             for (; t + 1 < F; t += 2) {
-                pipe_step<OPEN, true, false, MODE, LINES>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R);
-                pipe_step<OPEN, true, false, MODE, LINES>(pl, st, r, h, pi, b0, prev, have_prev, t + 1, nb, c0, R);
+                pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R);
+                pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b0, prev, have_prev, t + 1, nb, c0, R);
             }
-            if (t < F) pipe_step<OPEN, true, false, MODE, LINES>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R);
+            if (t < F) pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R);
         }
         pending = 4;
-        if constexpr (LINES) { // the last full block
-            wave_sync();
-            ring_store(R, ring_get(R, (F - 1) & 1u), F - 1);
-        }
     }
     if (bl > 0) {
         // chunk F lives in b(F % kDepth); select by value (a reference select
@@ -287,7 +328,7 @@ __device__ __forceinline__ Acc pipe_pass(uint4 *pl, const Stream &st, const Mul 
         pending = bl;
     }
     if (have_prev && MODE != 1) st16<(MODE == 7 ? 4 : MODE >= 4 ? MODE - 3 : 0)>(pl + 4 * F - 1, prev);
-    absorb_chunk(h, pi, r, pending); // the last chunk's blocks
+    if constexpr (!(OPEN && PIPE_OPEN_CUR)) absorb_chunk(h, pi, r, pending); // the last chunk's blocks
     return h;
 }
 
@@ -385,7 +426,7 @@ __device__ __forceinline__ void pipe_seal_packet(const SealArgs &a, uint32_t i, 
                        d.offset <= a.buf_len && P + 32 <= a.buf_len - d.offset;
     // block stores through the LDS ring: every lane of the wave a valid packet of one size
     bool lines = false;
-    if constexpr (MODE == 0)
+    if constexpr (MODE == 0 || MODE == 8)
         lines = lines_ok && G == 1 && __ballot(valid && P == uniform_u32(P)) == ~0ull;
     if (!valid) {
         if (a.status && j == 0) a.status[i] = d.key_idx == RG_KEY_SKIP ? RG_PKT_REJECTED : RG_PKT_INVALID;
@@ -692,17 +733,19 @@ hipError_t launch_pipe(const SealArgs *sa, const OpenArgs *oa, const Launch &L, 
     else if (sa && L.debug_mode == 5) hipLaunchKernelGGL(pipe_seal_kernel<5>, dim3(blocks), dim3(256), lds, s, *sa, fl, pp);
     else if (sa && L.debug_mode == 6) hipLaunchKernelGGL(pipe_seal_kernel<6>, dim3(blocks), dim3(256), lds, s, *sa, fl, pp);
     else if (sa && L.debug_mode == 7) hipLaunchKernelGGL(pipe_seal_kernel<7>, dim3(blocks), dim3(256), lds, s, *sa, fl, pp);
+    else if (sa && L.debug_mode == 8) hipLaunchKernelGGL(pipe_seal_kernel<8>, dim3(blocks), dim3(256), lds, s, *sa, fl, pp);
     else if (sa) hipLaunchKernelGGL(pipe_seal_kernel<0>, dim3(blocks), dim3(256), lds, s, *sa, fl, pp);
     else hipLaunchKernelGGL(pipe_open_kernel, dim3(blocks), dim3(256), lds, s, *oa, fl, pp);
     return hipGetLastError();
 }
 
 hipError_t prepare_pipe_kernels(int max_wg[2]) {
-    const void *f[8] = {(const void *)pipe_seal_kernel<0>, (const void *)pipe_open_kernel,
+    const void *f[9] = {(const void *)pipe_seal_kernel<0>, (const void *)pipe_open_kernel,
                         (const void *)pipe_seal_kernel<1>, (const void *)pipe_seal_kernel<2>,
                         (const void *)pipe_seal_kernel<4>, (const void *)pipe_seal_kernel<5>,
-                        (const void *)pipe_seal_kernel<6>, (const void *)pipe_seal_kernel<7>};
-    for (int w = 0; w < 8; ++w) {
+                        (const void *)pipe_seal_kernel<6>, (const void *)pipe_seal_kernel<7>,
+                        (const void *)pipe_seal_kernel<8>};
+    for (int w = 0; w < 9; ++w) {
         hipError_t e = hipFuncSetAttribute(f[w], hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsPerCu);
         if (e != hipSuccess) return e;
         int nb = 0;
