@@ -36,7 +36,7 @@ struct Chunk {
 #define RG_PIPE_DEPTH 3
 #endif
 constexpr int kDepth = RG_PIPE_DEPTH;
-static_assert(kDepth == 2 || kDepth == 3, "pipeline depth");
+static_assert(kDepth >= 2 && kDepth <= 4, "pipeline depth");
 
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 template <int NT> __device__ __forceinline__ uint4 ld16(const uint4 *p) {
@@ -105,6 +105,16 @@ __device__ __forceinline__ void absorb_chunk(Acc &h, const Chunk &c, const Mul &
 #define RG_PIPE_OPEN_CUR 1
 #endif
 constexpr bool PIPE_OPEN_CUR = RG_PIPE_OPEN_CUR != 0;
+#ifndef RG_PIPE_LOAD_FIRST
+#define RG_PIPE_LOAD_FIRST 0
+#endif
+constexpr bool PIPE_LOAD_FIRST = RG_PIPE_LOAD_FIRST != 0;
+// experiment: ring stores written through to memory (1), so that fewer dirty lines are left in L2
+// for the end-of-kernel write-back
+#ifndef RG_PIPE_WT
+#define RG_PIPE_WT 0
+#endif
+constexpr int PIPE_WT = RG_PIPE_WT;
 constexpr uint32_t kPipeLinesFlag = 4u;      // launch flag bit (bits 0-1: log2 lanes per packet)
 constexpr uint32_t kRingBytes = 64u * 256u; // per wave
 // (plain vector types: HIP's uint4 has no assignment in a qualified address space)
@@ -173,7 +183,14 @@ __device__ __forceinline__ void ring_store(const Ring &R, const Ring4 &x, uint32
         if (((lane >> 2) & 1u) && 2 * k + 1 >= nblk) return;
     }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) (h ? R.fr[1][q] : R.fr[0][q])[8 * k] = x.v[q];
+    for (int q = 0; q < 4; ++q) {
+        glb_u4 *dst = (h ? R.fr[1][q] : R.fr[0][q]) + 8 * k;
+        if constexpr (PIPE_WT != 0) // device-scope write-through (sc1): the line leaves L2 clean
+            // (the s_nop: a VALU write to the data registers of a store wider than 64 bits needs a wait
+            // state, which the hazard pass does not insert behind inline asm)
+            asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(dst), "v"(x.v[q]) : "memory");
+        else *dst = x.v[q];
+    }
 }
 
 // One step: keystream block t+1 -- with the previous chunk's four Poly1305
@@ -234,6 +251,12 @@ __device__ __forceinline__ void pipe_step(uint4 *pl, const Stream &st, const Mul
         return;
     }
     constexpr int NT = MODE == 7 ? 4 : MODE >= 4 ? MODE - 3 : 0;
+    if constexpr (PIPE_LOAD_FIRST && !TAIL) {
+        // chunk t + kDepth is requested before this step's stores: vmcnt retires in issue order, so a
+        // load issued behind a store is not usable before that store is acknowledged
+        if constexpr (!(OPEN && PIPE_OPEN_CUR)) pi = OPEN ? buf : x;
+        load_chunk<NT>(buf, pl, t + kDepth, nb - 1);
+    }
     if constexpr (LINES && !TAIL) {
         ring_put(R, t, prev, x.q0, x.q1, x.q2); // prev: the header before the first chunk
         if constexpr (FLUSH) ring_store(R, fl, MODE == 8 ? 0u : (t - 2) >> 1, t & 1u);
@@ -255,6 +278,7 @@ __device__ __forceinline__ void pipe_step(uint4 *pl, const Stream &st, const Mul
         prev = x.q3;
         have_prev = true;
     }
+    if constexpr (PIPE_LOAD_FIRST && !TAIL) return;
     if constexpr (!(OPEN && PIPE_OPEN_CUR)) pi = OPEN ? buf : x;
     if constexpr (!TAIL) load_chunk<NT>(buf, pl, t + kDepth, nb - 1);
 }
@@ -269,7 +293,7 @@ __device__ __forceinline__ void pipe_step(uint4 *pl, const Stream &st, const Mul
 // LINES (a wave of valid packets of one size, has_head set): blocks through the LDS ring.
 template <bool OPEN, int MODE = 0, bool LINES = false>
 __device__ __forceinline__ Acc pipe_pass(uint4 *pl, const Stream &st, const Mul &r, uint32_t nb, uint32_t c0,
-                                         Chunk &b0, Chunk &b1, Chunk &b2, uint4 head, bool has_head,
+                                         Chunk &b0, Chunk &b1, Chunk &b2, Chunk &b3, uint4 head, bool has_head,
                                          const Ring &R) {
     const uint32_t F = nb >> 2, bl = nb & 3u; // full chunks, blocks in the partial last chunk
     Acc h = {0, 0, 0, 0, 0};
@@ -285,9 +309,20 @@ __device__ __forceinline__ Acc pipe_pass(uint4 *pl, const Stream &st, const Mul 
         // leave the waitcnt pass a path without its memory operations
         // (vmcnt(0) at the next one); the remainder steps run after the loop
         if constexpr (LINES) {
-            static_assert(kDepth == 3, "line stores: three chunk buffers");
+            static_assert(kDepth >= 3, "line stores: three or four chunk buffers");
             // step 1 has no complete line yet; steps 2.. each store half a line
             if (F > 1) pipe_step<OPEN, true, false, MODE, true>(pl, st, r, h, pi, b1, prev, have_prev, 1, nb, c0, R);
+            if constexpr (kDepth == 4) {
+                for (t = 2; t + 3 < F; t += 4) {
+                    pipe_step<OPEN, true, false, MODE, true, true>(pl, st, r, h, pi, b2, prev, have_prev, t, nb, c0, R);
+                    pipe_step<OPEN, true, false, MODE, true, true>(pl, st, r, h, pi, b3, prev, have_prev, t + 1, nb, c0, R);
+                    pipe_step<OPEN, true, false, MODE, true, true>(pl, st, r, h, pi, b0, prev, have_prev, t + 2, nb, c0, R);
+                    pipe_step<OPEN, true, false, MODE, true, true>(pl, st, r, h, pi, b1, prev, have_prev, t + 3, nb, c0, R);
+                }
+                if (t < F) pipe_step<OPEN, true, false, MODE, true, true>(pl, st, r, h, pi, b2, prev, have_prev, t, nb, c0, R);
+                if (t + 1 < F) pipe_step<OPEN, true, false, MODE, true, true>(pl, st, r, h, pi, b3, prev, have_prev, t + 1, nb, c0, R);
+                if (t + 2 < F) pipe_step<OPEN, true, false, MODE, true, true>(pl, st, r, h, pi, b0, prev, have_prev, t + 2, nb, c0, R);
+            } else {
             for (t = 2; t + 2 < F; t += 3) {
                 pipe_step<OPEN, true, false, MODE, true, true>(pl, st, r, h, pi, b2, prev, have_prev, t, nb, c0, R);
                 pipe_step<OPEN, true, false, MODE, true, true>(pl, st, r, h, pi, b0, prev, have_prev, t + 1, nb, c0, R);
@@ -295,11 +330,22 @@ __device__ __forceinline__ Acc pipe_pass(uint4 *pl, const Stream &st, const Mul 
             }
             if (t < F) pipe_step<OPEN, true, false, MODE, true, true>(pl, st, r, h, pi, b2, prev, have_prev, t, nb, c0, R);
             if (t + 1 < F) pipe_step<OPEN, true, false, MODE, true, true>(pl, st, r, h, pi, b0, prev, have_prev, t + 1, nb, c0, R);
+            }
             // the halves not stored yet: m = F - 2 .. 2 ceil(F / 2) - 1 (k = m / 2, h = m % 2); a
             // last line of one block stores its first four pieces only
             wave_sync();
             for (uint32_t m = F >= 2 ? F - 2 : 0; m < 2 * ((F + 1) >> 1); ++m)
                 ring_store<true>(R, ring_get(R, m >> 1, m & 1u), MODE == 8 ? 0u : m >> 1, m & 1u, F);
+        } else if constexpr (kDepth == 4) {
+            for (; t + 3 < F; t += 4) {
+                pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R);
+                pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b2, prev, have_prev, t + 1, nb, c0, R);
+                pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b3, prev, have_prev, t + 2, nb, c0, R);
+                pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b0, prev, have_prev, t + 3, nb, c0, R);
+            }
+            if (t < F) pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R);
+            if (t + 1 < F) pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b2, prev, have_prev, t + 1, nb, c0, R);
+            if (t + 2 < F) pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b3, prev, have_prev, t + 2, nb, c0, R);
         } else if constexpr (kDepth == 3) {
             for (; t + 2 < F; t += 3) {
                 pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R);
@@ -321,8 +367,10 @@ __device__ __forceinline__ Acc pipe_pass(uint4 *pl, const Stream &st, const Mul 
         // chunk F lives in b(F % kDepth); select by value (a reference select
         // between the buffers would move them to scratch memory)
         const uint32_t k = F % kDepth;
-        Chunk bp = {k == 1 ? b1.q0 : k == 2 ? b2.q0 : b0.q0, k == 1 ? b1.q1 : k == 2 ? b2.q1 : b0.q1,
-                    k == 1 ? b1.q2 : k == 2 ? b2.q2 : b0.q2, k == 1 ? b1.q3 : k == 2 ? b2.q3 : b0.q3};
+        Chunk bp = {k == 1 ? b1.q0 : k == 2 ? b2.q0 : k == 3 ? b3.q0 : b0.q0,
+                    k == 1 ? b1.q1 : k == 2 ? b2.q1 : k == 3 ? b3.q1 : b0.q1,
+                    k == 1 ? b1.q2 : k == 2 ? b2.q2 : k == 3 ? b3.q2 : b0.q2,
+                    k == 1 ? b1.q3 : k == 2 ? b2.q3 : k == 3 ? b3.q3 : b0.q3};
         if (F > 0) pipe_step<OPEN, true, true, MODE, LINES>(pl, st, r, h, pi, bp, prev, have_prev, F, nb, c0, R);
         else pipe_step<OPEN, false, true, MODE, LINES>(pl, st, r, h, pi, bp, prev, have_prev, F, nb, c0, R);
         pending = bl;
@@ -438,16 +486,18 @@ __device__ __forceinline__ void pipe_seal_packet(const SealArgs &a, uint32_t i, 
     const Seg sg = make_seg(nb, j, G);
     // an empty segment reads (never writes) the payload start, which is in the frame
     uint4 *pl = reinterpret_cast<uint4 *>(frame + 16) + (sg.nb ? 4 * sg.c0 : 0);
-    Chunk b0, b1, b2 = {};
+    Chunk b0, b1, b2 = {}, b3 = {};
     if constexpr (MODE == 1) {
         b0 = {make_uint4(i, 1, 2, 3), make_uint4(4, i, 6, 7), make_uint4(8, 9, i, 11), make_uint4(12, 13, 14, i)};
         b1 = b0;
         b2 = b0;
+        b3 = b0;
     } else {
         constexpr int NT = MODE >= 4 && MODE != 7 ? MODE - 3 : 0;
         load_chunk<NT>(b0, pl, 0, sg.nb ? sg.nb - 1 : 0);
         load_chunk<NT>(b1, pl, 1, sg.nb ? sg.nb - 1 : 0);
-        if constexpr (kDepth == 3) load_chunk<NT>(b2, pl, 2, sg.nb ? sg.nb - 1 : 0);
+        if constexpr (kDepth >= 3) load_chunk<NT>(b2, pl, 2, sg.nb ? sg.nb - 1 : 0);
+        if constexpr (kDepth >= 4) load_chunk<NT>(b3, pl, 3, sg.nb ? sg.nb - 1 : 0);
     }
     const Key8 key = load_key(a.keys, d.key_idx);
     const uint64_t ctr = a.counters[i];
@@ -464,9 +514,9 @@ __device__ __forceinline__ void pipe_seal_packet(const SealArgs &a, uint32_t i, 
     Acc h;
     if (lines) { // wave-uniform
         if (!head) hdr = *reinterpret_cast<const uint4 *>(frame); // block 0 is stored whole: header unchanged
-        h = pipe_pass<false, MODE, true>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, hdr, true, make_ring(frame));
+        h = pipe_pass<false, MODE, true>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, b3, hdr, true, make_ring(frame));
     } else {
-        h = pipe_pass<false, MODE, false>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, hdr, head, Ring{});
+        h = pipe_pass<false, MODE, false>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, b3, hdr, head, Ring{});
     }
     RG_MARK(3, h.h4);
     h = combine_segments(h, r, sg.after, G);
@@ -508,10 +558,11 @@ __device__ __forceinline__ void pipe_open_packet(const OpenArgs &a, uint32_t i, 
     uint4 *safe = const_cast<uint4 *>(reinterpret_cast<const uint4 *>(a.desc + i));
     uint4 *pl = go ? reinterpret_cast<uint4 *>(frame + 16) + (sg.nb ? 4 * sg.c0 : 0) : safe;
     const uint4 hdr = *(desc_ok ? reinterpret_cast<const uint4 *>(frame) : safe);
-    Chunk b0, b1, b2 = {};
+    Chunk b0, b1, b2 = {}, b3 = {};
     load_chunk(b0, pl, 0, sg.nb ? sg.nb - 1 : 0);
     load_chunk(b1, pl, 1, sg.nb ? sg.nb - 1 : 0);
-    if constexpr (kDepth == 3) load_chunk(b2, pl, 2, sg.nb ? sg.nb - 1 : 0);
+    if constexpr (kDepth >= 3) load_chunk(b2, pl, 2, sg.nb ? sg.nb - 1 : 0);
+    if constexpr (kDepth >= 4) load_chunk(b3, pl, 3, sg.nb ? sg.nb - 1 : 0);
     const uint4 want = *(go ? reinterpret_cast<const uint4 *>(frame + 16 + P) : safe);
     const Key8 key = load_key(a.keys, go ? d.key_idx : 0);
     uint64_t ctr = 0;
@@ -538,8 +589,8 @@ __device__ __forceinline__ void pipe_open_packet(const OpenArgs &a, uint32_t i, 
     stream_block(stm, 0, ks);
     const Mul r = make_mul(ks[0], ks[1], ks[2], ks[3]);
     Acc h;
-    if (lines) h = pipe_pass<true, 0, true>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, hdr, true, make_ring(frame)); // header unchanged
-    else h = pipe_pass<true, 0, false>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, make_uint4(0, 0, 0, 0), false, Ring{});
+    if (lines) h = pipe_pass<true, 0, true>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, b3, hdr, true, make_ring(frame)); // header unchanged
+    else h = pipe_pass<true, 0, false>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, b3, make_uint4(0, 0, 0, 0), false, Ring{});
     h = combine_segments(h, r, sg.after, G);
     uint32_t tag[4];
     pipe_tag(h, r, P, ks + 4, tag);
