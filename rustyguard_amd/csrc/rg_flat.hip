@@ -353,6 +353,7 @@ template <bool OPEN> __global__ __launch_bounds__(64 * kFlatWaves) void flat_ker
     // diagnostics (debug mode 3): per wave, s_memtime at the end of each phase of its first sub-unit
     uint64_t *const dbg = OPEN ? A.oa.dbg : A.sa.dbg;
     uint64_t mk[8] = {__builtin_amdgcn_s_memtime(), 0, 0, 0, 0, 0, 0, 0};
+    const uint64_t rt0 = dbg ? __builtin_amdgcn_s_memrealtime() : 0; // 100 MHz wall clock (wave start / end)
 #define RG_FLAT_MARK(slot)                                                  \
     do {                                                                    \
         if (dbg && mk[slot] == 0) mk[slot] = __builtin_amdgcn_s_memtime(); \
@@ -818,8 +819,12 @@ template <bool OPEN> __global__ __launch_bounds__(64 * kFlatWaves) void flat_ker
     }
     if (dbg) {
         mk[7] = __builtin_amdgcn_s_memtime();
-        if (lane == 0)
+        const uint64_t rt1 = __builtin_amdgcn_s_memrealtime();
+        if (lane == 0) {
             for (int q = 0; q < 8; ++q) dbg[8ull * wid + q] = mk[q];
+            dbg[8ull * (nw + wid) + 0] = rt0; // second block of rows: wall-clock start and end
+            dbg[8ull * (nw + wid) + 1] = rt1;
+        }
     }
 #undef RG_FLAT_MARK
 }

@@ -47,6 +47,9 @@ for op in ("seal", "open"):
             b.open()
         torch.cuda.synchronize()
     d = dbg.cpu().numpy().reshape(-1, 8).astype(np.int64)
+    nwv = int((d[:1024, 0] != 0).sum())
+    rt = d[nwv:2 * nwv, :2].astype(np.float64) / 100.0  # wall clock, us (s_memrealtime at 100 MHz)
+    d = d[:nwv]
     d = d[d[:, 0] != 0]
     t0 = d[:, 0:1]
     rel = d - t0
@@ -64,6 +67,11 @@ for op in ("seal", "open"):
                                    for i in range(1, 8)]
     start = d[:, 0] - d[:, 0].min()
     out["start_spread_cyc"] = int(start.max())
+    if len(rt) and rt[:, 0].min() > 0:
+        r0 = rt[:, 0].min()
+        out["wall_us_start_pct_0_50_100"] = [round(float(x), 2) for x in np.percentile(rt[:, 0] - r0, [0, 50, 100])]
+        out["wall_us_end_pct_0_50_90_100"] = [round(float(x), 2) for x in np.percentile(rt[:, 1] - r0, [0, 50, 90, 100])]
+        out["clock_ghz"] = round(float(rel[:, 7].sum() / ((rt[:, 1] - rt[:, 0]).sum() * 1e3)), 3)
     res[op] = out
     print(op, json.dumps(out), flush=True)
     if args.per_wave and op == "seal":
