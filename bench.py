@@ -580,6 +580,11 @@ def main():
     # only counters of the kernel family this run used (a kernel change makes them stale)
     if pmc and pmc.get(dominant) and pmc[dominant].get("family") == eng.last_kernel():
         traffic = pmc[dominant].get("hbm_bytes_per_launch")
+        n_pmc = pmc[dominant].get("packets_per_launch")
+        if traffic and n_pmc and n_pmc != w.n:
+            # counters taken on another shard size of the same geometry (config 5 on one GPU vs a rank's
+            # shard): HBM bytes per packet carried over
+            traffic = int(round(traffic * w.n / n_pmc))
 
     out = {
         "metric": METRIC,

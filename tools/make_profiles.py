@@ -85,7 +85,7 @@ def main():
     if a.fetch and a.write:
         fetch, names = counter_means(a.fetch)
         write, _ = counter_means(a.write)
-        alg = {}
+        alg, npk = {}, None
         if a.bench:
             for line in open(a.bench):
                 if line.startswith("{"):
@@ -93,6 +93,7 @@ def main():
                     n = b["config"]["packets_per_gpu"]
                     p = b["config"]["mean_payload_bytes"] * n
                     alg = {"seal": int(2 * p + 32 * n), "open": int(2 * p + 33 * n)}
+                    npk = n
         res = {"source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), round {a.tag}",
                "workload": a.workload, "units": "bytes per launch; FETCH_SIZE KiB x 1024 x 2 (gfx950 correction), "
                                                 "WRITE_SIZE KiB x 1024"}
@@ -103,6 +104,8 @@ def main():
             wr = write[k]["WRITE_SIZE"] * 1024
             res[k] = {"kernel": names[k], "family": family_of(names[k]), "fetch_size_kib_raw": round(fetch[k]["FETCH_SIZE"], 1),
                       "read_bytes": int(rd), "write_bytes": int(wr), "hbm_bytes_per_launch": int(rd + wr)}
+            if npk:
+                res[k]["packets_per_launch"] = npk
             if k in alg:
                 res[k]["alg_bytes_per_launch"] = alg[k]
                 res[k]["traffic_over_alg"] = round((rd + wr) / alg[k], 3)

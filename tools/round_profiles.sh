@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 G="bash tools/gpu_run.sh"
 $G default || exit $?
 for W in cfg2 cfg3 cfg4; do RG_WORKLOAD=$W $G prof || exit $?; done
-for W in cfg2 cfg3; do RG_WORKLOAD=$W $G pmc_hbm || exit $?; done
+for W in cfg2 cfg3 cfg4 cfg5; do RG_WORKLOAD=$W $G pmc_hbm || exit $?; done
 RG_WORKLOADS="cfg2 cfg3 cfg4" $G valu || exit $?
 RG_WORKLOADS="cfg2 cfg3 cfg4 cfg5" $G bench_all || exit $?
 echo "round profiles done"
