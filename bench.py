@@ -307,6 +307,29 @@ def forged_open_timing(w, b, stream, frac: float, verify: bool):
             "open_gib_s": round(w.payload_bytes / (open_ms / 1e3) / 2**30, 3)}
 
 
+def hbm_copy_rate(stream, nbytes: int = 1 << 30, reps: int = 5):
+    """Achievable HBM bandwidth on this GPU for comparison with the 8 TB/s spec peak: a device-to-device
+    copy of a 1 GiB buffer (4x the Infinity Cache, so it streams from HBM), (read + written bytes) /
+    time, median of `reps` event-timed copies.  Outside the timed region."""
+    import torch
+
+    src = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    dst = torch.empty_like(src)
+    src.fill_(1)
+    with torch.cuda.stream(stream):
+        dst.copy_(src)  # warm-up
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+        for e0, e1 in evs:
+            e0.record(stream)
+            dst.copy_(src)
+            e1.record(stream)
+    torch.cuda.synchronize()
+    ms = sorted(e0.elapsed_time(e1) for e0, e1 in evs)[reps // 2]
+    del src, dst
+    return {"gb_s": round(2 * nbytes / (ms / 1e3) / 1e9, 1), "bytes": 2 * nbytes,
+            "how": "torch copy_ of a 1 GiB device buffer, read + write bytes / time, median of 5"}
+
+
 def cold_cache_timing(eng, w, b, stream, verify: bool):
     """Per-launch seal / open time when the batch is not cache resident: a batch smaller than the
     256 MB Infinity Cache stays there between a step's seal and open and across steps.  Copies
@@ -558,6 +581,7 @@ def main():
         assert (b.status[: w.n] == 0).all().item(), "open failed in the kernel-timing pass"
     cold = cold_cache_timing(eng, w, b, stream, args.verify) if args.cold and w.buf_bytes < MALL_BYTES else None
     forged = forged_open_timing(w, b, stream, args.forged, args.verify) if args.forged > 0 else None
+    copy_ceiling = hbm_copy_rate(stream) if rank == 0 else None
     if args.verify:
         strict_check(w, b, stream)
 
@@ -616,6 +640,8 @@ def main():
         "seal_gib_s": round(payload / (seal_ms / 1e3) / 2**30 * world, 3),
         "open_gib_s": round(payload / (open_ms / 1e3) / 2**30 * world, 3),
         "seal_mpkt_s": round(w.n / (seal_ms / 1e3) / 1e6 * world, 3),
+        # the same rate counted in wire bytes W = P + 32 per packet (header + tag), SURVEY §8(d)
+        "wire_gib_s": round(2 * w.wire_bytes * args.steps * world / tmax / 2**30, 3),
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "alg_bytes_per_launch": dom_alg,
@@ -625,6 +651,10 @@ def main():
     }
     if pmc:
         out["roofline"]["pmc_source"] = pmc.get("source")
+    if copy_ceiling:
+        # the spec peak stays the denominator; the copy rate is what a plain streaming kernel reaches here
+        out["roofline"]["copy_achievable"] = copy_ceiling
+        out["roofline"]["frac_of_copy"] = round(achieved / copy_ceiling["gb_s"], 4)
     # the bound that actually applies: integer VALU (ChaCha20 ARX + Poly1305 multiplies), see DESIGN.md §5
     ceil_gbs = valu_ceiling_gbs(w.desc["len"], False)
     pay_gbs = payload / (seal_ms / 1e3) / 1e9

@@ -194,7 +194,11 @@ int rg_set_debug_mode(rg_ctx *ctx, int mode);
 /* Per-wave s_memtime stamps are written to this device buffer, 8 x u64 per
  * wave: mode 3 on the tile kernels (setup, store, dma-issue, dma-wait, chunk,
  * tail, valid, real-time ticks at 100 MHz); any non-zero mode on the
- * pipelined kernel (cycles, 0, 0, 0, start tick, 4, valid, real-time ticks). */
+ * pipelined kernel (cycles, 0, 0, 0, start tick, 4, valid, real-time ticks);
+ * mode 3 on the flattened kernel (s_memtime at the end of each phase) plus a
+ * second block of rows after the first CUs x 4 (wall-clock start and end), so
+ * size the buffer for 2 x CUs x 4 x 8 u64 there.  Modes 7 and 8 (pipelined seal):
+ * no payload stores / all block stores to block 0. */
 int rg_set_debug_buffer(rg_ctx *ctx, void *dev_ptr);
 
 /* ----------------------------------------- host-memory batch (blocking) */
