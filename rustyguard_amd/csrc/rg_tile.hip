@@ -180,7 +180,7 @@ template <int G> struct StagedCfg {
     static constexpr uint32_t BUF = 64 * PPW * 16;  // bytes per window buffer per wave
     static constexpr uint32_t WAVE_LDS = 2 * BUF;   // double-buffered
     static constexpr uint32_t COMB = 8 * kSlotRows * 64 * 4; // segment hand-off slots, one per wave
-    static constexpr uint32_t FLAGS = 2 * 8 * 4;     // ready / ack generation per wave slot
+    static constexpr uint32_t FLAGS = 2 * 8 * 4 + 16; // ready / ack generation per wave slot, work counter
     static constexpr uint32_t WG_LDS = 8 * WAVE_LDS + COMB + FLAGS;
 };
 
@@ -202,6 +202,9 @@ __device__ __forceinline__ uint64_t realtime() { // 100 MHz constant clock
 }
 
 constexpr uint32_t kMinSegment = 4;
+#ifndef RG_TILE_DYN
+#define RG_TILE_DYN 1
+#endif
 
 __device__ __forceinline__ uint32_t pow2ceil(uint32_t x) { return x <= 1 ? 1u : 1u << (32 - __clz(x - 1)); }
 
@@ -285,7 +288,8 @@ __global__ __launch_bounds__(512) void tile_kernel(SealArgs sa, OpenArgs oa, Til
     uint32_t *const comb = reinterpret_cast<uint32_t *>(lds_raw + 8 * Cfg::WAVE_LDS); // [wave][kSlotRows][64]
     volatile uint32_t *const f_ready = reinterpret_cast<volatile uint32_t *>(lds_raw + 8 * Cfg::WAVE_LDS + Cfg::COMB);
     volatile uint32_t *const f_ack = f_ready + 8;
-    if (threadIdx.x < 16) f_ready[threadIdx.x] = 0;
+    uint32_t *const f_next = const_cast<uint32_t *>(f_ready) + 16; // next work item (dynamic deal)
+    if (threadIdx.x < 17) f_ready[threadIdx.x] = 0;
     __syncthreads();
 
     // Group schedule: the groups (largest class first) are dealt to the
@@ -295,16 +299,42 @@ __global__ __launch_bounds__(512) void tile_kernel(SealArgs sa, OpenArgs oa, Til
     // gets at most one.  The halves never synchronise with each other; the K
     // segment waves of one tile hand over their Poly1305 sums through LDS slots
     // guarded by per-wave generation flags.
+    //
+    // Dynamic deal (every class unsegmented, 8-wave workgroups): the two halves of a SIMD are not
+    // served evenly -- the older wave wins VALU issue, finishes its static share at ~60 % of the
+    // launch and leaves the younger one alone on the SIMD (one wave: no latency hiding, half-rate
+    // v_mad_u64_u32) for the rest (tools/stamps.py at config 4: wave ends 0.73 / 1.21 ms).  So the
+    // workgroup's tiles -- the same ones the static deal gives its two halves, in the same order --
+    // are taken by whichever of its waves is free, from one LDS counter: item c is round c / 8,
+    // half (c / 4) % 2, tile c % 4 of that group.  With segments (K > 1) the waves of a half work
+    // on one tile together and keep the static deal.
     const Sched sc = make_sched(tp, n);
     const uint32_t halves = blockDim.x / 256; // 1 when the host launched 4-wave workgroups
     const uint32_t S = halves * gridDim.x;
     const uint32_t my_slot = half == 0 ? blockIdx.x : S - 1 - blockIdx.x;
-    uint32_t gen = 0;
-    for (uint32_t base = 0; base < sc.total_groups; base += S) {
+    const uint32_t rounds = (sc.total_groups + S - 1) / S;
+    const bool dyn = RG_TILE_DYN && halves == 2 && __ballot(sc.K > 1) == 0; // same in every wave
+    uint32_t next_v = 0; // the next item, requested one item ahead (LDS atomic, lane 0)
+    if (dyn && lane == 0) next_v = atomicAdd(f_next, 1u);
+    uint32_t gen = 0, round_s = 0;
+    for (;;) {
+        uint32_t g, thw; // group, and this wave's tile (segment) slot in it
+        if (dyn) {
+            const uint32_t item = uniform_u32(__shfl((int)next_v, 0));
+            const uint32_t r = item >> 3;
+            if (r >= rounds) break;
+            if (lane == 0) next_v = atomicAdd(f_next, 1u);
+            const uint32_t sl = ((item >> 2) & 1u) == 0 ? blockIdx.x : S - 1 - blockIdx.x;
+            g = r * S + ((r & 1) ? S - 1 - sl : sl);
+            thw = item & 3u;
+        } else {
+            if (round_s >= rounds) break;
+            g = round_s * S + ((round_s & 1) ? S - 1 - my_slot : my_slot);
+            thw = hw;
+            ++round_s;
+        }
+        if (g >= sc.total_groups) continue; // uniform over the half (static deal: the last round only)
         ++gen;
-        const uint32_t round = base / S;
-        const uint32_t g = base + ((round & 1) ? S - 1 - my_slot : my_slot);
-        if (g >= sc.total_groups) continue; // uniform over the half
         if constexpr (STAMP) {
             const uint64_t t = stamp();
             t_tail += t - t_mark;
@@ -317,8 +347,8 @@ __global__ __launch_bounds__(512) void tile_kernel(SealArgs sa, OpenArgs oa, Til
         const uint32_t K = uniform_u32(__shfl(sc.K, pb));
         const uint32_t g0 = pb == 0 ? 0u : uniform_u32(__shfl(sc.g_end, pb - 1));
         const uint32_t tiles_per_group = 4 / K;
-        const uint32_t tile = (g - g0) * tiles_per_group + hw / K;
-        const uint32_t seg = hw % K;
+        const uint32_t tile = (g - g0) * tiles_per_group + thw / K;
+        const uint32_t seg = thw % K;
         const uint32_t slot = tile * 64 + lane;
         const bool live = slot < cnt;
         const uint32_t i = live ? (tp.counts ? tp.lists[(uint64_t)cls * tp.cap + slot] : slot) : 0u;
@@ -610,7 +640,7 @@ __global__ __launch_bounds__(512) void tile_kernel(SealArgs sa, OpenArgs oa, Til
         // so every slot's flags advance by exactly one per generation.
         uint32_t *const mine = comb + wave * kSlotRows * 64;
         bool bad = false;
-        if (hw > 0) {
+        if (hw > 0 && !dyn) {
             while (f_ack[wave] != gen - 1) __builtin_amdgcn_s_sleep(1);
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
             if (K > 1 && seg > 0) {
