@@ -198,7 +198,7 @@ int rg_set_debug_mode(rg_ctx *ctx, int mode);
  * mode 3 on the flattened kernel (s_memtime at the end of each phase) plus a
  * second block of rows after the first CUs x 4 (wall-clock start and end), so
  * size the buffer for 2 x CUs x 4 x 8 u64 there.  Modes 7 and 8 (pipelined seal):
- * no payload stores / all block stores to block 0. */
+ * no payload stores / line stores alternating between two lines per frame. */
 int rg_set_debug_buffer(rg_ctx *ctx, void *dev_ptr);
 
 /* ----------------------------------------- host-memory batch (blocking) */

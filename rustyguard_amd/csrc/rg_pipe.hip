@@ -208,7 +208,8 @@ __device__ __forceinline__ void ring_store(const Ring &R, const Ring4 &x, uint32
 // MODE (seal diagnostics, rg_set_debug_mode): 0 normal; 1 compute only (no
 // payload loads or stores, loop-carried fake data); 2 memory only (no
 // keystream and no Poly1305); 4/5/6 non-temporal loads / stores / both; 7 no payload stores;
-// 8 block stores all to block 0 of the frames (cache-resident: store issue without HBM writes).
+// 8 line stores alternate between lines 0 and 1 of each frame (cache-resident: the store instructions
+// without their HBM writes).
 // LINES: the frame blocks go through the wave's LDS ring (block t goes into
 // the ring; with FLUSH, half t & 1 of line (t - 2) / 2 is read back before the
 // rounds and stored after them).
@@ -259,7 +260,7 @@ __device__ __forceinline__ void pipe_step(uint4 *pl, const Stream &st, const Mul
     }
     if constexpr (LINES && !TAIL) {
         ring_put(R, t, prev, x.q0, x.q1, x.q2); // prev: the header before the first chunk
-        if constexpr (FLUSH) ring_store(R, fl, MODE == 8 ? 0u : (t - 2) >> 1, t & 1u);
+        if constexpr (FLUSH) ring_store(R, fl, MODE == 8 ? ((t - 2) >> 1) & 1u : (t - 2) >> 1, t & 1u);
         prev = x.q3;
         have_prev = true;
     } else if constexpr (TAIL) {
@@ -335,7 +336,7 @@ __device__ __forceinline__ Acc pipe_pass(uint4 *pl, const Stream &st, const Mul 
             // last line of one block stores its first four pieces only
             wave_sync();
             for (uint32_t m = F >= 2 ? F - 2 : 0; m < 2 * ((F + 1) >> 1); ++m)
-                ring_store<true>(R, ring_get(R, m >> 1, m & 1u), MODE == 8 ? 0u : m >> 1, m & 1u, F);
+                ring_store<true>(R, ring_get(R, m >> 1, m & 1u), MODE == 8 ? (m >> 1) & 1u : m >> 1, m & 1u, F);
         } else if constexpr (kDepth == 4) {
             for (; t + 3 < F; t += 4) {
                 pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R);
