@@ -292,6 +292,43 @@ __device__ __forceinline__ Acc flat_pow_mul(Acc h, const Mul &r, uint32_t e) {
     return y;
 }
 
+// ------------------------------------------------ quad key blocks
+// One ChaCha20 block on a lane quad: lane j holds column j (rows a, b, c, d = state words j, 4 + j,
+// 8 + j, 12 + j); the diagonal rounds rotate rows b, c, d across the quad with DPP quad_perm.  Only
+// the one-time key is wanted: r_j = keystream word j, s_j = word 4 + j (RFC 8439 §2.6).
+#ifndef RG_FLAT_QUAD
+#define RG_FLAT_QUAD 1
+#endif
+template <int CTRL> __device__ __forceinline__ uint32_t quad_perm(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL> __device__ __forceinline__ uint32_t quad_bcast(uint32_t v) { return quad_perm<CTRL>(v); }
+__device__ __forceinline__ void quad_qr(uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d) {
+    a += b; d ^= a; d = rotl(d, 16);
+    c += d; b ^= c; b = rotl(b, 12);
+    a += b; d ^= a; d = rotl(d, 8);
+    c += d; b ^= c; b = rotl(b, 7);
+}
+// kw: the packet's key-record row (key[8], counter lo, hi); block 0, nonce 0 || le64(counter)
+__device__ __forceinline__ void quad_otk(const uint32_t *kw, uint32_t j, uint32_t &r_j, uint32_t &s_j) {
+    const uint32_t a0 = j == 0 ? 0x61707865u : j == 1 ? 0x3320646eu : j == 2 ? 0x79622d32u : 0x6b206574u;
+    const uint32_t b0 = kw[j];
+    uint32_t a = a0, b = b0, c = kw[4 + j], d = j < 2 ? 0u : kw[6 + j]; // words 12, 13 = 0; 14, 15 = counter
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        quad_qr(a, b, c, d); // columns
+        b = quad_perm<0x39>(b); // lane j <- j + 1
+        c = quad_perm<0x4E>(c); // lane j <- j + 2
+        d = quad_perm<0x93>(d); // lane j <- j + 3
+        quad_qr(a, b, c, d); // diagonals
+        b = quad_perm<0x93>(b);
+        c = quad_perm<0x4E>(c);
+        d = quad_perm<0x39>(d);
+    }
+    r_j = a + a0;
+    s_j = b + b0;
+}
+
 struct FlatArgs {
     SealArgs sa;
     OpenArgs oa;
@@ -605,6 +642,9 @@ template <bool OPEN> __global__ __launch_bounds__(64 * kFlatWaves) void flat_ker
             if (s.fj + 1 < s.nsteps) { ++s.fj; fcur_next(s.f, L, buf, m); }
             fload(b2, s.f.pl, s.f.t, s.f.nb ? s.f.nb - 1 : 0);
             // ---- phase A: checks, one-time-key blocks, header (seal), counters_out (open)
+            // Packets 64.. of a sub-unit of 65-96 get their key blocks from lane quads (16 blocks per
+            // pass at ~0.36 of a full pass) instead of a second one-lane-per-packet pass.
+            const bool quad = RG_FLAT_QUAD && m > 64 && m <= 96; // wave-uniform
 #pragma unroll
             for (uint32_t q = 0; q < kFlatMaxPk / 64; ++q) {
                 const uint32_t k = lane + 64 * q;
@@ -628,13 +668,19 @@ template <bool OPEN> __global__ __launch_bounds__(64 * kFlatWaves) void flat_ker
                     }
                     if (A.oa.counters_out) A.oa.counters_out[i] = ((uint64_t)n2 << 32) | n1;
                 }
+                uint4 *kr = reinterpret_cast<uint4 *>(L.kr[k]);
+                kr[0] = ka[q];
+                kr[1] = kb[q];
+                if (q == 1 && quad) {
+                    // overflow packet: its one-time-key block is computed by a lane quad below
+                    L.kr[k][8] = n1;
+                    L.kr[k][9] = n2;
+                    if constexpr (OPEN) *reinterpret_cast<uint4 *>(L.sw[k]) = tg[q]; // the tag; s is subtracted there
+                } else {
                 const Key8 key = {{ka[q].x, ka[q].y, ka[q].z, ka[q].w, kb[q].x, kb[q].y, kb[q].z, kb[q].w}};
                 const Stream stm = make_stream(key, 0u, n1, n2); // nonce 0 || le64(counter), prim.rs:32-36
                 uint32_t ks[16];
                 stream_block(stm, 0, ks); // RFC 8439 §2.6 one-time key
-                uint4 *kr = reinterpret_cast<uint4 *>(L.kr[k]);
-                kr[0] = ka[q];
-                kr[1] = kb[q];
                 kr[2] = make_uint4(n1, n2, ks[0], ks[1]);
                 L.kr[k][12] = ks[2];
                 L.kr[k][13] = ks[3];
@@ -647,6 +693,7 @@ template <bool OPEN> __global__ __launch_bounds__(64 * kFlatWaves) void flat_ker
                     *reinterpret_cast<uint4 *>(L.sw[k]) = make_uint4(w0, w1, w2, w3);
                 } else {
                     *reinterpret_cast<uint4 *>(L.sw[k]) = make_uint4(ks[4], ks[5], ks[6], ks[7]);
+                }
                 }
                 {
                     unsigned long long *z = L.ps[k];
@@ -664,6 +711,32 @@ template <bool OPEN> __global__ __launch_bounds__(64 * kFlatWaves) void flat_ker
                 }
             }
             wave_sync();
+            if (quad) { // the overflow packets' one-time keys: 16 per wave instruction stream (lane quads)
+                for (uint32_t p0 = 64; p0 < m; p0 += 16) {
+                    const uint32_t k = p0 + (lane >> 2), j = lane & 3u;
+                    const uint32_t kk = k < m ? k : p0;
+                    uint32_t r_j, s_j;
+                    quad_otk(L.kr[kk], j, r_j, s_j);
+                    if constexpr (OPEN) {
+                        // tag - s (mod 2^128) needs all four words of s in every lane of the quad
+                        const uint32_t s0 = quad_bcast<0x00>(s_j), s1 = quad_bcast<0x55>(s_j);
+                        const uint32_t s2 = quad_bcast<0xAA>(s_j), s3 = quad_bcast<0xFF>(s_j);
+                        const uint4 t = *reinterpret_cast<const uint4 *>(L.sw[kk]);
+                        uint32_t c0, w[4];
+                        w[0] = __builtin_subc(t.x, s0, 0u, &c0);
+                        w[1] = __builtin_subc(t.y, s1, c0, &c0);
+                        w[2] = __builtin_subc(t.z, s2, c0, &c0);
+                        w[3] = __builtin_subc(t.w, s3, c0, &c0);
+                        s_j = j == 0 ? w[0] : j == 1 ? w[1] : j == 2 ? w[2] : w[3];
+                    }
+                    wave_sync(); // every quad has read its row before any lane writes one
+                    if (k < m) {
+                        L.kr[k][10 + j] = r_j;
+                        L.sw[k][j] = s_j;
+                    }
+                }
+                wave_sync();
+            }
             RG_FLAT_MARK(3);
             // ---- phase C: the chunk stream
             const uint32_t S = (D + 63) / 64;
