@@ -313,6 +313,45 @@ def test_schedule_targets_vs_oracle(engine, mix):
         _reset(engine)
 
 
+@pytest.mark.parametrize("rounds", [1.02, 2.5])
+@pytest.mark.parametrize("plan", [0, 1])
+def test_tile_dynamic_deal_vs_oracle(engine, rounds, plan):
+    """The tile kernel's dynamic deal (unsegmented classes, rg_tile.hip): a workgroup's tiles taken by
+    whichever of its eight waves is free, over several deal rounds with a partial last one, one forged
+    frame per round; seal and open bit-exact against the oracle."""
+    engine.set_staged(2)
+    engine.set_plan(plan)
+    engine.set_segments(1)
+    rng = np.random.default_rng(53)
+    waves = 8 * torch.cuda.get_device_properties(0).multi_processor_count
+    n = int(rounds * waves * 64) + 13
+    sizes = rng.integers(0, 9, n) * 16  # P in [0, 128]: many tiles, a quick oracle
+    keys, rec, desc, ctr, buf = _random_batch(rng, n, nkeys=4, sizes=sizes)
+    want = buf.copy()
+    oracle.seal_batch(keys, rec, desc, ctr, want, nthreads=8)
+    got, st = _gpu_seal(engine, keys, rec, desc, ctr, buf)
+    assert (st == aead.PKT_OK).all()
+    assert np.array_equal(got, want)
+    od = desc.copy()
+    od["len"] += 32
+    forged = rng.choice(n, size=5, replace=False)
+    tampered = got.copy()
+    for j in forged:  # last tag byte
+        tampered[int(od[j]["offset"]) + int(od[j]["len"]) - 1] ^= 0x01
+    back, st, co = _gpu_open(engine, keys, od, tampered)
+    ok = np.ones(n, bool)
+    ok[forged] = False
+    assert (st[ok] == aead.PKT_OK).all() and (st[forged] == aead.PKT_DECRYPT_ERR).all()
+    assert np.array_equal(co, ctr)
+    for j in forged:
+        o, w = int(od[j]["offset"]), int(od[j]["len"])
+        assert np.array_equal(back[o:o + w], tampered[o:o + w])
+    for i in np.nonzero(ok)[0][::97]:
+        o, p = int(desc[i]["offset"]), int(desc[i]["len"])
+        assert np.array_equal(back[o + 16: o + 16 + p], buf[o + 16: o + 16 + p])
+    _reset(engine)
+
+
 @pytest.mark.parametrize("mode", MODES, ids=_mode_id)
 def test_large_payload_mix_vs_oracle(engine, mode):
     """Every size class of the planner (up to the 1 MiB payload limit), shuffled with small packets,
