@@ -81,6 +81,14 @@ struct HostBuf {
 struct PlanBuf {
     DevBuf counts, lists;
     DevBuf sched; // pipelined kernel's tile queue and per-class schedule (rg_pipe.hip), zero between launches
+    DevBuf gq;    // tile kernel's global work pool (rg_tile.hip), zero between launches
+    // allocated with the context: a launch may come inside a stream capture, where allocation is not permitted
+    hipError_t ensure_gq() {
+        if (gq.p) return hipSuccess;
+        hipError_t e = gq.reserve(256);
+        if (e == hipSuccess) e = hipMemset(gq.p, 0, 256);
+        return e;
+    }
     uint32_t cap = 0;
     // auto planning: the tile kernel reports the number of size classes of the
     // last planned batch into host-mapped memory (read without synchronising;
@@ -120,6 +128,7 @@ struct PlanBuf {
         counts.release();
         lists.release();
         sched.release();
+        gq.release();
         cap = 0;
         if (h_classes) (void)hipHostFree(const_cast<uint32_t *>(h_classes));
         h_classes = nullptr;
@@ -204,6 +213,9 @@ int rg_create(int device, rg_ctx **out) {
         // the flattened kernel's store sink, allocated now: the automatic choice may first pick that
         // kernel inside a stream capture (HIP graph), where allocation is not permitted
         if (e == hipSuccess) e = c->d_junk.reserve(rg::flat_junk_bytes(c->cus));
+        if (e == hipSuccess) e = c->plan_dev.ensure_gq();
+        for (auto &sl : c->slots)
+            if (e == hipSuccess) e = sl.plan.ensure_gq();
         if (e != hipSuccess) {
             delete c;
             return set_err(RG_EDEVICE, "kernel setup", e);
@@ -351,6 +363,7 @@ static hipError_t launch_tiles_any(rg_ctx *ctx, const rg::SealArgs *sa, const rg
     rg::TilePlan tp{};
     tp.target_lanes = (uint32_t)std::max(1, ctx->cus) * 256u; // one wave per SIMD
     tp.fixed_k = (uint32_t)ctx->segments;
+    tp.gq = static_cast<uint32_t *>(pb.gq.p);
     bool plan = ctx->plan == 1;
     if (ctx->plan == 2) {
         hipError_t e = pb.reserve(n);

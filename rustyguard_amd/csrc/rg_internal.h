@@ -98,6 +98,8 @@ struct TilePlan {
     uint32_t *classes_out; // host-mapped: number of non-empty classes of the batch (or nullptr)
     uint32_t *sched;       // pipelined kernel: the planner also writes its schedule here (else nullptr)
     uint32_t simds;        // SIMDs the pipelined kernel runs on (schedule balance)
+    uint32_t *gq;          // tile kernel: global pool of the last deal rounds ([0] next item, [32] workgroups
+                           // done), zero between launches (the last workgroup clears it); may be nullptr
 };
 
 // Planner + LDS-staged tile kernel (rg_tile.hip); exactly one of sa / oa is non-null.

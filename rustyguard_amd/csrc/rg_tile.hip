@@ -205,6 +205,9 @@ constexpr uint32_t kMinSegment = 4;
 #ifndef RG_TILE_DYN
 #define RG_TILE_DYN 1
 #endif
+#ifndef RG_TILE_POOL
+#define RG_TILE_POOL 1
+#endif
 
 __device__ __forceinline__ uint32_t pow2ceil(uint32_t x) { return x <= 1 ? 1u : 1u << (32 - __clz(x - 1)); }
 
@@ -314,18 +317,38 @@ __global__ __launch_bounds__(512) void tile_kernel(SealArgs sa, OpenArgs oa, Til
     const uint32_t my_slot = half == 0 ? blockIdx.x : S - 1 - blockIdx.x;
     const uint32_t rounds = (sc.total_groups + S - 1) / S;
     const bool dyn = RG_TILE_DYN && halves == 2 && __ballot(sc.K > 1) == 0; // same in every wave
-    uint32_t next_v = 0; // the next item, requested one item ahead (LDS atomic, lane 0)
+    // From 16 deal rounds on, the last eighth of them goes to a pool shared by the whole grid: the XCDs
+    // do not run at one rate (per-CU finish times at config 4 spread by 8 %, by XCD), so the workgroups
+    // that run out of their own tiles first take these, one tile per device-scope atomic on tp.gq[0]
+    // -- taken only between tiles, when the wave has nothing in flight.  Measured: config 5 on one GPU
+    // (64 rounds) +1.5 %; with 8 rounds (config 4) the pool's exposed atomics cost more than it evens out.
+    const uint32_t R = (RG_TILE_POOL && dyn && tp.gq && rounds >= 16) ? rounds / 8 : 0u;
+    const uint32_t rounds_local = rounds - R;
+    const uint32_t pool = R ? (sc.total_groups - rounds_local * S) * 4u : 0u; // tiles in the global pool
+    bool pooled = false;
+    uint32_t next_v = 0; // the next local item, requested one item ahead (LDS atomic, lane 0)
     if (dyn && lane == 0) next_v = atomicAdd(f_next, 1u);
     uint32_t gen = 0, round_s = 0;
     for (;;) {
         uint32_t g, thw; // group, and this wave's tile (segment) slot in it
-        if (dyn) {
+        if (dyn && !pooled) {
             const uint32_t item = uniform_u32(__shfl((int)next_v, 0));
             const uint32_t r = item >> 3;
-            if (r >= rounds) break;
+            if (r >= rounds_local) {
+                if (pool == 0) break;
+                pooled = true;
+                continue;
+            }
             if (lane == 0) next_v = atomicAdd(f_next, 1u);
             const uint32_t sl = ((item >> 2) & 1u) == 0 ? blockIdx.x : S - 1 - blockIdx.x;
             g = r * S + ((r & 1) ? S - 1 - sl : sl);
+            thw = item & 3u;
+        } else if (dyn) {
+            uint32_t v = 0;
+            if (lane == 0) v = __hip_atomic_fetch_add(tp.gq, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t item = uniform_u32(__shfl((int)v, 0));
+            if (item >= pool) break;
+            g = rounds_local * S + (item >> 2);
             thw = item & 3u;
         } else {
             if (round_s >= rounds) break;
@@ -749,6 +772,19 @@ __global__ __launch_bounds__(512) void tile_kernel(SealArgs sa, OpenArgs oa, Til
             o[5] = t_tail;
             o[6] = 1;
             o[7] = realtime() - rt0;
+        }
+    }
+    if (R) {
+        // the last workgroup to finish clears the pool for the next launch (every wave of every
+        // workgroup has taken its last item before its workgroup counts itself done)
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __atomic_thread_fence(__ATOMIC_SEQ_CST);
+            if (__hip_atomic_fetch_add(tp.gq + 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
+                __hip_atomic_store(tp.gq, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(tp.gq + 32, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __atomic_thread_fence(__ATOMIC_SEQ_CST);
+            }
         }
     }
     if (tp.counts) {
