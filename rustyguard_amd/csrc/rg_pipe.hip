@@ -109,8 +109,8 @@ constexpr bool PIPE_OPEN_CUR = RG_PIPE_OPEN_CUR != 0;
 #define RG_PIPE_LOAD_FIRST 0
 #endif
 constexpr bool PIPE_LOAD_FIRST = RG_PIPE_LOAD_FIRST != 0;
-// experiment: ring stores written through to memory (1), so that fewer dirty lines are left in L2
-// for the end-of-kernel write-back
+// experiment: ring stores written through to memory (1) or non-temporal (2), so that fewer dirty
+// lines are left in L2 for the end-of-kernel write-back
 #ifndef RG_PIPE_WT
 #define RG_PIPE_WT 0
 #endif
@@ -185,10 +185,12 @@ __device__ __forceinline__ void ring_store(const Ring &R, const Ring4 &x, uint32
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         glb_u4 *dst = (h ? R.fr[1][q] : R.fr[0][q]) + 8 * k;
-        if constexpr (PIPE_WT != 0) // device-scope write-through (sc1): the line leaves L2 clean
-            // (the s_nop: a VALU write to the data registers of a store wider than 64 bits needs a wait
-            // state, which the hazard pass does not insert behind inline asm)
+        // (the s_nop: a VALU write to the data registers of a store wider than 64 bits needs a wait
+        // state, which the hazard pass does not insert behind inline asm)
+        if constexpr (PIPE_WT == 1) // device-scope write-through (sc1): the line leaves L2 clean
             asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(dst), "v"(x.v[q]) : "memory");
+        else if constexpr (PIPE_WT == 2) // non-temporal (streaming) whole-line stores
+            asm volatile("global_store_dwordx4 %0, %1, off nt\n\ts_nop 1" ::"v"(dst), "v"(x.v[q]) : "memory");
         else *dst = x.v[q];
     }
 }
