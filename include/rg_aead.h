@@ -101,7 +101,9 @@ const char *rg_last_error(void);
  * (hipStream_t, NULL = legacy default stream) and the call returns without
  * synchronising.  status/counters_out may be NULL for seal.  The kernels
  * bounds-check every descriptor against buf_len and never touch memory
- * outside [buf, buf + buf_len). */
+ * outside [buf, buf + buf_len).  Calls on one context are ordered on one stream
+ * (they share the planner buffers and the tile kernel's work pool, see
+ * rg_set_plan); use a context per concurrent stream. */
 int rg_seal_batch_dev(rg_ctx *ctx, const uint8_t *keys, const uint32_t *receivers, uint32_t nkeys,
                       const rg_pkt_desc *desc, const uint64_t *counters, size_t n, uint8_t *buf, size_t buf_len,
                       uint8_t *status, void *stream);
@@ -177,9 +179,10 @@ int rg_last_kernel(rg_ctx *ctx);
  * 0 = off (tiles take packets in array order), 1 = always, 2 (default) =
  * auto: plan unless the last planned batch of this context held a single size
  * class (re-checked every 32nd call).  Results are identical in every mode.
- * Device-API calls that share a context use one set of planner buffers: issue
- * them on one stream (or order them) -- the host-memory API has its own per
- * pipeline stream. */
+ * Device-API calls that share a context use one set of planner buffers and one
+ * tile-kernel work pool (batches of 16 or more deal rounds, ~2 Mi packets on 256
+ * CUs, even with the planner off): issue them on one stream (or order them) --
+ * the host-memory API has its own per pipeline stream. */
 int rg_set_plan(rg_ctx *ctx, int on);
 /* Segments per packet for the tile kernels: 0 (default) = per size class,
  * aiming at two resident waves per SIMD; 1/2/4 = split every packet into that
