@@ -603,10 +603,17 @@ __device__ __forceinline__ void pipe_open_packet(const OpenArgs &a, uint32_t i, 
         // (callers never read the buffer on Err, but the frame is left as it came); with block stores
         // other lanes wrote this frame: their stores complete and this lane's cached lines go first
         if (lines) __threadfence();
+        // the chunk's four loads (clamped inside the segment) are issued before its keystream block, so the
+        // block's rounds cover their latency
         for (uint32_t c = 0; 4 * c < sg.nb; ++c) {
+            Chunk m;
+            load_chunk(m, pl, c, sg.nb - 1);
             stream_block(stm, sg.c0 + c + 1, ks);
             const uint32_t cnt = chunk_blocks(sg.nb, c);
-            for (uint32_t q = 0; q < cnt; ++q) pl[4 * c + q] = xor4(pl[4 * c + q], ks + 4 * q);
+            if (cnt > 0) pl[4 * c + 0] = xor4(m.q0, ks + 0);
+            if (cnt > 1) pl[4 * c + 1] = xor4(m.q1, ks + 4);
+            if (cnt > 2) pl[4 * c + 2] = xor4(m.q2, ks + 8);
+            if (cnt > 3) pl[4 * c + 3] = xor4(m.q3, ks + 12);
         }
     }
     if (j == 0) {

@@ -749,11 +749,17 @@ __global__ __launch_bounds__(512) void tile_kernel(SealArgs sa, OpenArgs oa, Til
                 }
             }
             if (bad) {
+                // each chunk's loads (clamped inside the payload) go out before its keystream block
                 uint4 *pl = reinterpret_cast<uint4 *>(frame + 16);
                 for (uint32_t c = c0; c < c1; ++c) {
-                    const uint32_t hi = 4 * c + 4 < nb ? 4 * c + 4 : nb;
+                    const uint32_t b0 = 4 * c, last = nb - 1;
+                    const uint4 m0 = pl[min(b0, last)], m1 = pl[min(b0 + 1, last)];
+                    const uint4 m2 = pl[min(b0 + 2, last)], m3 = pl[min(b0 + 3, last)];
                     stream_block(stm, c + 1, ks);
-                    for (uint32_t q = 4 * c; q < hi; ++q) pl[q] = xor4(pl[q], ks + 4 * (q - 4 * c));
+                    if (b0 < nb) pl[b0] = xor4(m0, ks + 0);
+                    if (b0 + 1 < nb) pl[b0 + 1] = xor4(m1, ks + 4);
+                    if (b0 + 2 < nb) pl[b0 + 2] = xor4(m2, ks + 8);
+                    if (b0 + 3 < nb) pl[b0 + 3] = xor4(m3, ks + 12);
                 }
             }
         }
