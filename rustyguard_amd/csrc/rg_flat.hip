@@ -871,13 +871,17 @@ template <bool OPEN> __global__ __launch_bounds__(64 * kFlatWaves) void flat_ker
                         Stream stm = make_stream(q.key, 0u, q.n1, q.n2);
                         for (uint32_t j = 0; j < s.nsteps; ++j) {
                             if (L.hs[p.k][6] == kFail) {
-                                uint32_t ks[16];
-                                stream_block(stm, p.t + 1, ks);
+                                // the chunk's loads (clamped inside the payload) before its keystream block
                                 uint4 *w = const_cast<uint4 *>(p.pl) + 4 * p.t;
                                 const uint32_t c = min(4u, p.nb - 4 * p.t);
+                                uint4 m[4];
+#pragma unroll
+                                for (uint32_t b = 0; b < 4; ++b) m[b] = w[b < c ? b : c - 1];
+                                uint32_t ks[16];
+                                stream_block(stm, p.t + 1, ks);
 #pragma unroll
                                 for (uint32_t b = 0; b < 4; ++b)
-                                    if (b < c) w[b] = xor4(w[b], ks + 4 * b);
+                                    if (b < c) w[b] = xor4(m[b], ks + 4 * b);
                             }
                             if (fcur_next(p, L, buf, m) && p.k < m) {
                                 q = fkey(L, p.k);
