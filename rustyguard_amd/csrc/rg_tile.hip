@@ -208,6 +208,12 @@ constexpr uint32_t kMinSegment = 4;
 #ifndef RG_TILE_POOL
 #define RG_TILE_POOL 1
 #endif
+#ifndef RG_TILE_POOL_MIN
+#define RG_TILE_POOL_MIN 2 // deal rounds from which the grid-wide pool is used
+#endif
+#ifndef RG_TILE_POOL_AHEAD
+#define RG_TILE_POOL_AHEAD 1 // pool items requested one tile ahead
+#endif
 
 __device__ __forceinline__ uint32_t pow2ceil(uint32_t x) { return x <= 1 ? 1u : 1u << (32 - __clz(x - 1)); }
 
@@ -317,15 +323,16 @@ __global__ __launch_bounds__(512) void tile_kernel(SealArgs sa, OpenArgs oa, Til
     const uint32_t my_slot = half == 0 ? blockIdx.x : S - 1 - blockIdx.x;
     const uint32_t rounds = (sc.total_groups + S - 1) / S;
     const bool dyn = RG_TILE_DYN && halves == 2 && __ballot(sc.K > 1) == 0; // same in every wave
-    // From 16 deal rounds on, the last eighth of them goes to a pool shared by the whole grid: the XCDs
-    // do not run at one rate (per-CU finish times at config 4 spread by 8 %, by XCD), so the workgroups
-    // that run out of their own tiles first take these, one tile per device-scope atomic on tp.gq[0]
-    // -- taken only between tiles, when the wave has nothing in flight.  Measured: config 5 on one GPU
-    // (64 rounds) +1.5 %; with 8 rounds (config 4) the pool's exposed atomics cost more than it evens out.
-    const uint32_t R = (RG_TILE_POOL && dyn && tp.gq && rounds >= 16) ? rounds / 8 : 0u;
+    // From two deal rounds on, the last eighth of them (at least one) goes to a pool shared by the whole
+    // grid: the XCDs do not run at one rate (per-CU finish times at config 4 spread by 8 %, by XCD), so
+    // the workgroups that run out of their own tiles first take these, one tile per device-scope atomic
+    // on tp.gq[0], requested one tile ahead.  Measured: config 5 on one GPU (64 rounds) +1.5 %, config 4
+    // (8 rounds) +0.7 % (with each draw waited for on the spot, config 4 lost 1 %).
+    const uint32_t R = (RG_TILE_POOL && dyn && tp.gq && rounds >= RG_TILE_POOL_MIN) ? max(1u, rounds / 8) : 0u;
     const uint32_t rounds_local = rounds - R;
     const uint32_t pool = R ? (sc.total_groups - rounds_local * S) * 4u : 0u; // tiles in the global pool
-    bool pooled = false;
+    bool pooled = false, gq_pending = false;
+    uint32_t gq_next = 0; // lane 0: the next pool item
     uint32_t next_v = 0; // the next local item, requested one item ahead (LDS atomic, lane 0)
     if (dyn && lane == 0) next_v = atomicAdd(f_next, 1u);
     uint32_t gen = 0, round_s = 0;
@@ -344,10 +351,17 @@ __global__ __launch_bounds__(512) void tile_kernel(SealArgs sa, OpenArgs oa, Til
             g = r * S + ((r & 1) ? S - 1 - sl : sl);
             thw = item & 3u;
         } else if (dyn) {
-            uint32_t v = 0;
-            if (lane == 0) v = __hip_atomic_fetch_add(tp.gq, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const uint32_t item = uniform_u32(__shfl((int)v, 0));
+            // the first draw waits for its atomic; later ones were requested one tile ahead (an atomic
+            // still in flight only makes the tile's exact vmcnt waits wait for it too, never less)
+            if (!gq_pending && lane == 0)
+                gq_next = __hip_atomic_fetch_add(tp.gq, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t item = uniform_u32(__shfl((int)gq_next, 0));
+            gq_pending = false;
             if (item >= pool) break;
+            if (RG_TILE_POOL_AHEAD && lane == 0) {
+                gq_next = __hip_atomic_fetch_add(tp.gq, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            gq_pending = RG_TILE_POOL_AHEAD != 0;
             g = rounds_local * S + (item >> 2);
             thw = item & 3u;
         } else {
