@@ -180,8 +180,8 @@ int rg_last_kernel(rg_ctx *ctx);
  * auto: plan unless the last planned batch of this context held a single size
  * class (re-checked every 32nd call).  Results are identical in every mode.
  * Device-API calls that share a context use one set of planner buffers and one
- * tile-kernel work pool (batches of 16 or more deal rounds, ~2 Mi packets on 256
- * CUs, even with the planner off): issue them on one stream (or order them) --
+ * tile-kernel work pool (batches of two or more deal rounds, ~260 Ki packets on
+ * 256 CUs, even with the planner off): issue them on one stream (or order them) --
  * the host-memory API has its own per pipeline stream. */
 int rg_set_plan(rg_ctx *ctx, int on);
 /* Segments per packet for the tile kernels: 0 (default) = per size class,

@@ -317,7 +317,7 @@ def test_schedule_targets_vs_oracle(engine, mix):
 @pytest.mark.parametrize("plan", [0, 1])
 def test_tile_dynamic_deal_vs_oracle(engine, rounds, plan):
     """The tile kernel's dynamic deal (unsegmented classes, rg_tile.hip): a workgroup's tiles taken by
-    whichever of its eight waves is free, over several deal rounds with a partial last one (from 16 rounds
+    whichever of its eight waves is free, over several deal rounds with a partial last one (from two rounds
     the last eighth from the grid-wide pool), five forged frames; seal and open bit-exact against the
     oracle."""
     engine.set_staged(2)
