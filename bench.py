@@ -287,10 +287,13 @@ def forged_open_timing(w, b, stream, frac: float, verify: bool):
     idx = torch.from_numpy(pos.astype(np.int64)).to(b.buf.device)
     reps = 5
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(reps)]
-    for e in evs:
+    before = None
+    for r, e in enumerate(evs):
         b.seal(stream=stream)
         with torch.cuda.stream(stream):
             b.buf[idx] ^= 1
+            if verify and r == reps - 1:
+                before = b.buf.clone()  # the submitted (tampered) frames of the last rep
         e[0].record(stream)
         b.open(stream=stream, counters_out=False)
         e[1].record(stream)
@@ -300,6 +303,17 @@ def forged_open_timing(w, b, stream, frac: float, verify: bool):
         bad = np.zeros(w.n, bool)
         bad[pick] = True
         assert (st[bad] == 1).all() and (st[~bad] == 0).all(), "forged-batch statuses"
+        # a rejected frame is left exactly as it came (prim.rs:190-201): every byte of every forged frame
+        off = torch.from_numpy(w.desc["offset"][pick].astype(np.int64)).to(b.buf.device)
+        wl = torch.from_numpy(w.desc["len"][pick].astype(np.int64) + 32).to(b.buf.device)
+        span = int(wl.max().item())
+        ar = torch.arange(span, device=b.buf.device)
+        for g in range(0, k, 32768):
+            pos = off[g:g + 32768, None] + ar[None, :]
+            m = ar[None, :] < wl[g:g + 32768, None]
+            pos = pos[m]
+            assert torch.equal(b.buf[pos], before[pos]), "a forged frame was not restored byte for byte"
+        del before
     b.fill(stream=stream)  # back to the synthetic plaintext the later checks start from
     torch.cuda.synchronize()
     open_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / reps

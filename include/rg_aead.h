@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define RG_ABI_VERSION 3
+#define RG_ABI_VERSION 4
 
 typedef struct rg_ctx rg_ctx;
 
@@ -336,6 +336,18 @@ int rg_recv_batch_dev(rg_sessions *s, const rg_pkt_desc *desc, size_t n, uint8_t
                       uint8_t *status, void *stream);
 int rg_recv_batch_dev_finish(rg_sessions *s, const uint64_t *src, uint8_t *status_out, uint32_t *slots_out,
                              uint8_t *flags_out);
+
+/* ------------------------------------------------------------ test hooks */
+/* Not for production use.  rg_debug_read_arena copies up to `bytes` of one of the context's
+ * key-bearing device buffers to host memory -- which = 0: the per-message drop-in's arena (its
+ * job record holds the key while a call runs and is zeroed before the call returns), 1: the
+ * batched host API's key table, 2: the MAC key states -- and returns the number of bytes copied
+ * (>= 0) or a negative rg_status.  Key-bearing buffers are zeroed before they are freed or
+ * regrown (rg_destroy, rg_sessions_destroy), as the reference zeroizes keys on drop
+ * (rustyguard-crypto/src/prim.rs:227-231).  rg_debug_fail_reserve(n) makes the n-th following
+ * device or pinned-host buffer allocation of any context fail (0 = off), for error-path tests. */
+int rg_debug_read_arena(rg_ctx *ctx, int which, void *dst, size_t bytes);
+void rg_debug_fail_reserve(int nth);
 
 /* ------------------------------------------------ synthetic workloads */
 /* Device fill of payload bytes: inner bytes [0, inner_len[i]) of packet i

@@ -73,6 +73,8 @@ SIGNATURES = {
     "rg_recv_batch_dev": (c_int, [c_vp, c_vp, c_size, c_vp, c_size, c_vp, c_vp]),
     "rg_recv_batch_dev_finish": (c_int, [c_vp, c_vp, c_u8p, c_vp, c_u8p]),
     "rg_synth_fill_dev": (c_int, [c_vp, c_vp, c_vp, c_size, c_u8p, c_size, c_u64, c_vp]),
+    "rg_debug_read_arena": (c_int, [c_vp, c_int, c_vp, c_size]),
+    "rg_debug_fail_reserve": (None, [c_int]),
 }
 
 

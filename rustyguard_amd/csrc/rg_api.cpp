@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -36,45 +37,59 @@ int set_err(int code, const char *what, hipError_t e = hipSuccess) {
         if (e_ != hipSuccess) return set_err(RG_EDEVICE, what, e_);          \
     } while (0)
 
-// grow-only device allocation
+// test hook (rg_debug_fail_reserve): the n-th following allocation of a DevBuf / HostBuf fails
+std::atomic<int> g_fail_reserve{0};
+bool injected_failure() {
+    int v = g_fail_reserve.load();
+    while (v > 0)
+        if (g_fail_reserve.compare_exchange_weak(v, v - 1)) return v == 1;
+    return false;
+}
+
+// grow-only device allocation.  `secret` buffers hold key material: they are zeroed before their
+// memory goes back to the allocator (the reference zeroizes keys on drop, prim.rs:227-231).
 struct DevBuf {
     void *p = nullptr;
     size_t cap = 0;
-    hipError_t reserve(size_t bytes) {
-        if (bytes <= cap) return hipSuccess;
+    bool secret = false;
+    void drop() {
+        if (p && secret) (void)hipMemset(p, 0, cap);
         if (p) (void)hipFree(p);
         p = nullptr;
         cap = 0;
+    }
+    hipError_t reserve(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        drop();
+        if (injected_failure()) return hipErrorOutOfMemory;
         size_t want = std::max<size_t>(bytes, 4096);
         hipError_t e = hipMalloc(&p, want);
         if (e == hipSuccess) cap = want;
         return e;
     }
-    void release() {
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        cap = 0;
-    }
+    void release() { drop(); }
 };
 
 struct HostBuf {
     void *p = nullptr;
     size_t cap = 0;
-    hipError_t reserve(size_t bytes) {
-        if (bytes <= cap) return hipSuccess;
+    bool secret = false;
+    void drop() {
+        if (p && secret) memset(p, 0, cap);
         if (p) (void)hipHostFree(p);
         p = nullptr;
         cap = 0;
+    }
+    hipError_t reserve(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        drop();
+        if (injected_failure()) return hipErrorOutOfMemory;
         size_t want = std::max<size_t>(bytes, 4096);
         hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
         if (e == hipSuccess) cap = want;
         return e;
     }
-    void release() {
-        if (p) (void)hipHostFree(p);
-        p = nullptr;
-        cap = 0;
-    }
+    void release() { drop(); }
 };
 
 // planner work lists (rg_tile.hip): class counts + [kClasses][cap] indices
@@ -205,6 +220,7 @@ int rg_create(int device, rg_ctx **out) {
     rg_ctx *c = new (std::nothrow) rg_ctx();
     if (!c) return set_err(RG_ENOMEM, "alloc ctx");
     c->device = device;
+    c->d_keys.secret = c->d_general.secret = c->d_mac_keys.secret = c->h_general.secret = true;
     {
         hipError_t e = hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device);
         if (e == hipSuccess) e = rg::prepare_tile_kernels();
@@ -810,6 +826,8 @@ static int general_one(rg_ctx *ctx, bool dec, const uint8_t key[32], const uint8
     RG_HIP(hipMemcpyAsync(d, h, arena, hipMemcpyHostToDevice, st), "H2D arena");
     RG_HIP(rg::launch_general(reinterpret_cast<rg::GeneralJob *>(d), 1, d + job_bytes, st), "general launch");
     RG_HIP(hipMemcpyAsync(h, d, arena, hipMemcpyDeviceToHost, st), "D2H arena");
+    // the key does not stay in device memory either (prim.rs:227-231 zeroizes on drop)
+    RG_HIP(hipMemsetAsync(d, 0, job_bytes, st), "wipe arena key");
     RG_HIP(hipStreamSynchronize(st), "general sync");
     memcpy(&job, h, sizeof job);
     memset(h, 0, sizeof job); // the key does not stay in the pinned image
@@ -838,6 +856,21 @@ int rg_xchacha20poly1305_dec(rg_ctx *ctx, const uint8_t key[32], const uint8_t n
                              size_t aad_len, uint8_t *payload, size_t len, const uint8_t tag[16]) {
     return general_one(ctx, true, key, nonce, aad, aad_len, payload, len, const_cast<uint8_t *>(tag), true);
 }
+
+// ------------------------------------------------------------ test hooks
+int rg_debug_read_arena(rg_ctx *ctx, int which, void *dst, size_t bytes) {
+    int rc = check_ctx(ctx);
+    if (rc) return rc;
+    if (!dst) return set_err(RG_EINVAL, "debug_read_arena: null dst");
+    const DevBuf *b = which == 0 ? &ctx->d_general : which == 1 ? &ctx->d_keys : which == 2 ? &ctx->d_mac_keys : nullptr;
+    if (!b) return set_err(RG_EINVAL, "debug_read_arena: which must be 0, 1 or 2");
+    std::lock_guard<std::mutex> g(ctx->mu);
+    const size_t m = std::min(bytes, b->cap);
+    if (m) RG_HIP(hipMemcpy(dst, b->p, m, hipMemcpyDeviceToHost), "debug_read_arena copy");
+    return (int)std::min<size_t>(m, 0x7FFFFFFF);
+}
+
+void rg_debug_fail_reserve(int nth) { g_fail_reserve.store(nth > 0 ? nth : 0); }
 
 // ------------------------------------------------------------- AntiReplay
 // rustyguard-utils/src/anti_replay.rs:1-64 with usize = u64:
@@ -1015,6 +1048,7 @@ int rg_sessions_create(rg_ctx *ctx, uint32_t capacity, rg_sessions **out) {
     if (!s) return set_err(RG_ENOMEM, "alloc sessions");
     s->ctx = ctx;
     s->cap = capacity;
+    s->dev.keys.secret = true;
     s->s.resize(capacity);
     s->keys.assign((size_t)capacity * 64, 0);
     s->receivers.assign((size_t)capacity * 2, 0);
@@ -1028,8 +1062,7 @@ void rg_sessions_destroy(rg_sessions *s) {
     SessDev &D = s->dev;
     (void)hipSetDevice(s->ctx->device);
     (void)drain_device_work(D);
-    if (D.keys.p) (void)hipMemset(D.keys.p, 0, D.keys.cap);
-    D.keys.release(); D.recv.release(); D.rx.release();
+    D.keys.release(); D.recv.release(); D.rx.release(); // keys: a secret buffer, zeroed before it is freed
     for (auto &g : D.send) {
         g.d_desc.release(); g.d_kidx.release(); g.d_ctr.release(); g.h_kidx.release(); g.h_ctr.release();
         if (g.ev) (void)hipEventDestroy(g.ev);
@@ -1297,33 +1330,39 @@ int rg_recv_batch_dev(rg_sessions *s, const rg_pkt_desc *desc, size_t n, uint8_t
     RG_HIP(ensure_event(R.ev_done), "recv event");
     RG_HIP(hipEventSynchronize(R.ev_done), "recv staging"); // the previous batch's fix-ups are done
     hipStream_t st = static_cast<hipStream_t>(stream);
-    R.pending = true;
+    // The batch becomes pending only once every buffer is reserved and every step is enqueued: a
+    // failure leaves no pending batch (finish then reports none), and work already enqueued is
+    // fenced by ev_done, which the next call waits for before it reuses the staging buffers.
+    if (n > 0) {
+        RG_HIP(R.d_rdesc.reserve(n * sizeof(rg_pkt_desc)), "alloc recv descriptors");
+        RG_HIP(R.d_ctr.reserve(n * 8), "alloc recv counters");
+        RG_HIP(R.d_key.reserve(n * 4), "alloc recv key rows");
+        RG_HIP(R.h_status.reserve(n), "alloc recv staging");
+        RG_HIP(R.h_ctr.reserve(n * 8), "alloc recv staging");
+        RG_HIP(R.h_key.reserve(n * 4), "alloc recv staging");
+        auto fenced = [&](int code) {
+            (void)hipEventRecord(R.ev_done, st);
+            return code;
+        };
+        auto *rd = static_cast<rg_pkt_desc *>(R.d_rdesc.p);
+        hipError_t e = rg::launch_rx_resolve(desc, (uint32_t)n, buf, buf_len, static_cast<const rg_rx_entry *>(D.rx.p),
+                                             D.rx_cap, rd, static_cast<uint32_t *>(R.d_key.p), st);
+        if (e != hipSuccess) return fenced(set_err(RG_EDEVICE, "rx resolve launch", e));
+        rc = rg_open_batch_dev(s->ctx, static_cast<const uint8_t *>(D.keys.p), 2 * s->cap, rd, n, buf, buf_len, status,
+                               static_cast<uint64_t *>(R.d_ctr.p), stream);
+        if (rc) return fenced(rc);
+        e = hipMemcpyAsync(R.h_status.p, status, n, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipMemcpyAsync(R.h_ctr.p, R.d_ctr.p, n * 8, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipMemcpyAsync(R.h_key.p, R.d_key.p, n * 4, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipEventRecord(R.ev_meta, st);
+        if (e != hipSuccess) return fenced(set_err(RG_EDEVICE, "recv metadata copies", e));
+    }
     R.n = n;
     R.st = st;
     R.buf = buf;
     R.buf_len = buf_len;
     R.status = status;
-    if (n == 0) return RG_OK;
-    RG_HIP(R.d_rdesc.reserve(n * sizeof(rg_pkt_desc)), "alloc recv descriptors");
-    RG_HIP(R.d_ctr.reserve(n * 8), "alloc recv counters");
-    RG_HIP(R.d_key.reserve(n * 4), "alloc recv key rows");
-    RG_HIP(R.h_status.reserve(n), "alloc recv staging");
-    RG_HIP(R.h_ctr.reserve(n * 8), "alloc recv staging");
-    RG_HIP(R.h_key.reserve(n * 4), "alloc recv staging");
-    auto *rd = static_cast<rg_pkt_desc *>(R.d_rdesc.p);
-    RG_HIP(rg::launch_rx_resolve(desc, (uint32_t)n, buf, buf_len, static_cast<const rg_rx_entry *>(D.rx.p), D.rx_cap,
-                                 rd, static_cast<uint32_t *>(R.d_key.p), st),
-           "rx resolve launch");
-    rc = rg_open_batch_dev(s->ctx, static_cast<const uint8_t *>(D.keys.p), 2 * s->cap, rd, n, buf, buf_len, status,
-                           static_cast<uint64_t *>(R.d_ctr.p), stream);
-    if (rc) {
-        R.pending = false;
-        return rc;
-    }
-    RG_HIP(hipMemcpyAsync(R.h_status.p, status, n, hipMemcpyDeviceToHost, st), "D2H recv status");
-    RG_HIP(hipMemcpyAsync(R.h_ctr.p, R.d_ctr.p, n * 8, hipMemcpyDeviceToHost, st), "D2H recv counters");
-    RG_HIP(hipMemcpyAsync(R.h_key.p, R.d_key.p, n * 4, hipMemcpyDeviceToHost, st), "D2H recv key rows");
-    RG_HIP(hipEventRecord(R.ev_meta, st), "recv event record");
+    R.pending = true;
     return RG_OK;
 }
 

@@ -54,7 +54,7 @@ def test_ctypes_binding_covers_header():
 
 
 def test_abi_version():
-    assert _lib.lib().rg_abi_version() == 3
+    assert _lib.lib().rg_abi_version() == 4
 
 
 def test_struct_layout_with_gcc(tmp_path):

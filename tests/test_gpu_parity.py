@@ -940,3 +940,27 @@ def test_flat_first_launch_inside_graph_capture():
     ref = b.host_buf()
     oracle.seal_batch(w.keys, w.receivers, w.desc, w.counters, ref)
     assert np.array_equal(got, ref)
+
+
+def test_per_message_key_wiped_from_device(engine):
+    """The per-message drop-in leaves no key in device memory (the reference zeroizes keys on drop,
+    rustyguard-crypto/src/prim.rs:227-231): after enc, dec, a failed dec and the XChaCha pair, the
+    device arena read back through the test hook holds none of the key bytes."""
+    import ctypes
+
+    from rustyguard_amd import _lib
+
+    key = bytes(range(0xA0, 0xC0))
+    msg = bytearray(b"\x5a" * 200)
+    tag = engine.chacha20poly1305_enc(key, aead.nonce(9), b"aad", msg)
+    engine.chacha20poly1305_dec(key, aead.nonce(9), b"aad", msg, tag)
+    with pytest.raises(aead.DecryptionError):
+        engine.chacha20poly1305_dec(key, aead.nonce(9), b"aad", msg, bytes(16))
+    xt = engine.xchacha20poly1305_enc(key, bytes(24), b"", msg)
+    engine.xchacha20poly1305_dec(key, bytes(24), b"", msg, xt)
+    out = (ctypes.c_uint8 * (1 << 16))()
+    got = _lib.check(_lib.lib().rg_debug_read_arena(engine.handle, 0, out, len(out)), "rg_debug_read_arena")
+    assert got > 0
+    arena = bytes(out[:got])
+    for w in range(0, 32, 8):  # no 8-byte run of the key anywhere
+        assert key[w:w + 8] not in arena

@@ -204,3 +204,44 @@ def test_recv_batch_dev_pending_rules(engine):
     ad.recv_batch_dev(dd2, db2, dst2)
     st, sl, fl = ad.recv_batch_dev_finish(2)
     assert list(st) == [0, 0] and list(sl) == [s2, s2]
+
+
+def test_recv_batch_dev_failed_setup_leaves_no_pending_batch(engine):
+    """An allocation that fails inside rg_recv_batch_dev (forced by rg_debug_fail_reserve: the k-th
+    allocation after the hook is armed) leaves no pending batch behind -- finish reports none, and
+    neither the window nor the frames moved: the next receive matches the host path on a twin table."""
+    L = _lib.lib()
+    failed = 0
+    try:
+        for k in range(1, 12):
+            ah, ad, b, sa, sc, sb = _twins(engine)
+            rng = np.random.default_rng(20 + k)
+            rdesc, ob = _recv_batch(b, sb, rng)
+            n = len(rdesc)
+            db, dd = _dev(ob), _dev(rdesc)
+            dst = torch.zeros(n, dtype=torch.uint8, device="cuda")
+            L.rg_debug_fail_reserve(k)
+            try:
+                ad.recv_batch_dev(dd, db, dst)
+                ok = True
+            except _lib.RgError:
+                ok = False
+            L.rg_debug_fail_reserve(0)
+            torch.cuda.synchronize()
+            if ok:
+                ad.recv_batch_dev_finish(n)
+                continue
+            failed += 1
+            with pytest.raises(_lib.RgError):
+                ad.recv_batch_dev_finish(n)  # no pending batch: no replay pass over stale staging
+            assert np.array_equal(db.cpu().numpy(), ob)  # nothing was opened
+            hb = ob.copy()
+            st_h, sl_h = ah.recv_batch(rdesc, hb)
+            ad.recv_batch_dev(dd, db, dst)
+            st_d, sl_d, _ = ad.recv_batch_dev_finish(n)
+            torch.cuda.synchronize()
+            assert list(st_d) == list(st_h) and list(sl_d) == list(sl_h)
+            assert np.array_equal(db.cpu().numpy(), hb)
+    finally:
+        L.rg_debug_fail_reserve(0)
+    assert failed >= 6  # the staging reserves (and the table mirrors) were all exercised
