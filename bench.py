@@ -429,6 +429,50 @@ def strict_check(w, b, stream):
         assert np.array_equal(fr[16:16 + len(exp[k])], exp[k]), f"open did not restore packet {k}"
 
 
+def run_legs(rank: int, world: int, workload: str, args) -> list:
+    """What a rank runs after the timed steps.  With N > 1 rank 0 also makes the line self-contained:
+    the same workload's whole batch on its one GPU (the strong-scaling base, `base_1gpu`) and the CPU
+    baselines; the other ranks wait at the final barrier."""
+    legs = ["timed"]
+    if rank == 0:
+        if world > 1 and workload == "cfg5":
+            legs.append("base_1gpu")
+        if args.cpu_seconds > 0:
+            legs.append("cpu_baseline")
+    return legs
+
+
+def base_one_gpu(eng, steps: int = 3):
+    """Config 5's whole 8 Mi-packet batch sealed and opened on this rank's GPU alone (graph-replayed
+    steps, as the timed region): the 1-GPU base of the strong-scaling split, measured in the same run."""
+    import torch
+
+    from rustyguard_amd import workloads
+    from rustyguard_amd.device import DeviceBatch
+
+    w = workloads.build("cfg5", 0, 1)
+    b = DeviceBatch(eng, w)
+    b.fill()
+    torch.cuda.synchronize()
+    s = torch.cuda.current_stream()
+    b.seal(stream=s)
+    b.open(stream=s, counters_out=False)  # warm-up (planner state, caches)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        b.seal(stream=s)
+        b.open(stream=s, counters_out=False)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    ok = bool((b.status[: w.n] == 0).all().item())
+    out = {"workload": f"cfg5 whole batch ({w.n} packets) on one GPU", "steps": steps,
+           "gib_s": round(2 * w.payload_bytes * steps / el / 2**30, 3), "ms_per_step": round(el / steps * 1e3, 4),
+           "statuses_ok": ok}
+    del b
+    torch.cuda.empty_cache()
+    return out
+
+
 def load_traffic(workload: str):
     p = os.path.join(REPO, "profiles", f"pmc_{workload}.json")
     if os.path.exists(p):
@@ -454,8 +498,11 @@ def main():
         return
     workload = args.workload or ("cfg2" if world == 1 else "cfg5")
     if args.dry_run:
-        line = json.dumps({"rank": int(os.environ.get("RANK", "0")), "world": world, "gpus": args.gpus,
-                           "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "workload": workload}) + "\n"
+        plan = {"rank": int(os.environ.get("RANK", "0")), "world": world, "gpus": args.gpus,
+                "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "workload": workload}
+        if world > 1:
+            plan["legs"] = run_legs(plan["rank"], world, workload, args)
+        line = json.dumps(plan) + "\n"
         os.write(1, line.encode())  # one write: ranks sharing the pipe never interleave a line
         return
     import torch
@@ -682,7 +729,18 @@ def main():
         out["forged_open"] = forged
     if args.e2e and rank == 0:
         out["e2e"] = e2e_host(eng, w, b)
-    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+    legs = run_legs(rank, world, workload, args)
+    if world == 1 and workload == "cfg2":
+        out["note"] = ("N = 1 runs BASELINE config 2 (the configuration the metric is quoted on); N > 1 runs config 5's "
+                       "strong split, whose line carries its own 1-GPU base (base_1gpu) and speed-up")
+    if "base_1gpu" in legs:
+        del b
+        torch.cuda.empty_cache()
+        base = base_one_gpu(eng)
+        out["base_1gpu"] = base
+        out["base_1gpu_gib_s"] = base["gib_s"]
+        out["speedup"] = round(value / base["gib_s"], 3) if base["gib_s"] else None
+    if "cpu_baseline" in legs:
         port, ossl = cpu_baselines(w, args.cpu_seconds, all_core_threads(args.cpu_threads))
         out["cpu_baseline"] = port
         if ossl:
@@ -690,6 +748,7 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:
+        dist.barrier()  # the other ranks wait for rank 0's extra legs
         dist.destroy_process_group()
 
 

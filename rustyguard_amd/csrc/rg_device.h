@@ -536,6 +536,119 @@ __device__ __forceinline__ void acc_fold(Acc &h) {
     h.h4 = (h.h4 & 3u) + k;
 }
 
+// --------------------------------------------------- buffer / LDS-DMA access
+// Raw buffer resources and LDS-DMA in inline asm: the compiler does not see these vector-memory
+// operations, so it inserts no vmcnt waits for them; the kernels count them and wait with exact
+// s_waitcnt vmcnt(N) (loads, stores and LDS-DMA retire in issue order on one counter).
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ v4i make_rsrc(const uint8_t *base, uint32_t num_records) {
+    const uint64_t a = (uint64_t)base;
+    v4i r;
+    r.x = (int)uniform_u32((uint32_t)a);
+    r.y = (int)uniform_u32((uint32_t)(a >> 32)); // stride 0
+    r.z = (int)uniform_u32(num_records);
+    r.w = 0x00020000; // raw buffer, 32-bit data format (gfx9 family)
+    return r;
+}
+
+// one LDS-DMA wave-instruction: 16 bytes per lane to lds_byte + 16 * lane
+__device__ __forceinline__ void dma16(const v4i &rsrc, uint32_t voff, uint32_t lds_byte) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\t"
+                 "s_mov_b32 m0, %3\n\t"
+                 "s_nop 0\n\t"
+                 "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+                 "s_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(voff), "s"(rsrc), "s"(lds_byte)
+                 : "memory");
+}
+
+__device__ __forceinline__ void store16(const v4i &rsrc, uint32_t voff, const uint4 &v) {
+    v4u d;
+    d.x = v.x;
+    d.y = v.y;
+    d.z = v.z;
+    d.w = v.w;
+    asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen\n\t"
+                 "s_nop 1"
+                 :
+                 : "v"(d), "v"(voff), "s"(rsrc)
+                 : "memory");
+}
+
+template <int N> __device__ __forceinline__ void wait_vm() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// ---------------------------------------------------- forged-frame restore
+// Open decrypts in place before the tag is known; a frame whose tag fails is turned back into the
+// ciphertext that came in (rustyguard-crypto/src/prim.rs:190-201: DecryptionError leaves the
+// buffer unchanged).  The chunks of every forged lane of the wave -- chunks [c0, c0 + ceil(nb / 4))
+// of its payload, pl pointing at chunk c0 -- are dealt over the wave's active lanes, 64 at a time,
+// and each is re-XORed with its keystream block.  A wave holding k forged packets of C chunks thus
+// pays ~k C / 64 keystream blocks instead of the one lane's C blocks for every forged lane in turn
+// (the whole wave waiting): the cost is per forged packet, not per wave.  The caller has made the
+// frames' stores visible to these loads (__threadfence).  Called by every active lane.
+__device__ __forceinline__ void restore_forged(bool forged, const Key8 &key, uint32_t n1, uint32_t n2, uint4 *pl,
+                                               uint32_t c0, uint32_t nb) {
+    const uint64_t active = __ballot(true);
+    uint64_t fm = __ballot(forged && nb > 0);
+    if (fm == 0) return;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t nact = (uint32_t)__popcll(active);
+    const uint32_t arank = (uint32_t)__popcll(active & ((1ull << lane) - 1ull)); // rank among active lanes
+    const uint32_t myC = (nb + 3) >> 2;
+    const uint64_t plv = reinterpret_cast<uint64_t>(pl);
+    int own = -1;      // forged lane whose chunk this lane re-XORs in the current round
+    uint32_t oc = 0;   // that chunk's index inside the owner's range
+    uint32_t pos = 0;  // next free active-lane rank (wave-uniform)
+    auto round = [&]() {
+        const int src = own >= 0 ? own : (int)lane; // every active lane takes part in the shuffles
+        Key8 k;
+#pragma unroll
+        for (int w = 0; w < 8; ++w) k.k[w] = (uint32_t)__shfl((int)key.k[w], src);
+        const uint32_t m1 = (uint32_t)__shfl((int)n1, src), m2 = (uint32_t)__shfl((int)n2, src);
+        const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)plv, src), hi = (uint32_t)__shfl((int)(uint32_t)(plv >> 32), src);
+        const uint32_t oc0 = (uint32_t)__shfl((int)c0, src), onb = (uint32_t)__shfl((int)nb, src);
+        if (own >= 0) {
+            uint4 *p = reinterpret_cast<uint4 *>(((uint64_t)hi << 32) | lo) + 4 * oc;
+            const uint32_t b0 = 4 * oc, last = onb - 1;
+            const uint4 q0 = p[min(b0, last) - b0], q1 = p[min(b0 + 1, last) - b0];
+            const uint4 q2 = p[min(b0 + 2, last) - b0], q3 = p[min(b0 + 3, last) - b0];
+            const Stream stm = make_stream(k, 0u, m1, m2);
+            uint32_t ks[16];
+            stream_block(stm, oc0 + oc + 1, ks);
+            if (b0 < onb) p[0] = xor4(q0, ks + 0);
+            if (b0 + 1 < onb) p[1] = xor4(q1, ks + 4);
+            if (b0 + 2 < onb) p[2] = xor4(q2, ks + 8);
+            if (b0 + 3 < onb) p[3] = xor4(q3, ks + 12);
+        }
+        own = -1;
+    };
+    while (fm) {
+        const uint32_t f = (uint32_t)__ffsll((unsigned long long)fm) - 1;
+        fm &= fm - 1;
+        const uint32_t Cf = (uint32_t)__builtin_amdgcn_readlane((int)myC, (int)f);
+        for (uint32_t done = 0; done < Cf;) {
+            const uint32_t take = min(Cf - done, nact - pos);
+            if (arank >= pos && arank < pos + take) {
+                own = (int)f;
+                oc = done + arank - pos;
+            }
+            pos += take;
+            done += take;
+            if (pos == nact) {
+                round();
+                pos = 0;
+            }
+        }
+    }
+    if (pos > 0) round();
+}
+
 __device__ __forceinline__ uint64_t mix64(uint64_t x) {
     uint64_t z = x + 0x9E3779B97F4A7C15ull;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;

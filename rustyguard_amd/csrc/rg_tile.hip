@@ -121,48 +121,7 @@ __global__ __launch_bounds__(256) void plan_kernel(const rg_pkt_desc *desc, uint
 // vmcnt waits are exact.
 constexpr uint32_t kOOB = 0xFFFFFFF0u;
 
-typedef int v4i __attribute__((ext_vector_type(4)));
-typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ v4i make_rsrc(const uint8_t *base, uint32_t num_records) {
-    const uint64_t a = (uint64_t)base;
-    v4i r;
-    r.x = (int)uniform_u32((uint32_t)a);
-    r.y = (int)uniform_u32((uint32_t)(a >> 32)); // stride 0
-    r.z = (int)uniform_u32(num_records);
-    r.w = 0x00020000; // raw buffer, 32-bit data format (gfx9 family)
-    return r;
-}
-
-// one LDS-DMA wave-instruction: 16 bytes per lane to lds_byte + 16 * lane
-__device__ __forceinline__ void dma16(const v4i &rsrc, uint32_t voff, uint32_t lds_byte) {
-    uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\t"
-                 "s_mov_b32 m0, %3\n\t"
-                 "s_nop 0\n\t"
-                 "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
-                 "s_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(voff), "s"(rsrc), "s"(lds_byte)
-                 : "memory");
-}
-
-__device__ __forceinline__ void store16(const v4i &rsrc, uint32_t voff, const uint4 &v) {
-    v4u d;
-    d.x = v.x;
-    d.y = v.y;
-    d.z = v.z;
-    d.w = v.w;
-    asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen\n\t"
-                 "s_nop 1"
-                 :
-                 : "v"(d), "v"(voff), "s"(rsrc)
-                 : "memory");
-}
-
-template <int N> __device__ __forceinline__ void wait_vm() {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
+// make_rsrc / dma16 / store16 / wait_vm: rg_device.h
 
 // segment hand-off slot per wave: rows 0-4 partial sum A_j, 5-9 q_j = r^{n_j},
 // 10 the open verdict sent back by segment 0
@@ -762,19 +721,11 @@ __global__ __launch_bounds__(512) void tile_kernel(SealArgs sa, OpenArgs oa, Til
                     bad = mine[10 * 64 + lane] != 0;
                 }
             }
-            if (bad) {
-                // each chunk's loads (clamped inside the payload) go out before its keystream block
-                uint4 *pl = reinterpret_cast<uint4 *>(frame + 16);
-                for (uint32_t c = c0; c < c1; ++c) {
-                    const uint32_t b0 = 4 * c, last = nb - 1;
-                    const uint4 m0 = pl[min(b0, last)], m1 = pl[min(b0 + 1, last)];
-                    const uint4 m2 = pl[min(b0 + 2, last)], m3 = pl[min(b0 + 3, last)];
-                    stream_block(stm, c + 1, ks);
-                    if (b0 < nb) pl[b0] = xor4(m0, ks + 0);
-                    if (b0 + 1 < nb) pl[b0 + 1] = xor4(m1, ks + 4);
-                    if (b0 + 2 < nb) pl[b0 + 2] = xor4(m2, ks + 8);
-                    if (b0 + 3 < nb) pl[b0 + 3] = xor4(m3, ks + 12);
-                }
+            if (__ballot(bad)) {
+                // the forged segments' chunks dealt over the wave's lanes (restore_forged): a lane re-XORs
+                // chunks another lane's window stores wrote, so those complete and this CU's L1 goes first
+                __threadfence();
+                restore_forged(bad, key, n1, n2, reinterpret_cast<uint4 *>(frame + 16) + 4 * c0, c0, snb);
             }
         }
     }

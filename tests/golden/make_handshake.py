@@ -71,8 +71,9 @@ def chacha_block(key: bytes, counter: int, rounds: int) -> list[int]:
 
 
 class StdRng:
-    def __init__(self, seed: int):
-        self.key = pcg32_seed(seed)
+    def __init__(self, seed: int | None = None, key: bytes | None = None):
+        # seed_from_u64 (PCG32-expanded seed), or from_seed / from_rng (a 32-byte key taken as is)
+        self.key = pcg32_seed(seed) if key is None else key
         self.block = 0
         self.words: list[int] = []
 
@@ -252,10 +253,58 @@ def core_snapshot_macs() -> dict:
             "response": resp.hex(), "response_mac1_key": k_i.hex()}
 
 
+def core_snapshot_initiation_aead() -> dict:
+    """The two AEAD fields of the reference's recorded initiation (test `snapshot`, seed 1), re-derived:
+    encrypted_static (P = 32) and encrypted_timestamp (P = 12), both sealed under AAD = the transcript
+    hash (encrypt_handshake_init, rustyguard-crypto/src/lib.rs:287-344).  The initiator's ephemeral
+    key comes from its inner RNG, ChaCha12Rng::from_rng of words 58-65 of the seed-1 stream (reseeded
+    by the first `turn`, rustyguard-core/src/lib.rs:396-409), after the sender
+    id (rustyguard-core/src/handshake.rs:271-275); its public key must be the snapshot's ephemeral field.
+    The timestamp's plaintext is the test clock's TAI64N, recovered by opening the field (the tag must
+    verify under the derived key and hash)."""
+    from oracle import oracle
+
+    outer = StdRng(1)
+    words = [outer.next_u32() for _ in range(128)]
+    ssk_i, ssk_r = b"".join(w.to_bytes(4, "little") for w in words[0:8]), b"".join(
+        w.to_bytes(4, "little") for w in words[8:16])
+    pk_i, pk_r = pubkey(ssk_i), pubkey(ssk_r)
+    inner = StdRng(key=b"".join(w.to_bytes(4, "little") for w in words[58:66]))
+    init = snap_bytes(f"{REF}/rustyguard-core/src/snapshots/rustyguard_core__tests__snapshot.snap")
+    sender = inner.next_u32()
+    assert sender == 0x2F65BA4A and init[4:8] == sender.to_bytes(4, "little"), "initiator sender id"
+    esk_i = inner.fill(32)
+    epk_i = pubkey(esk_i)
+    assert epk_i == init[8:40], "ephemeral public key"
+    hs = HS()
+    hs.mix_hash(pk_r)
+    hs.mix_hash(epk_i)
+    hs.mix_chain(epk_i)
+    k_es = hs.mix_key(x25519(esk_i, pk_r))
+    aad_static = hs.hash
+    ct, tag = aead_seal(k_es, aad_static, pk_i)
+    assert ct + tag == init[40:88], "encrypted_static"
+    hs.mix_hash(ct + tag)
+    k_ss = hs.mix_key(x25519(ssk_i, pk_r))
+    aad_ts = hs.hash
+    ts = oracle.aead_open(k_ss, b"\0" * 12, aad_ts, init[88:100], init[100:116])
+    assert ts is not None and len(ts) == 12, "encrypted_timestamp tag"
+    assert aead_seal(k_ss, aad_ts, ts) == (init[88:100], init[100:116])
+    src = ("rustyguard-core/src/lib.rs:846-925 (test `snapshot`, StdRng seed 1) -> "
+           "rustyguard-core/src/snapshots/rustyguard_core__tests__snapshot.snap bytes 40-88 / 88-116")
+    return {"source": src,
+            "encrypted_static": {"key": k_es.hex(), "nonce": (b"\0" * 12).hex(), "aad": aad_static.hex(),
+                                 "plaintext": pk_i.hex(), "ciphertext": init[40:72].hex(), "tag": init[72:88].hex()},
+            "encrypted_timestamp": {"key": k_ss.hex(), "nonce": (b"\0" * 12).hex(), "aad": aad_ts.hex(),
+                                    "plaintext": ts.hex(), "ciphertext": init[88:100].hex(),
+                                    "tag": init[100:116].hex()}}
+
+
 def main():
     out = {"generator": "tests/golden/make_handshake.py (rand 0.9 StdRng + X25519 + BLAKE2s restated; "
                         "every value checked against the reference's .snap files)",
-           "aead_with_aad": crypto_handshake_resp(), "handshake_macs": core_snapshot_macs()}
+           "aead_with_aad": crypto_handshake_resp(), "handshake_macs": core_snapshot_macs(),
+           "initiation_aead": core_snapshot_initiation_aead()}
     with open(os.path.join(HERE, "handshake_vectors.json"), "w") as f:
         json.dump(out, f, indent=1)
         f.write("\n")

@@ -887,6 +887,34 @@ def test_aead_with_aad_reference_handshake_snapshot(engine):
         engine.chacha20poly1305_dec(key, nonce, bytes(bad), bytearray(), tag)
 
 
+def test_aead_reference_initiation_fields(engine):
+    """The per-message drop-in at lengths that are not multiples of 16, with a 32-byte AAD, against the
+    reference's own bytes: encrypted_static (P = 32) and encrypted_timestamp (P = 12) of the recorded
+    148-byte initiation (rustyguard-core/src/snapshots/rustyguard_core__tests__snapshot.snap; sealed by
+    encrypt_handshake_init, rustyguard-crypto/src/lib.rs:287-344), keys and transcript hashes
+    re-derived by tests/golden/make_handshake.py.  Seal reproduces them, open restores the plaintext,
+    and a flipped AAD, ciphertext or tag bit is a DecryptionError that leaves the payload untouched."""
+    g = load_golden("handshake_vectors.json")["initiation_aead"]
+    for name in ("encrypted_static", "encrypted_timestamp"):
+        v = g[name]
+        key, nz, aad = bytes.fromhex(v["key"]), bytes.fromhex(v["nonce"]), bytes.fromhex(v["aad"])
+        buf = bytearray.fromhex(v["plaintext"])
+        tag = engine.chacha20poly1305_enc(key, nz, aad, buf)
+        assert buf.hex() == v["ciphertext"] and tag.hex() == v["tag"], name
+        engine.chacha20poly1305_dec(key, nz, aad, buf, tag)
+        assert buf.hex() == v["plaintext"], name
+        ct = bytearray.fromhex(v["ciphertext"])
+        for a, c, t in ((bytes([aad[0] ^ 1]) + aad[1:], ct, tag), (aad, ct, bytes([tag[0] ^ 0x80]) + tag[1:])):
+            body = bytearray(c)
+            with pytest.raises(aead.DecryptionError):
+                engine.chacha20poly1305_dec(key, nz, a, body, t)
+            assert body == ct
+        body = bytearray(ct)
+        body[-1] ^= 1
+        with pytest.raises(aead.DecryptionError):
+            engine.chacha20poly1305_dec(key, nz, aad, body, tag)
+
+
 def test_auto_routes_mixed_small_batches_to_flat():
     """Automatic kernel choice (rg_get_kernel / rg_last_kernel): the first IMIX batch runs the planned
     pipelined kernel, whose planner sees several size classes; the next ones run the flattened chunk

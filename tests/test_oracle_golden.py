@@ -180,3 +180,21 @@ def test_reference_handshake_vectors():
     init, resp = bytes.fromhex(m["initiation"]), bytes.fromhex(m["response"])
     assert oracle.blake2s(init[:116], bytes.fromhex(m["initiation_mac1_key"]), 16) == init[116:132]
     assert oracle.blake2s(resp[:60], bytes.fromhex(m["response_mac1_key"]), 16) == resp[60:76]
+
+
+def test_reference_initiation_aead_fields():
+    """The recorded initiation's encrypted_static (P = 32) and encrypted_timestamp (P = 12), both with
+    AAD = the transcript hash (encrypt_handshake_init, rustyguard-crypto/src/lib.rs:287-344), re-derived
+    by make_handshake.py: the oracle seals each to the snapshot's bytes and opens them back."""
+    g = load_golden("handshake_vectors.json")
+    init = bytes.fromhex(g["handshake_macs"]["initiation"])
+    fields = g["initiation_aead"]
+    for name, (lo, hi) in (("encrypted_static", (40, 88)), ("encrypted_timestamp", (88, 116))):
+        v = fields[name]
+        key, nz, aad, pt = (bytes.fromhex(v[k]) for k in ("key", "nonce", "aad", "plaintext"))
+        ct, tag = oracle.aead_seal(key, nz, aad, pt)
+        assert ct + tag == init[lo:hi] and ct.hex() == v["ciphertext"] and tag.hex() == v["tag"], name
+        assert oracle.aead_open(key, nz, aad, ct, tag) == pt
+        bad = bytearray(aad)
+        bad[0] ^= 1
+        assert oracle.aead_open(key, nz, bytes(bad), ct, tag) is None
