@@ -719,7 +719,7 @@ __device__ __forceinline__ void pipe_seal_packet(const SealArgs &a, uint32_t i, 
             const uint4 hdr = a.receivers != nullptr ? make_uint4(4u, a.receivers[d.key_idx], n1, n2)
                                                      : *reinterpret_cast<const uint4 *>(frame);
             retire_loads(key, n1, n2, hdr, hdr);
-            const uint32_t nb = P >> 4, C = (nb + 3) >> 2;
+            const uint32_t nb = uniform_u32(P >> 4), C = (nb + 3) >> 2; // one size on every lane: scalar loop control
             for (uint32_t c = 0; c < min(kDmaDepth, C); ++c) stage_chunk(S, c, nb, 0u);
             const Stream stm = make_stream(key, 0u, n1, n2);
             uint32_t ks[16];
@@ -812,7 +812,7 @@ __device__ __forceinline__ void pipe_open_packet(const OpenArgs &a, uint32_t i, 
         const uint64_t span = wave_span(frame, W, lo);
         if (__ballot(hdr.x == 4u) == ~0ull && span <= kStageSpan) {
             const Stage S = make_stage(frame, lo, span);
-            const uint32_t P = W - 32, nb = P >> 4, C = (nb + 3) >> 2;
+            const uint32_t P = uniform_u32(W - 32), nb = P >> 4, C = (nb + 3) >> 2; // scalar loop control
             const uint4 want = *reinterpret_cast<const uint4 *>(frame + 16 + P);
             const Key8 key = load_key(a.keys, d.key_idx);
             const uint64_t ctr = ((uint64_t)hdr.w << 32) | hdr.z;
