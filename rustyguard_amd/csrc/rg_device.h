@@ -590,8 +590,12 @@ template <int N> __device__ __forceinline__ void wait_vm() {
 // of its payload, pl pointing at chunk c0 -- are dealt over the wave's active lanes, 64 at a time,
 // and each is re-XORed with its keystream block.  A wave holding k forged packets of C chunks thus
 // pays ~k C / 64 keystream blocks instead of the one lane's C blocks for every forged lane in turn
-// (the whole wave waiting): the cost is per forged packet, not per wave.  The caller has made the
-// frames' stores visible to these loads (__threadfence).  Called by every active lane.
+// (the whole wave waiting): the cost is per forged packet, not per wave.  Every byte involved was
+// stored by this wave: its vector-memory instructions are performed in order, so a wavefront-scope
+// fence (wave_sync: no waitcnt, no cache maintenance) orders the restore's loads after the stores.
+// (An agent-scope __threadfence costs a buffer_wbl2 -- the write-back of every dirty line of the
+// XCD's L2 -- and a workgroup-scope one a vmcnt(0) store drain: +50 % and +37 % on config 2's open
+// with 1 % of the frames forged, profiles/r3_forged_open.txt.)  Called by every active lane.
 __device__ __forceinline__ void restore_forged(bool forged, const Key8 &key, uint32_t n1, uint32_t n2, uint4 *pl,
                                                uint32_t c0, uint32_t nb) {
     const uint64_t active = __ballot(true);

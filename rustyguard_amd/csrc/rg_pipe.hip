@@ -105,10 +105,6 @@ __device__ __forceinline__ void absorb_chunk(Acc &h, const Chunk &c, const Mul &
 #define RG_PIPE_OPEN_CUR 1
 #endif
 constexpr bool PIPE_OPEN_CUR = RG_PIPE_OPEN_CUR != 0;
-// the staged (LDS-DMA) chunk stream of uniform waves, below
-#ifndef RG_PIPE_DMA
-#define RG_PIPE_DMA 1
-#endif
 #ifndef RG_PIPE_LOAD_FIRST
 #define RG_PIPE_LOAD_FIRST 0
 #endif
@@ -195,230 +191,16 @@ __device__ __forceinline__ void ring_store(const Ring &R, const Ring4 &x, uint32
             asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(dst), "v"(x.v[q]) : "memory");
         else if constexpr (PIPE_WT == 2) // non-temporal (streaming) whole-line stores
             asm volatile("global_store_dwordx4 %0, %1, off nt\n\ts_nop 1" ::"v"(dst), "v"(x.v[q]) : "memory");
+        else if constexpr (PIPE_WT == 3) // plain stores pinned where they are issued (spread experiment)
+            asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" ::"v"(dst), "v"(x.v[q]) : "memory");
         else *dst = x.v[q];
     }
 }
 
-// ------------------------------------------------------------- LDS-DMA chunk stream
-// A wave of valid packets of one size (the line-store case above) takes its payload chunks by
-// LDS-DMA instead of loads into VGPRs.  Reason (profiles/r3_*): with register loads the compiler's
-// vmcnt waits are conservative -- waiting for a chunk's loads also waited for loads issued a step
-// later, and since loads and stores retire in issue order on one counter, for the line stores of
-// two steps back: the ARX wave sat on store acknowledgements (slower acks, slower waves: debug
-// mode 8).  The DMA instructions are inline asm, invisible to the compiler's waitcnt pass; the
-// kernel counts every vector-memory instruction it issues and waits with an exact vmcnt for the
-// chunk it is about to read, kDmaDepth chunks ahead, so the stores of up to kDmaDepth - 1 steps
-// stay in flight.  Chunk c's four pieces land in slot c % kDmaDepth of the wave's staging area
-// (piece q of lane l at byte 1024 q + 16 l: one conflict-free ds_read_b128 per piece).
-constexpr uint32_t kPipeDmaFlag = 8u; // launch flag bit: the staging area is reserved too
-#ifndef RG_PIPE_DMA_DEPTH
-#define RG_PIPE_DMA_DEPTH 5
-#endif
-constexpr uint32_t kDmaDepth = RG_PIPE_DMA_DEPTH;
-constexpr uint32_t kStageBytes = kDmaDepth * 4096u; // per wave
-static_assert(kDmaDepth >= 2 && 4 * (kRingBytes + kStageBytes) <= kLdsPerCu, "ring + staging of 4 waves fit one CU");
-
-struct Stage {
-    v4i rsrc;          // raw buffer over the wave's frames
-    uint32_t voff;     // this lane's payload block 0, relative to the resource base
-    uint32_t lds;      // LDS byte address of the wave's slot 0 (wave-uniform)
-    const lds_u4 *rd;  // this lane's piece 0 of slot 0
-};
-
-// the wave's frames [lo, hi) (wave-uniform); the staged stream needs hi - lo inside a 32-bit window
-__device__ __forceinline__ uint64_t wave_span(const uint8_t *frame, uint32_t W, uint64_t &lo_out) {
-    uint64_t lo = reinterpret_cast<uint64_t>(frame), hi = lo + W;
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) {
-        const uint64_t a = __shfl_xor(lo, m), b = __shfl_xor(hi, m);
-        lo = a < lo ? a : lo;
-        hi = b > hi ? b : hi;
-    }
-    lo_out = uniform_u64(lo);
-    return uniform_u64(hi) - lo_out;
-}
-constexpr uint64_t kStageSpan = 0xFFFFF000ull;
-
-__device__ __forceinline__ Stage make_stage(const uint8_t *frame, uint64_t lo, uint64_t span) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t pipe_lds[];
-    Stage S;
-    S.rsrc = make_rsrc(reinterpret_cast<const uint8_t *>(lo), (uint32_t)span);
-    S.voff = (uint32_t)(reinterpret_cast<uint64_t>(frame) - lo) + 16u;
-    uint8_t *st = pipe_lds + 4 * kRingBytes + (threadIdx.x >> 6) * kStageBytes;
-    S.lds = uniform_u32((uint32_t)(uintptr_t)st);
-    S.rd = (const lds_u4 *)st + (threadIdx.x & 63);
-    return S;
-}
-
-// one LDS-DMA wave-instruction (dma16), issued only once `dep` is computed: the slot it refills was
-// read into registers by this wave, and those reads must have returned first
-__device__ __forceinline__ void dma16_after(const v4i &rsrc, uint32_t voff, uint32_t lds_byte, uint32_t dep) {
-    uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\t"
-                 "s_mov_b32 m0, %3\n\t"
-                 "s_nop 0\n\t"
-                 "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
-                 "s_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(voff), "s"(rsrc), "s"(lds_byte), "v"(dep)
-                 : "memory");
-}
-
-// chunk c of an nb-block payload into slot c % kDmaDepth (pieces clamped to the last block)
-__device__ __forceinline__ void stage_chunk(const Stage &S, uint32_t c, uint32_t nb, uint32_t dep) {
-    const uint32_t lb = uniform_u32(S.lds + (c % kDmaDepth) * 4096u);
-    const uint32_t b = 4 * c, last = nb - 1;
-    dma16_after(S.rsrc, S.voff + 16 * min(b, last), lb, dep);
-    dma16_after(S.rsrc, S.voff + 16 * min(b + 1, last), lb + 1024u, dep);
-    dma16_after(S.rsrc, S.voff + 16 * min(b + 2, last), lb + 2048u, dep);
-    dma16_after(S.rsrc, S.voff + 16 * min(b + 3, last), lb + 3072u, dep);
-}
-
-__device__ __forceinline__ Chunk read_chunk(const Stage &S, uint32_t c) {
-    const lds_u4 *p = S.rd + (c % kDmaDepth) * 256u;
-    const v4u a = p[0], b = p[64], d = p[128], e = p[192];
-    return {make_uint4(a.x, a.y, a.z, a.w), make_uint4(b.x, b.y, b.z, b.w), make_uint4(d.x, d.y, d.z, d.w),
-            make_uint4(e.x, e.y, e.z, e.w)};
-}
-
-// Vector-memory instructions the wave issued after chunk t's four DMAs, when step t begins (so
-// s_waitcnt vmcnt(that) retires exactly them and everything older).  Issue order: the prologue
-// DMAs chunks 0 .. P-1 (P = min(kDmaDepth, C)); step s then issues its line stores (4, steps
-// s >= 2) and the DMAs of chunk s + kDmaDepth (4, while < C).  Chunk t >= P was issued at the end of
-// step t - kDmaDepth.
-__device__ __forceinline__ uint32_t dma_younger(uint32_t t, uint32_t P, uint32_t C) {
-    const int D = (int)kDmaDepth, T = (int)t;
-    const int a = T < (int)P ? 0 : T - D + 1;
-    const int pro = T < (int)P ? (int)P - 1 - T : 0;
-    const int nst = max(0, T - max(a, 2));
-    const int ndma = max(0, min(T, (int)C - D) - a);
-    return 4u * (uint32_t)(pro + nst + ndma);
-}
-
-// s_waitcnt takes an immediate: y (wave-uniform, a multiple of 4) picks it
-__device__ __forceinline__ void wait_staged(uint32_t y) {
-    switch (y) {
-    case 0: wait_vm<0>(); break;
-    case 4: wait_vm<4>(); break;
-    case 8: wait_vm<8>(); break;
-    case 12: wait_vm<12>(); break;
-    case 16: wait_vm<16>(); break;
-    case 20: wait_vm<20>(); break;
-    case 24: wait_vm<24>(); break;
-    case 28: wait_vm<28>(); break;
-    case 32: wait_vm<32>(); break;
-    case 36: wait_vm<36>(); break;
-    case 40: wait_vm<40>(); break;
-    case 44: wait_vm<44>(); break;
-    case 48: wait_vm<48>(); break;
-    default: wait_vm<0>(); break;
-    }
-}
-
-// the compiler's own loads (key, counter, header, tag) retire here, before the first DMA: its
-// waitcnt pass does not count the DMAs, so a wait it placed after them would be a vmcnt(0)
-__device__ __forceinline__ void retire_loads(const Key8 &k, uint32_t a, uint32_t b, const uint4 &x, const uint4 &y) {
-    asm volatile("" ::"v"(k.k[0]), "v"(k.k[1]), "v"(k.k[2]), "v"(k.k[3]), "v"(k.k[4]), "v"(k.k[5]), "v"(k.k[6]),
-                 "v"(k.k[7]), "v"(a), "v"(b));
-    asm volatile("" ::"v"(x.x), "v"(x.y), "v"(x.z), "v"(x.w), "v"(y.x), "v"(y.y), "v"(y.z), "v"(y.w));
-}
-
-// One full-chunk step of the staged stream (the line-store step of pipe_step, chunk t from LDS):
-// wait for chunk t, read it, keystream block t + 1 with the Poly1305 blocks in its rounds (seal:
-// the previous chunk's ciphertext, open: this chunk's), XOR, block t into the ring, half a line out
-// (FLUSH), then chunk t + kDmaDepth into the slot just read.
-template <bool OPEN, bool ABSORB, bool FLUSH>
-__device__ __forceinline__ void dma_step(const Stage &S, const Stream &st, const Mul &r, Acc &h, Chunk &pi,
-                                         uint4 &prev, uint32_t t, uint32_t P, uint32_t C, uint32_t nb,
-                                         const Ring &R) {
-    wait_staged(dma_younger(t, P, C));
-    const Chunk m = read_chunk(S, t);
-    Ring4 fl;
-    if constexpr (FLUSH) {
-        wave_sync(); // block t - 1 was put by every lane
-        fl = ring_get(R, (t - 2) >> 1, t & 1u);
-    }
-    uint32_t ks[16];
-    stream_block_hooked(st, t + 1, ks, [&](int dr) {
-        if constexpr (OPEN) {
-            if (dr == 1) acc_block(h, m.q0, r);
-            if (dr == 3) acc_block(h, m.q1, r);
-            if (dr == 5) acc_block(h, m.q2, r);
-            if (dr == 7) acc_block(h, m.q3, r);
-            if (dr % 2 == 1) pin_acc(h);
-        } else if constexpr (ABSORB) {
-            if (dr == 1) acc_block(h, pi.q0, r);
-            if (dr == 3) acc_block(h, pi.q1, r);
-            if (dr == 5) acc_block(h, pi.q2, r);
-            if (dr == 7) acc_block(h, pi.q3, r);
-            if (dr % 2 == 1) pin_acc(h);
-        }
-    });
-    const Chunk x = {xor4(m.q0, ks + 0), xor4(m.q1, ks + 4), xor4(m.q2, ks + 8), xor4(m.q3, ks + 12)};
-    ring_put(R, t, prev, x.q0, x.q1, x.q2);
-    if constexpr (FLUSH) ring_store(R, fl, (t - 2) >> 1, t & 1u);
-    prev = x.q3;
-    if constexpr (!OPEN) pi = x;
-    if (t + kDmaDepth < C) stage_chunk(S, t + kDmaDepth, nb, x.q3.w);
-}
-
-// pipe_pass for a wave of valid packets of one size with the chunk stream staged by LDS-DMA (the
-// caller issued the prologue DMAs of chunks 0 .. min(kDmaDepth, C) - 1 before the one-time-key
-// block).  head: block 0's first piece (the header to write, or the one in the frame).
-template <bool OPEN>
-__device__ __forceinline__ Acc pipe_pass_dma(uint4 *pl, const Stream &st, const Mul &r, uint32_t nb, uint4 head,
-                                             const Ring &R, const Stage &S) {
-    const uint32_t F = nb >> 2, bl = nb & 3u, C = F + (bl ? 1u : 0u), P = min(kDmaDepth, C);
-    Acc h = {0, 0, 0, 0, 0};
-    Chunk pi = {};
-    uint4 prev = head;
-    wave_sync(); // the previous packet's last read-back is done
-    if (F > 0) dma_step<OPEN, false, false>(S, st, r, h, pi, prev, 0, P, C, nb, R);
-    if (F > 1) dma_step<OPEN, true, false>(S, st, r, h, pi, prev, 1, P, C, nb, R);
-    for (uint32_t t = 2; t < F; ++t) dma_step<OPEN, true, true>(S, st, r, h, pi, prev, t, P, C, nb, R);
-    Chunk m = {};
-    if (bl) { // the partial last chunk, read before the flush stores below (the count assumes so)
-        wait_staged(dma_younger(F, P, C));
-        m = read_chunk(S, F);
-    }
-    if (F > 0) { // the halves not stored yet (as pipe_pass)
-        wave_sync();
-        for (uint32_t k = F >= 2 ? F - 2 : 0; k < 2 * ((F + 1) >> 1); ++k)
-            ring_store<true>(R, ring_get(R, k >> 1, k & 1u), k >> 1, k & 1u, F);
-    }
-    uint4 *dst = pl + 4 * F;
-    if (bl) {
-        uint32_t ks[16];
-        const bool full = F > 0;
-        stream_block_hooked(st, F + 1, ks, [&](int dr) {
-            if constexpr (OPEN) {
-                if (dr == 1) acc_block_pred(h, m.q0, r, true);
-                if (dr == 3) acc_block_pred(h, m.q1, r, bl > 1);
-                if (dr == 5) acc_block_pred(h, m.q2, r, bl > 2);
-            } else {
-                if (dr == 1) acc_block_pred(h, pi.q0, r, full);
-                if (dr == 3) acc_block_pred(h, pi.q1, r, full);
-                if (dr == 5) acc_block_pred(h, pi.q2, r, full);
-                if (dr == 7) acc_block_pred(h, pi.q3, r, full);
-            }
-            if (dr % 2 == 1) pin_acc(h);
-        });
-        const uint4 x0 = xor4(m.q0, ks + 0), x1 = xor4(m.q1, ks + 4), x2 = xor4(m.q2, ks + 8);
-        dst[-1] = prev; // the last full chunk's final block, or the header (F == 0)
-        dst[0] = x0;
-        if (bl > 1) dst[1] = x1;
-        if (bl > 2) dst[2] = x2;
-        if constexpr (!OPEN) {
-            acc_block(h, x0, r);
-            acc_block_pred(h, x1, r, bl > 1);
-            acc_block_pred(h, x2, r, bl > 2);
-        }
-    } else {
-        dst[-1] = prev; // the last chunk's final block (or the header of an empty payload)
-        if constexpr (!OPEN)
-            if (F > 0) absorb_chunk(h, pi, r, 4);
-    }
-    return h;
+// store q of ring_store (the spread experiment): an asm store, so that it stays where it is issued
+__device__ __forceinline__ void ring_store_one(const Ring &R, const Ring4 &x, uint32_t k, uint32_t h, int q) {
+    glb_u4 *dst = (h ? R.fr[1][q] : R.fr[0][q]) + 8 * k;
+    asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" ::"v"(dst), "v"(x.v[q]) : "memory");
 }
 
 // One step: keystream block t+1 -- with the previous chunk's four Poly1305
@@ -441,6 +223,16 @@ __device__ __forceinline__ Acc pipe_pass_dma(uint4 *pl, const Stream &st, const 
 // LINES: the frame blocks go through the wave's LDS ring (block t goes into
 // the ring; with FLUSH, half t & 1 of line (t - 2) / 2 is read back before the
 // rounds and stored after them).
+// experiment: the step's four line stores issued one by one inside the keystream rounds (after double
+// rounds 2, 4, 6, 8) instead of back to back after them
+#ifndef RG_PIPE_SPREAD
+#define RG_PIPE_SPREAD 0
+#endif
+// experiment: wave w of a workgroup starts w * RG_PIPE_STAGGER x 64 cycles late, so that the four
+// waves of a CU (identical work, lockstep) do not issue their memory instructions at the same time
+#ifndef RG_PIPE_STAGGER
+#define RG_PIPE_STAGGER 0
+#endif
 template <bool OPEN, bool ABSORB, bool TAIL, int MODE = 0, bool LINES = false, bool FLUSH = false>
 __device__ __forceinline__ void pipe_step(uint4 *pl, const Stream &st, const Mul &r, Acc &h, Chunk &pi, Chunk &buf,
                                           uint4 &prev, bool &have_prev, uint32_t t, uint32_t nb, uint32_t c0,
@@ -457,6 +249,9 @@ __device__ __forceinline__ void pipe_step(uint4 *pl, const Stream &st, const Mul
         for (int i = 0; i < 16; ++i) ks[i] = t * 16 + i;
         h.h0 ^= pi.q0.x ^ pi.q1.y ^ pi.q2.z ^ pi.q3.w;
     } else stream_block_hooked(st, c0 + t + 1, ks, [&](int dr) {
+        if constexpr (FLUSH && RG_PIPE_SPREAD && MODE != 8) {
+            if (dr == 2 || dr == 4 || dr == 6 || dr == 8) ring_store_one(R, fl, (t - 2) >> 1, t & 1u, dr / 2 - 1);
+        }
         if constexpr (OPEN && PIPE_OPEN_CUR) { // this chunk's ciphertext (TAIL: its nb % 4 blocks)
             const uint32_t bl = TAIL ? nb & 3u : 4u;
             if (dr == 1) acc_block_pred(h, buf.q0, r, bl > 0);
@@ -488,7 +283,8 @@ __device__ __forceinline__ void pipe_step(uint4 *pl, const Stream &st, const Mul
     }
     if constexpr (LINES && !TAIL) {
         ring_put(R, t, prev, x.q0, x.q1, x.q2); // prev: the header before the first chunk
-        if constexpr (FLUSH) ring_store(R, fl, MODE == 8 ? ((t - 2) >> 1) & 1u : (t - 2) >> 1, t & 1u);
+        if constexpr (FLUSH && !(RG_PIPE_SPREAD && MODE != 8))
+            ring_store(R, fl, MODE == 8 ? ((t - 2) >> 1) & 1u : (t - 2) >> 1, t & 1u);
         prev = x.q3;
         have_prev = true;
     } else if constexpr (TAIL) {
@@ -697,7 +493,7 @@ __device__ __forceinline__ Acc combine_segments(Acc h, const Mul &r, uint32_t af
 // segment j; lane 0 writes header, tag and status.
 template <int MODE>
 __device__ __forceinline__ void pipe_seal_packet(const SealArgs &a, uint32_t i, const rg_pkt_desc &d, uint32_t j,
-                                                 uint32_t G, bool lines_ok, bool dma_ok) {
+                                                 uint32_t G, bool lines_ok) {
     const uint32_t P = d.len;
     const bool valid = d.key_idx < a.nkeys && (P & 15u) == 0 && (d.offset & 15u) == 0 && P <= kMaxPayload &&
                        d.offset <= a.buf_len && P + 32 <= a.buf_len - d.offset;
@@ -705,35 +501,6 @@ __device__ __forceinline__ void pipe_seal_packet(const SealArgs &a, uint32_t i, 
     bool lines = false;
     if constexpr (MODE == 0 || MODE == 8)
         lines = lines_ok && G == 1 && __ballot(valid && P == uniform_u32(P)) == ~0ull;
-    if constexpr (MODE == 0) {
-        uint8_t *frame = a.buf + d.offset;
-        uint64_t lo = 0;
-        const uint64_t span = lines && dma_ok ? wave_span(frame, P + 32, lo) : ~0ull;
-        if (span <= kStageSpan) { // wave-uniform
-            const Stage S = make_stage(frame, lo, span);
-            // the staged chunk stream (pipe_pass_dma); the compiler's loads retire before the first DMA
-            const Key8 key = load_key(a.keys, d.key_idx);
-            const uint64_t ctr = a.counters[i];
-            const uint32_t n1 = (uint32_t)ctr, n2 = (uint32_t)(ctr >> 32); // nonce = 0 || le64(ctr) (prim.rs:32-36)
-            // DataHeader {4, receiver, counter} (rustyguard-core/src/lib.rs:286-290), or the frame's own
-            const uint4 hdr = a.receivers != nullptr ? make_uint4(4u, a.receivers[d.key_idx], n1, n2)
-                                                     : *reinterpret_cast<const uint4 *>(frame);
-            retire_loads(key, n1, n2, hdr, hdr);
-            const uint32_t nb = uniform_u32(P >> 4), C = (nb + 3) >> 2; // one size on every lane: scalar loop control
-            for (uint32_t c = 0; c < min(kDmaDepth, C); ++c) stage_chunk(S, c, nb, 0u);
-            const Stream stm = make_stream(key, 0u, n1, n2);
-            uint32_t ks[16];
-            stream_block(stm, 0, ks); // RFC 8439 §2.6 one-time key; covers the first chunks' latency
-            const Mul r = make_mul(ks[0], ks[1], ks[2], ks[3]);
-            uint4 *pl = reinterpret_cast<uint4 *>(frame + 16);
-            const Acc h = pipe_pass_dma<false>(pl, stm, r, nb, hdr, make_ring(frame), S);
-            uint32_t tag[4];
-            pipe_tag(h, r, P, ks + 4, tag);
-            *reinterpret_cast<uint4 *>(frame + 16 + P) = make_uint4(tag[0], tag[1], tag[2], tag[3]);
-            if (a.status) a.status[i] = RG_PKT_OK;
-            return;
-        }
-    }
     if (!valid) {
         if (a.status && j == 0) a.status[i] = d.key_idx == RG_KEY_SKIP ? RG_PKT_REJECTED : RG_PKT_INVALID;
         return;
@@ -793,7 +560,7 @@ __device__ __forceinline__ void pipe_seal_packet(const SealArgs &a, uint32_t i, 
 // (constant-time compare, identical on every lane of the group) makes each
 // lane re-apply its segment's keystream, so the frame is left unchanged.
 __device__ __forceinline__ void pipe_open_packet(const OpenArgs &a, uint32_t i, const rg_pkt_desc &d, uint32_t j,
-                                                 uint32_t G, bool lines_ok, bool dma_ok) {
+                                                 uint32_t G, bool lines_ok) {
     const uint32_t W = d.len;
     uint32_t st;
     if (d.key_idx == RG_KEY_SKIP) st = RG_PKT_REJECTED;
@@ -803,40 +570,6 @@ __device__ __forceinline__ void pipe_open_packet(const OpenArgs &a, uint32_t i, 
         st = RG_PKT_INVALID;
     else st = 0xFF;
     uint8_t *frame = a.buf + d.offset;
-    // A wave of whole data frames of one length takes the staged chunk stream (pipe_pass_dma): the
-    // descriptors decide the candidate, the headers (all type 4) confirm it, else the general path below.
-    if (lines_ok && dma_ok && G == 1 &&
-        __ballot(st == 0xFF && W >= 32 && (W & 15u) == 0 && W == uniform_u32(W)) == ~0ull) {
-        const uint4 hdr = *reinterpret_cast<const uint4 *>(frame);
-        uint64_t lo = 0;
-        const uint64_t span = wave_span(frame, W, lo);
-        if (__ballot(hdr.x == 4u) == ~0ull && span <= kStageSpan) {
-            const Stage S = make_stage(frame, lo, span);
-            const uint32_t P = uniform_u32(W - 32), nb = P >> 4, C = (nb + 3) >> 2; // scalar loop control
-            const uint4 want = *reinterpret_cast<const uint4 *>(frame + 16 + P);
-            const Key8 key = load_key(a.keys, d.key_idx);
-            const uint64_t ctr = ((uint64_t)hdr.w << 32) | hdr.z;
-            const uint32_t n1 = hdr.z, n2 = hdr.w;
-            retire_loads(key, n1, n2, hdr, want);
-            for (uint32_t c = 0; c < min(kDmaDepth, C); ++c) stage_chunk(S, c, nb, 0u);
-            const Stream stm = make_stream(key, 0u, n1, n2);
-            uint32_t ks[16];
-            stream_block(stm, 0, ks);
-            const Mul r = make_mul(ks[0], ks[1], ks[2], ks[3]);
-            uint4 *pl = reinterpret_cast<uint4 *>(frame + 16);
-            const Acc h = pipe_pass_dma<true>(pl, stm, r, nb, hdr, make_ring(frame), S); // header unchanged
-            uint32_t tag[4];
-            pipe_tag(h, r, P, ks + 4, tag);
-            const uint32_t diff = (tag[0] ^ want.x) | (tag[1] ^ want.y) | (tag[2] ^ want.z) | (tag[3] ^ want.w);
-            if (__ballot(diff != 0)) { // wave-uniform: the ring stores of every lane first
-                __threadfence();
-                restore_forged(diff != 0, key, n1, n2, pl, 0, nb);
-            }
-            a.status[i] = diff == 0 ? RG_PKT_OK : RG_PKT_DECRYPT_ERR;
-            if (a.counters_out) a.counters_out[i] = ctr;
-            return;
-        }
-    }
     // Every load the lane needs is issued before the header is inspected, so
     // the header check costs no round trip of its own.  Loads stay
     // unconditional (exact waits): a frame that fails the descriptor checks
@@ -892,7 +625,7 @@ __device__ __forceinline__ void pipe_open_packet(const OpenArgs &a, uint32_t i, 
         // the buffer on Err, but the frame is left as it came), their chunks dealt over the wave's
         // lanes; with block stores other lanes wrote a lane's frame: every store completes and the
         // CU's cached lines go first
-        __threadfence();
+        wave_sync();
         restore_forged(diff != 0, key, n1, n2, pl, sg.c0, sg.nb);
     }
     if (j == 0) {
@@ -1021,24 +754,29 @@ __device__ __forceinline__ void pipe_walk(uint32_t n, uint32_t lg0, const PipePl
 }
 
 // flags: bits 0-1 log2 lanes per packet (without a plan), kPipeLinesFlag: the LDS ring is reserved
+__device__ __forceinline__ void pipe_stagger() {
+    if constexpr (RG_PIPE_STAGGER > 0)
+        for (uint32_t k = uniform_u32(threadIdx.x >> 6) * RG_PIPE_STAGGER; k > 0; --k) __builtin_amdgcn_s_sleep(1);
+}
+
 template <int MODE> __global__ __launch_bounds__(256) void pipe_seal_kernel(SealArgs a, uint32_t flags, PipePlan pp) {
+    pipe_stagger();
     const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
     uint64_t marks[2] = {0, 0};
     const bool lines = RG_PIPE_LINES && (flags & kPipeLinesFlag) != 0;
-    const bool dma = RG_PIPE_DMA && (flags & kPipeDmaFlag) != 0;
     pipe_walk(a.n, flags & 3u, pp, a.desc, a.dbg != nullptr, marks, [=](uint32_t i, const rg_pkt_desc &d, uint32_t j, uint32_t G) {
-        pipe_seal_packet<MODE>(a, i, d, j, G, lines, dma);
+        pipe_seal_packet<MODE>(a, i, d, j, G, lines);
     });
     if (a.dbg) pipe_stamp(a.dbg, t0, r0, marks);
 }
 
 __global__ __launch_bounds__(256) void pipe_open_kernel(OpenArgs a, uint32_t flags, PipePlan pp) {
+    pipe_stagger();
     const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
     uint64_t marks[2] = {0, 0};
     const bool lines = RG_PIPE_LINES && (flags & kPipeLinesFlag) != 0;
-    const bool dma = RG_PIPE_DMA && (flags & kPipeDmaFlag) != 0;
     pipe_walk(a.n, flags & 3u, pp, a.desc, a.dbg != nullptr, marks, [=](uint32_t i, const rg_pkt_desc &d, uint32_t j, uint32_t G) {
-        pipe_open_packet(a, i, d, j, G, lines, dma);
+        pipe_open_packet(a, i, d, j, G, lines);
     });
     if (a.dbg) pipe_stamp(a.dbg, t0, r0, marks);
 }
@@ -1068,8 +806,7 @@ hipError_t launch_pipe(const SealArgs *sa, const OpenArgs *oa, const Launch &L, 
     } else {
         pipe_grid((uint64_t)n << lg, L, blocks, lds);
     }
-    const uint32_t fl = lg | (lds >= 4 * kRingBytes ? kPipeLinesFlag : 0u) |
-                        (lds >= 4 * (kRingBytes + kStageBytes) ? kPipeDmaFlag : 0u);
+    const uint32_t fl = lg | (lds >= 4 * kRingBytes ? kPipeLinesFlag : 0u);
     if (sa && L.debug_mode == 1) hipLaunchKernelGGL(pipe_seal_kernel<1>, dim3(blocks), dim3(256), lds, s, *sa, fl, pp);
     else if (sa && L.debug_mode == 2) hipLaunchKernelGGL(pipe_seal_kernel<2>, dim3(blocks), dim3(256), lds, s, *sa, fl, pp);
     else if (sa && L.debug_mode == 4) hipLaunchKernelGGL(pipe_seal_kernel<4>, dim3(blocks), dim3(256), lds, s, *sa, fl, pp);

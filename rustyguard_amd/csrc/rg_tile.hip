@@ -724,7 +724,7 @@ __global__ __launch_bounds__(512) void tile_kernel(SealArgs sa, OpenArgs oa, Til
             if (__ballot(bad)) {
                 // the forged segments' chunks dealt over the wave's lanes (restore_forged): a lane re-XORs
                 // chunks another lane's window stores wrote, so those complete and this CU's L1 goes first
-                __threadfence();
+                wave_sync();
                 restore_forged(bad, key, n1, n2, reinterpret_cast<uint4 *>(frame + 16) + 4 * c0, c0, snb);
             }
         }
