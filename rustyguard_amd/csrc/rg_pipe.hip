@@ -21,6 +21,8 @@
 //    that block hides the first chunks' latency.
 // A partial last chunk (P % 64 != 0) runs after the loop with per-block
 // predicates; the last chunk's Poly1305 blocks are absorbed after it.
+#include <type_traits>
+
 #include "rg_device.h"
 #include "rg_internal.h"
 
@@ -70,6 +72,10 @@ __device__ __forceinline__ void load_chunk(Chunk &c, const uint4 *pl, uint32_t t
     c.q1 = ld16<NT>(pl + min(b + 1, last));
     c.q2 = ld16<NT>(pl + min(b + 2, last));
     c.q3 = ld16<NT>(pl + min(b + 3, last));
+}
+
+__device__ __forceinline__ uint4 sel4(bool c, const uint4 &a, const uint4 &b) {
+    return make_uint4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
 }
 
 __device__ __forceinline__ void absorb_chunk(Acc &h, const Chunk &c, const Mul &r, uint32_t cnt) {
@@ -191,16 +197,8 @@ __device__ __forceinline__ void ring_store(const Ring &R, const Ring4 &x, uint32
             asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(dst), "v"(x.v[q]) : "memory");
         else if constexpr (PIPE_WT == 2) // non-temporal (streaming) whole-line stores
             asm volatile("global_store_dwordx4 %0, %1, off nt\n\ts_nop 1" ::"v"(dst), "v"(x.v[q]) : "memory");
-        else if constexpr (PIPE_WT == 3) // plain stores pinned where they are issued (spread experiment)
-            asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" ::"v"(dst), "v"(x.v[q]) : "memory");
         else *dst = x.v[q];
     }
-}
-
-// store q of ring_store (the spread experiment): an asm store, so that it stays where it is issued
-__device__ __forceinline__ void ring_store_one(const Ring &R, const Ring4 &x, uint32_t k, uint32_t h, int q) {
-    glb_u4 *dst = (h ? R.fr[1][q] : R.fr[0][q]) + 8 * k;
-    asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" ::"v"(dst), "v"(x.v[q]) : "memory");
 }
 
 // One step: keystream block t+1 -- with the previous chunk's four Poly1305
@@ -223,20 +221,12 @@ __device__ __forceinline__ void ring_store_one(const Ring &R, const Ring4 &x, ui
 // LINES: the frame blocks go through the wave's LDS ring (block t goes into
 // the ring; with FLUSH, half t & 1 of line (t - 2) / 2 is read back before the
 // rounds and stored after them).
-// experiment: the step's four line stores issued one by one inside the keystream rounds (after double
-// rounds 2, 4, 6, 8) instead of back to back after them
-#ifndef RG_PIPE_SPREAD
-#define RG_PIPE_SPREAD 0
-#endif
-// experiment: wave w of a workgroup starts w * RG_PIPE_STAGGER x 64 cycles late, so that the four
-// waves of a CU (identical work, lockstep) do not issue their memory instructions at the same time
-#ifndef RG_PIPE_STAGGER
-#define RG_PIPE_STAGGER 0
-#endif
-template <bool OPEN, bool ABSORB, bool TAIL, int MODE = 0, bool LINES = false, bool FLUSH = false>
+// POLY = false (open with the tag verified first, RG_PIPE_MAC_FIRST): no Poly1305 in the rounds, and a
+// lane whose packet failed its tag (keep) writes its ciphertext back unchanged instead of the plaintext.
+template <bool OPEN, bool ABSORB, bool TAIL, int MODE = 0, bool LINES = false, bool FLUSH = false, bool POLY = true>
 __device__ __forceinline__ void pipe_step(uint4 *pl, const Stream &st, const Mul &r, Acc &h, Chunk &pi, Chunk &buf,
                                           uint4 &prev, bool &have_prev, uint32_t t, uint32_t nb, uint32_t c0,
-                                          const Ring &R) {
+                                          const Ring &R, bool keep = false) {
     uint32_t ks[16];
     static_assert(!FLUSH || (LINES && ABSORB && !TAIL), "flush steps");
     Ring4 fl;
@@ -249,10 +239,8 @@ __device__ __forceinline__ void pipe_step(uint4 *pl, const Stream &st, const Mul
         for (int i = 0; i < 16; ++i) ks[i] = t * 16 + i;
         h.h0 ^= pi.q0.x ^ pi.q1.y ^ pi.q2.z ^ pi.q3.w;
     } else stream_block_hooked(st, c0 + t + 1, ks, [&](int dr) {
-        if constexpr (FLUSH && RG_PIPE_SPREAD && MODE != 8) {
-            if (dr == 2 || dr == 4 || dr == 6 || dr == 8) ring_store_one(R, fl, (t - 2) >> 1, t & 1u, dr / 2 - 1);
-        }
-        if constexpr (OPEN && PIPE_OPEN_CUR) { // this chunk's ciphertext (TAIL: its nb % 4 blocks)
+        if constexpr (OPEN && !POLY) {
+        } else if constexpr (OPEN && PIPE_OPEN_CUR) { // this chunk's ciphertext (TAIL: its nb % 4 blocks)
             const uint32_t bl = TAIL ? nb & 3u : 4u;
             if (dr == 1) acc_block_pred(h, buf.q0, r, bl > 0);
             if (dr == 3) acc_block_pred(h, buf.q1, r, bl > 1);
@@ -267,7 +255,11 @@ __device__ __forceinline__ void pipe_step(uint4 *pl, const Stream &st, const Mul
             if (dr % 2 == 1) pin_acc(h);
         }
     });
-    const Chunk x = {xor4(buf.q0, ks + 0), xor4(buf.q1, ks + 4), xor4(buf.q2, ks + 8), xor4(buf.q3, ks + 12)};
+    Chunk x = {xor4(buf.q0, ks + 0), xor4(buf.q1, ks + 4), xor4(buf.q2, ks + 8), xor4(buf.q3, ks + 12)};
+    if constexpr (OPEN && !POLY) { // component-wise: a ternary on uint4 objects selects a pointer (scratch)
+        x.q0 = sel4(keep, buf.q0, x.q0); x.q1 = sel4(keep, buf.q1, x.q1);
+        x.q2 = sel4(keep, buf.q2, x.q2); x.q3 = sel4(keep, buf.q3, x.q3);
+    }
     uint4 *dst = pl + 4 * t;
     if constexpr (MODE == 1) {
         pi = x;
@@ -283,8 +275,7 @@ __device__ __forceinline__ void pipe_step(uint4 *pl, const Stream &st, const Mul
     }
     if constexpr (LINES && !TAIL) {
         ring_put(R, t, prev, x.q0, x.q1, x.q2); // prev: the header before the first chunk
-        if constexpr (FLUSH && !(RG_PIPE_SPREAD && MODE != 8))
-            ring_store(R, fl, MODE == 8 ? ((t - 2) >> 1) & 1u : (t - 2) >> 1, t & 1u);
+        if constexpr (FLUSH) ring_store(R, fl, MODE == 8 ? ((t - 2) >> 1) & 1u : (t - 2) >> 1, t & 1u);
         prev = x.q3;
         have_prev = true;
     } else if constexpr (TAIL) {
@@ -316,10 +307,10 @@ __device__ __forceinline__ void pipe_step(uint4 *pl, const Stream &st, const Mul
 // head / has_head: the DataHeader a seal writes in front of the payload (only
 // the lane whose segment starts the payload has one).
 // LINES (a wave of valid packets of one size, has_head set): blocks through the LDS ring.
-template <bool OPEN, int MODE = 0, bool LINES = false>
+template <bool OPEN, int MODE = 0, bool LINES = false, bool POLY = true>
 __device__ __forceinline__ Acc pipe_pass(uint4 *pl, const Stream &st, const Mul &r, uint32_t nb, uint32_t c0,
                                          Chunk &b0, Chunk &b1, Chunk &b2, Chunk &b3, uint4 head, bool has_head,
-                                         const Ring &R) {
+                                         const Ring &R, bool keep = false) {
     const uint32_t F = nb >> 2, bl = nb & 3u; // full chunks, blocks in the partial last chunk
     Acc h = {0, 0, 0, 0, 0};
     Chunk pi = {};
@@ -328,7 +319,7 @@ __device__ __forceinline__ Acc pipe_pass(uint4 *pl, const Stream &st, const Mul 
     uint32_t pending = 0; // blocks of pi not yet absorbed
     if constexpr (LINES) wave_sync(); // the previous packet's last read-back is done
     if (F > 0) {
-        pipe_step<OPEN, false, false, MODE, LINES>(pl, st, r, h, pi, b0, prev, have_prev, 0, nb, c0, R);
+        pipe_step<OPEN, false, false, MODE, LINES, false, POLY>(pl, st, r, h, pi, b0, prev, have_prev, 0, nb, c0, R, keep);
         uint32_t t = 1;
         // whole rounds of kDepth steps only: a step that may be skipped would
         // leave the waitcnt pass a path without its memory operations
@@ -336,25 +327,25 @@ __device__ __forceinline__ Acc pipe_pass(uint4 *pl, const Stream &st, const Mul 
         if constexpr (LINES) {
             static_assert(kDepth >= 3, "line stores: three or four chunk buffers");
             // step 1 has no complete line yet; steps 2.. each store half a line
-            if (F > 1) pipe_step<OPEN, true, false, MODE, true>(pl, st, r, h, pi, b1, prev, have_prev, 1, nb, c0, R);
+            if (F > 1) pipe_step<OPEN, true, false, MODE, true, false, POLY>(pl, st, r, h, pi, b1, prev, have_prev, 1, nb, c0, R, keep);
             if constexpr (kDepth == 4) {
                 for (t = 2; t + 3 < F; t += 4) {
-                    pipe_step<OPEN, true, false, MODE, true, true>(pl, st, r, h, pi, b2, prev, have_prev, t, nb, c0, R);
-                    pipe_step<OPEN, true, false, MODE, true, true>(pl, st, r, h, pi, b3, prev, have_prev, t + 1, nb, c0, R);
-                    pipe_step<OPEN, true, false, MODE, true, true>(pl, st, r, h, pi, b0, prev, have_prev, t + 2, nb, c0, R);
-                    pipe_step<OPEN, true, false, MODE, true, true>(pl, st, r, h, pi, b1, prev, have_prev, t + 3, nb, c0, R);
+                    pipe_step<OPEN, true, false, MODE, true, true, POLY>(pl, st, r, h, pi, b2, prev, have_prev, t, nb, c0, R, keep);
+                    pipe_step<OPEN, true, false, MODE, true, true, POLY>(pl, st, r, h, pi, b3, prev, have_prev, t + 1, nb, c0, R, keep);
+                    pipe_step<OPEN, true, false, MODE, true, true, POLY>(pl, st, r, h, pi, b0, prev, have_prev, t + 2, nb, c0, R, keep);
+                    pipe_step<OPEN, true, false, MODE, true, true, POLY>(pl, st, r, h, pi, b1, prev, have_prev, t + 3, nb, c0, R, keep);
                 }
-                if (t < F) pipe_step<OPEN, true, false, MODE, true, true>(pl, st, r, h, pi, b2, prev, have_prev, t, nb, c0, R);
-                if (t + 1 < F) pipe_step<OPEN, true, false, MODE, true, true>(pl, st, r, h, pi, b3, prev, have_prev, t + 1, nb, c0, R);
-                if (t + 2 < F) pipe_step<OPEN, true, false, MODE, true, true>(pl, st, r, h, pi, b0, prev, have_prev, t + 2, nb, c0, R);
+                if (t < F) pipe_step<OPEN, true, false, MODE, true, true, POLY>(pl, st, r, h, pi, b2, prev, have_prev, t, nb, c0, R, keep);
+                if (t + 1 < F) pipe_step<OPEN, true, false, MODE, true, true, POLY>(pl, st, r, h, pi, b3, prev, have_prev, t + 1, nb, c0, R, keep);
+                if (t + 2 < F) pipe_step<OPEN, true, false, MODE, true, true, POLY>(pl, st, r, h, pi, b0, prev, have_prev, t + 2, nb, c0, R, keep);
             } else {
             for (t = 2; t + 2 < F; t += 3) {
-                pipe_step<OPEN, true, false, MODE, true, true>(pl, st, r, h, pi, b2, prev, have_prev, t, nb, c0, R);
-                pipe_step<OPEN, true, false, MODE, true, true>(pl, st, r, h, pi, b0, prev, have_prev, t + 1, nb, c0, R);
-                pipe_step<OPEN, true, false, MODE, true, true>(pl, st, r, h, pi, b1, prev, have_prev, t + 2, nb, c0, R);
+                pipe_step<OPEN, true, false, MODE, true, true, POLY>(pl, st, r, h, pi, b2, prev, have_prev, t, nb, c0, R, keep);
+                pipe_step<OPEN, true, false, MODE, true, true, POLY>(pl, st, r, h, pi, b0, prev, have_prev, t + 1, nb, c0, R, keep);
+                pipe_step<OPEN, true, false, MODE, true, true, POLY>(pl, st, r, h, pi, b1, prev, have_prev, t + 2, nb, c0, R, keep);
             }
-            if (t < F) pipe_step<OPEN, true, false, MODE, true, true>(pl, st, r, h, pi, b2, prev, have_prev, t, nb, c0, R);
-            if (t + 1 < F) pipe_step<OPEN, true, false, MODE, true, true>(pl, st, r, h, pi, b0, prev, have_prev, t + 1, nb, c0, R);
+            if (t < F) pipe_step<OPEN, true, false, MODE, true, true, POLY>(pl, st, r, h, pi, b2, prev, have_prev, t, nb, c0, R, keep);
+            if (t + 1 < F) pipe_step<OPEN, true, false, MODE, true, true, POLY>(pl, st, r, h, pi, b0, prev, have_prev, t + 1, nb, c0, R, keep);
             }
             // the halves not stored yet: m = F - 2 .. 2 ceil(F / 2) - 1 (k = m / 2, h = m % 2); a
             // last line of one block stores its first four pieces only
@@ -363,28 +354,28 @@ __device__ __forceinline__ Acc pipe_pass(uint4 *pl, const Stream &st, const Mul 
                 ring_store<true>(R, ring_get(R, m >> 1, m & 1u), MODE == 8 ? (m >> 1) & 1u : m >> 1, m & 1u, F);
         } else if constexpr (kDepth == 4) {
             for (; t + 3 < F; t += 4) {
-                pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R);
-                pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b2, prev, have_prev, t + 1, nb, c0, R);
-                pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b3, prev, have_prev, t + 2, nb, c0, R);
-                pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b0, prev, have_prev, t + 3, nb, c0, R);
+                pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R, keep);
+                pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b2, prev, have_prev, t + 1, nb, c0, R, keep);
+                pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b3, prev, have_prev, t + 2, nb, c0, R, keep);
+                pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b0, prev, have_prev, t + 3, nb, c0, R, keep);
             }
-            if (t < F) pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R);
-            if (t + 1 < F) pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b2, prev, have_prev, t + 1, nb, c0, R);
-            if (t + 2 < F) pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b3, prev, have_prev, t + 2, nb, c0, R);
+            if (t < F) pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R, keep);
+            if (t + 1 < F) pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b2, prev, have_prev, t + 1, nb, c0, R, keep);
+            if (t + 2 < F) pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b3, prev, have_prev, t + 2, nb, c0, R, keep);
         } else if constexpr (kDepth == 3) {
             for (; t + 2 < F; t += 3) {
-                pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R);
-                pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b2, prev, have_prev, t + 1, nb, c0, R);
-                pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b0, prev, have_prev, t + 2, nb, c0, R);
+                pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R, keep);
+                pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b2, prev, have_prev, t + 1, nb, c0, R, keep);
+                pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b0, prev, have_prev, t + 2, nb, c0, R, keep);
             }
-            if (t < F) pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R);
-            if (t + 1 < F) pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b2, prev, have_prev, t + 1, nb, c0, R);
+            if (t < F) pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R, keep);
+            if (t + 1 < F) pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b2, prev, have_prev, t + 1, nb, c0, R, keep);
         } else {
             for (; t + 1 < F; t += 2) {
-                pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R);
-                pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b0, prev, have_prev, t + 1, nb, c0, R);
+                pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R, keep);
+                pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b0, prev, have_prev, t + 1, nb, c0, R, keep);
             }
-            if (t < F) pipe_step<OPEN, true, false, MODE>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R);
+            if (t < F) pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R, keep);
         }
         pending = 4;
     }
@@ -396,12 +387,12 @@ __device__ __forceinline__ Acc pipe_pass(uint4 *pl, const Stream &st, const Mul 
                     k == 1 ? b1.q1 : k == 2 ? b2.q1 : k == 3 ? b3.q1 : b0.q1,
                     k == 1 ? b1.q2 : k == 2 ? b2.q2 : k == 3 ? b3.q2 : b0.q2,
                     k == 1 ? b1.q3 : k == 2 ? b2.q3 : k == 3 ? b3.q3 : b0.q3};
-        if (F > 0) pipe_step<OPEN, true, true, MODE, LINES>(pl, st, r, h, pi, bp, prev, have_prev, F, nb, c0, R);
-        else pipe_step<OPEN, false, true, MODE, LINES>(pl, st, r, h, pi, bp, prev, have_prev, F, nb, c0, R);
+        if (F > 0) pipe_step<OPEN, true, true, MODE, LINES, false, POLY>(pl, st, r, h, pi, bp, prev, have_prev, F, nb, c0, R, keep);
+        else pipe_step<OPEN, false, true, MODE, LINES, false, POLY>(pl, st, r, h, pi, bp, prev, have_prev, F, nb, c0, R, keep);
         pending = bl;
     }
     if (have_prev && MODE != 1) st16<(MODE == 7 ? 4 : MODE >= 4 ? MODE - 3 : 0)>(pl + 4 * F - 1, prev);
-    if constexpr (!(OPEN && PIPE_OPEN_CUR)) absorb_chunk(h, pi, r, pending); // the last chunk's blocks
+    if constexpr (!(OPEN && (PIPE_OPEN_CUR || !POLY))) absorb_chunk(h, pi, r, pending); // the last chunk's blocks
     return h;
 }
 
@@ -554,6 +545,34 @@ __device__ __forceinline__ void pipe_seal_packet(const SealArgs &a, uint32_t i, 
 }
 
 // ------------------------------------------------------------------ open
+// RG_PIPE_MAC_FIRST 1: verify, then decrypt -- no unauthenticated plaintext ever in memory, a forged
+// packet costs what a clean one does -- but the Poly1305 pass alone runs latency-bound at one wave per
+// SIMD: config 2's open +12 % (profiles/r3_macfirst_ab.txt).  Default 0: decrypt while MACing and
+// restore forged frames (restore_forged).
+#ifndef RG_PIPE_MAC_FIRST
+#define RG_PIPE_MAC_FIRST 0
+#endif
+
+// Pass 1 of the open: the Horner chain over the segment's nb ciphertext blocks, chunk t absorbed while
+// chunks t+1, t+2 are loading (b0 / b1 / b2 hold chunks 0 / 1 / 2 on entry; chunk c lives in b(c % 3);
+// loads clamped inside the segment, unconditional).
+__device__ __forceinline__ Acc poly_pass(const uint4 *pl, const Mul &r, uint32_t nb, Chunk &b0, Chunk &b1, Chunk &b2) {
+    Acc h = {0, 0, 0, 0, 0};
+    const uint32_t C = (nb + 3) >> 2, last = nb ? nb - 1 : 0;
+    uint32_t t = 0;
+    for (; t + 3 <= C; t += 3) {
+        absorb_chunk(h, b0, r, chunk_blocks(nb, t));
+        load_chunk(b0, pl, t + 3, last);
+        absorb_chunk(h, b1, r, chunk_blocks(nb, t + 1));
+        load_chunk(b1, pl, t + 4, last);
+        absorb_chunk(h, b2, r, chunk_blocks(nb, t + 2));
+        load_chunk(b2, pl, t + 5, last);
+    }
+    if (t < C) absorb_chunk(h, b0, r, chunk_blocks(nb, t));
+    if (t + 1 < C) absorb_chunk(h, b1, r, chunk_blocks(nb, t + 1));
+    return h;
+}
+
 // desc.len = W.  Checks mirror rustyguard-core/src/lib.rs:613-629,
 // rustyguard-types/src/lib.rs:181-196 and rustyguard-crypto/src/prim.rs:
 // 427-429.  Decrypts speculatively while MACing the ciphertext; a failed tag
@@ -613,6 +632,31 @@ __device__ __forceinline__ void pipe_open_packet(const OpenArgs &a, uint32_t i, 
     uint32_t ks[16];
     stream_block(stm, 0, ks);
     const Mul r = make_mul(ks[0], ks[1], ks[2], ks[3]);
+#if RG_PIPE_MAC_FIRST
+    // verify, then decrypt (the order of an in-place AEAD open, prim.rs:190-201): pass 1 runs Poly1305
+    // over the ciphertext, pass 2 the keystream; a lane whose tag fails writes its ciphertext back
+    // unchanged in pass 2 (the line stores carry whole lines of eight frames), so a forged packet
+    // costs what a clean one does and no unauthenticated plaintext ever reaches memory
+    const Acc h1 = poly_pass(pl, r, sg.nb, b0, b1, b2);
+    // one instance per store mode, each with chunk buffers of its own (the two passes sharing buffers
+    // across the branch left them in scratch memory)
+    auto verify_decrypt = [&](auto lines_tag) -> uint32_t {
+        constexpr bool L = decltype(lines_tag)::value;
+        Chunk p0, p1, p2, p3 = {}; // pass 2's first chunks, in flight during the tag
+        load_chunk(p0, pl, 0, sg.nb ? sg.nb - 1 : 0);
+        load_chunk(p1, pl, 1, sg.nb ? sg.nb - 1 : 0);
+        load_chunk(p2, pl, 2, sg.nb ? sg.nb - 1 : 0);
+        const Acc h = combine_segments(h1, r, sg.after, G);
+        uint32_t tag[4];
+        pipe_tag(h, r, P, ks + 4, tag);
+        const uint32_t df = (tag[0] ^ want.x) | (tag[1] ^ want.y) | (tag[2] ^ want.z) | (tag[3] ^ want.w);
+        if constexpr (L) (void)pipe_pass<true, 0, true, false>(pl, stm, r, sg.nb, sg.c0, p0, p1, p2, p3, hdr, true, make_ring(frame), df != 0);
+        else (void)pipe_pass<true, 0, false, false>(pl, stm, r, sg.nb, sg.c0, p0, p1, p2, p3, make_uint4(0, 0, 0, 0), false, Ring{}, df != 0);
+        return df;
+    };
+    const uint32_t diff = lines ? verify_decrypt(std::true_type{}) : verify_decrypt(std::false_type{});
+    (void)key;
+#else
     Acc h;
     if (lines) h = pipe_pass<true, 0, true>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, b3, hdr, true, make_ring(frame)); // header unchanged
     else h = pipe_pass<true, 0, false>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, b3, make_uint4(0, 0, 0, 0), false, Ring{});
@@ -628,6 +672,7 @@ __device__ __forceinline__ void pipe_open_packet(const OpenArgs &a, uint32_t i, 
         wave_sync();
         restore_forged(diff != 0, key, n1, n2, pl, sg.c0, sg.nb);
     }
+#endif
     if (j == 0) {
         a.status[i] = diff == 0 ? RG_PKT_OK : RG_PKT_DECRYPT_ERR;
         if (a.counters_out) a.counters_out[i] = ctr;
@@ -754,13 +799,7 @@ __device__ __forceinline__ void pipe_walk(uint32_t n, uint32_t lg0, const PipePl
 }
 
 // flags: bits 0-1 log2 lanes per packet (without a plan), kPipeLinesFlag: the LDS ring is reserved
-__device__ __forceinline__ void pipe_stagger() {
-    if constexpr (RG_PIPE_STAGGER > 0)
-        for (uint32_t k = uniform_u32(threadIdx.x >> 6) * RG_PIPE_STAGGER; k > 0; --k) __builtin_amdgcn_s_sleep(1);
-}
-
 template <int MODE> __global__ __launch_bounds__(256) void pipe_seal_kernel(SealArgs a, uint32_t flags, PipePlan pp) {
-    pipe_stagger();
     const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
     uint64_t marks[2] = {0, 0};
     const bool lines = RG_PIPE_LINES && (flags & kPipeLinesFlag) != 0;
@@ -771,7 +810,6 @@ template <int MODE> __global__ __launch_bounds__(256) void pipe_seal_kernel(Seal
 }
 
 __global__ __launch_bounds__(256) void pipe_open_kernel(OpenArgs a, uint32_t flags, PipePlan pp) {
-    pipe_stagger();
     const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
     uint64_t marks[2] = {0, 0};
     const bool lines = RG_PIPE_LINES && (flags & kPipeLinesFlag) != 0;
