@@ -861,34 +861,64 @@ template <bool OPEN> __global__ __launch_bounds__(64 * kFlatWaves) void flat_ker
             }
             RG_FLAT_MARK(6);
             if constexpr (OPEN) {
-                // ---- forgeries: put the ciphertext back (plaintext ^ keystream)
+                // ---- forgeries: put the ciphertext back (plaintext ^ keystream), the forged packets'
+                // chunks dealt over the wave's 64 lanes (as restore_forged, rg_device.h): a wave pays
+                // ~chunks / 64 keystream blocks per forged packet, not the slowest lane's whole range.
+                // Every byte involved was stored by this wave (in-order: wavefront-scope ordering).
                 if (__ballot(any_fail)) {
                     wave_sync();
-                    if (s.nsteps) {
-                        FCur p;
-                        fcur_from(p, L.rec[kstart], buf, kstart, c_lo - L.rec[kstart].w);
-                        FKey q = fkey(L, p.k);
-                        Stream stm = make_stream(q.key, 0u, q.n1, q.n2);
-                        for (uint32_t j = 0; j < s.nsteps; ++j) {
-                            if (L.hs[p.k][6] == kFail) {
-                                // the chunk's loads (clamped inside the payload) before its keystream block
-                                uint4 *w = const_cast<uint4 *>(p.pl) + 4 * p.t;
-                                const uint32_t c = min(4u, p.nb - 4 * p.t);
-                                uint4 m[4];
+                    uint32_t cn[kFlatMaxPk / 64];
+                    uint64_t fmask[kFlatMaxPk / 64];
 #pragma unroll
-                                for (uint32_t b = 0; b < 4; ++b) m[b] = w[b < c ? b : c - 1];
-                                uint32_t ks[16];
-                                stream_block(stm, p.t + 1, ks);
+                    for (uint32_t q = 0; q < kFlatMaxPk / 64; ++q) {
+                        const uint32_t k = lane + 64 * q;
+                        const bool f = k < m && L.hs[k][6] == kFail;
+                        cn[q] = f ? ((L.rec[k].z & ~kLiveBit) + 3) >> 2 : 0u;
+                        fmask[q] = __ballot(f && cn[q] > 0);
+                    }
+                    int own = -1;
+                    uint32_t oc = 0, pos = 0;
+                    auto round = [&]() {
+                        if (own >= 0) {
+                            const uint4 rc = L.rec[own];
+                            const FKey fk = fkey(L, (uint32_t)own);
+                            const uint32_t onb = rc.z & ~kLiveBit, b0 = 4 * oc, last = onb - 1;
+                            uint4 *p = reinterpret_cast<uint4 *>(buf + (((uint64_t)rc.y << 32) | rc.x) + 16) + b0;
+                            const uint4 m0 = p[min(b0, last) - b0], m1 = p[min(b0 + 1, last) - b0];
+                            const uint4 m2 = p[min(b0 + 2, last) - b0], m3 = p[min(b0 + 3, last) - b0];
+                            const Stream stm = make_stream(fk.key, 0u, fk.n1, fk.n2);
+                            uint32_t ks[16];
+                            stream_block(stm, oc + 1, ks);
+                            if (b0 < onb) p[0] = xor4(m0, ks + 0);
+                            if (b0 + 1 < onb) p[1] = xor4(m1, ks + 4);
+                            if (b0 + 2 < onb) p[2] = xor4(m2, ks + 8);
+                            if (b0 + 3 < onb) p[3] = xor4(m3, ks + 12);
+                        }
+                        own = -1;
+                    };
 #pragma unroll
-                                for (uint32_t b = 0; b < 4; ++b)
-                                    if (b < c) w[b] = xor4(m[b], ks + 4 * b);
-                            }
-                            if (fcur_next(p, L, buf, m) && p.k < m) {
-                                q = fkey(L, p.k);
-                                stm = make_stream(q.key, 0u, q.n1, q.n2);
+                    for (uint32_t q = 0; q < kFlatMaxPk / 64; ++q) {
+                        uint64_t fm = fmask[q];
+                        while (fm) {
+                            const uint32_t f = (uint32_t)__ffsll((unsigned long long)fm) - 1;
+                            fm &= fm - 1;
+                            const uint32_t Cf = (uint32_t)__builtin_amdgcn_readlane((int)cn[q], (int)f);
+                            for (uint32_t done = 0; done < Cf;) {
+                                const uint32_t take = min(Cf - done, 64u - pos);
+                                if (lane >= pos && lane < pos + take) {
+                                    own = (int)(64 * q + f);
+                                    oc = done + lane - pos;
+                                }
+                                pos += take;
+                                done += take;
+                                if (pos == 64) {
+                                    round();
+                                    pos = 0;
+                                }
                             }
                         }
                     }
+                    if (pos > 0) round();
                 }
             }
             wave_sync(); // the next sub-unit overwrites the LDS image
