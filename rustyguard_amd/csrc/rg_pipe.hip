@@ -120,6 +120,10 @@ constexpr bool PIPE_LOAD_FIRST = RG_PIPE_LOAD_FIRST != 0;
 #ifndef RG_PIPE_WT
 #define RG_PIPE_WT 0
 #endif
+// diagnostics only (tools/build_variant.sh): 1 = line stores dropped, 2 = LDS ring dropped
+#ifndef RG_PIPE_ABL
+#define RG_PIPE_ABL 0
+#endif
 constexpr int PIPE_WT = RG_PIPE_WT;
 constexpr uint32_t kPipeLinesFlag = 4u;      // launch flag bit (bits 0-1: log2 lanes per packet)
 constexpr uint32_t kRingBytes = 64u * 256u; // per wave
@@ -201,6 +205,27 @@ __device__ __forceinline__ void ring_store(const Ring &R, const Ring4 &x, uint32
     }
 }
 
+// Diagnostic build only (RG_PIPE_WSTAMP, tools/wstamps.py): per wave, cycles of the line-store steps
+// by their place in the unrolled loop (t % 3), to price the waits hipcc puts in each, and (seal) the
+// cycles in an explicit vmcnt(16) before the XOR (exact for chunk t in steady state).  Each stamp
+// costs ~40 cycles and forbids overlap across it: read the shares, not the run time.
+#ifdef RG_PIPE_WSTAMP
+__device__ __forceinline__ uint64_t wst_now() {
+    uint64_t t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#define RG_WST(x) x
+// this wave's accumulators: slots 1-3 of its stamp record (pipe_stamp leaves them alone)
+__device__ __forceinline__ uint64_t *wst_slot(uint64_t *dbg) {
+    return dbg ? dbg + 8ull * (blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64) + 1 : nullptr;
+}
+#else
+#define RG_WST(x)
+#endif
+
 // One step: keystream block t+1 -- with the previous chunk's four Poly1305
 // blocks (pi, always a full chunk) absorbed in its rounds when ABSORB -- XORed
 // into chunk t (buf) and stored; then chunk t+kDepth is requested into buf.  Full
@@ -226,13 +251,18 @@ __device__ __forceinline__ void ring_store(const Ring &R, const Ring4 &x, uint32
 template <bool OPEN, bool ABSORB, bool TAIL, int MODE = 0, bool LINES = false, bool FLUSH = false, bool POLY = true>
 __device__ __forceinline__ void pipe_step(uint4 *pl, const Stream &st, const Mul &r, Acc &h, Chunk &pi, Chunk &buf,
                                           uint4 &prev, bool &have_prev, uint32_t t, uint32_t nb, uint32_t c0,
-                                          const Ring &R, bool keep = false) {
+                                          const Ring &R, bool keep = false, uint64_t *wacc = nullptr) {
     uint32_t ks[16];
     static_assert(!FLUSH || (LINES && ABSORB && !TAIL), "flush steps");
     Ring4 fl;
+    RG_WST(uint64_t w_t0 = 0; if constexpr (FLUSH) w_t0 = wst_now();)
     if constexpr (FLUSH) {
         wave_sync(); // block t - 1 was put by every lane
+#if RG_PIPE_ABL == 2 // diagnostics only: no ring (the line stores write this lane's registers; output invalid)
+        fl.v[0] = to_v4(buf.q0); fl.v[1] = to_v4(buf.q1); fl.v[2] = to_v4(buf.q2); fl.v[3] = to_v4(buf.q3);
+#else
         fl = ring_get(R, (t - 2) >> 1, t & 1u);
+#endif
     }
     if constexpr (MODE == 2) {
 #pragma unroll
@@ -255,6 +285,7 @@ __device__ __forceinline__ void pipe_step(uint4 *pl, const Stream &st, const Mul
             if (dr % 2 == 1) pin_acc(h);
         }
     });
+    RG_WST(if constexpr (FLUSH && !OPEN) { const uint64_t a_ = wst_now(); asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); wacc[3 + t % 3] += wst_now() - a_; })
     Chunk x = {xor4(buf.q0, ks + 0), xor4(buf.q1, ks + 4), xor4(buf.q2, ks + 8), xor4(buf.q3, ks + 12)};
     if constexpr (OPEN && !POLY) { // component-wise: a ternary on uint4 objects selects a pointer (scratch)
         x.q0 = sel4(keep, buf.q0, x.q0); x.q1 = sel4(keep, buf.q1, x.q1);
@@ -274,8 +305,16 @@ __device__ __forceinline__ void pipe_step(uint4 *pl, const Stream &st, const Mul
         load_chunk<NT>(buf, pl, t + kDepth, nb - 1);
     }
     if constexpr (LINES && !TAIL) {
+#if RG_PIPE_ABL == 2
+        asm volatile("" ::"v"(prev.x), "v"(x.q0.x), "v"(x.q1.x), "v"(x.q2.x));
+#else
         ring_put(R, t, prev, x.q0, x.q1, x.q2); // prev: the header before the first chunk
+#endif
+#if RG_PIPE_ABL == 1 // diagnostics only: the ring is read back but its lines are not stored (output invalid)
+        if constexpr (FLUSH) asm volatile("" ::"v"(fl.v[0]), "v"(fl.v[1]), "v"(fl.v[2]), "v"(fl.v[3]));
+#else
         if constexpr (FLUSH) ring_store(R, fl, MODE == 8 ? ((t - 2) >> 1) & 1u : (t - 2) >> 1, t & 1u);
+#endif
         prev = x.q3;
         have_prev = true;
     } else if constexpr (TAIL) {
@@ -296,7 +335,19 @@ __device__ __forceinline__ void pipe_step(uint4 *pl, const Stream &st, const Mul
     }
     if constexpr (PIPE_LOAD_FIRST && !TAIL) return;
     if constexpr (!(OPEN && PIPE_OPEN_CUR)) pi = OPEN ? buf : x;
+#if RG_PIPE_PAD
+    if constexpr (LINES && !FLUSH && !TAIL) {
+        // the two steps before the loop store no line: four loads stand in for the four line stores,
+        // so that the waitcnt pass sees as many operations behind each chunk's loads on the path into
+        // the loop as on its back edge (else it keeps the entry path's shorter counts for every pass)
+        const volatile uint32_t *hp = reinterpret_cast<const volatile uint32_t *>(pl) - 4;
+        uint32_t sink = 0;
+        for (int k = 0; k < 4; ++k) sink += hp[k];
+        asm volatile("" ::"v"(sink));
+    }
+#endif
     if constexpr (!TAIL) load_chunk<NT>(buf, pl, t + kDepth, nb - 1);
+    RG_WST(if constexpr (FLUSH) wacc[t % 3] += wst_now() - w_t0;)
 }
 
 // Keystream XOR in place + Poly1305 over the ciphertext of nb 16-byte blocks
@@ -310,8 +361,10 @@ __device__ __forceinline__ void pipe_step(uint4 *pl, const Stream &st, const Mul
 template <bool OPEN, int MODE = 0, bool LINES = false, bool POLY = true>
 __device__ __forceinline__ Acc pipe_pass(uint4 *pl, const Stream &st, const Mul &r, uint32_t nb, uint32_t c0,
                                          Chunk &b0, Chunk &b1, Chunk &b2, Chunk &b3, uint4 head, bool has_head,
-                                         const Ring &R, bool keep = false) {
+                                         const Ring &R, bool keep = false, uint64_t *wst = nullptr) {
     const uint32_t F = nb >> 2, bl = nb & 3u; // full chunks, blocks in the partial last chunk
+    uint64_t wacc[6] = {0, 0, 0, 0, 0, 0};
+    (void)wst;
     Acc h = {0, 0, 0, 0, 0};
     Chunk pi = {};
     uint4 prev = head; // block still to be stored just in front of the current chunk
@@ -319,7 +372,7 @@ __device__ __forceinline__ Acc pipe_pass(uint4 *pl, const Stream &st, const Mul 
     uint32_t pending = 0; // blocks of pi not yet absorbed
     if constexpr (LINES) wave_sync(); // the previous packet's last read-back is done
     if (F > 0) {
-        pipe_step<OPEN, false, false, MODE, LINES, false, POLY>(pl, st, r, h, pi, b0, prev, have_prev, 0, nb, c0, R, keep);
+        pipe_step<OPEN, false, false, MODE, LINES, false, POLY>(pl, st, r, h, pi, b0, prev, have_prev, 0, nb, c0, R, keep, wacc);
         uint32_t t = 1;
         // whole rounds of kDepth steps only: a step that may be skipped would
         // leave the waitcnt pass a path without its memory operations
@@ -327,25 +380,25 @@ __device__ __forceinline__ Acc pipe_pass(uint4 *pl, const Stream &st, const Mul 
         if constexpr (LINES) {
             static_assert(kDepth >= 3, "line stores: three or four chunk buffers");
             // step 1 has no complete line yet; steps 2.. each store half a line
-            if (F > 1) pipe_step<OPEN, true, false, MODE, true, false, POLY>(pl, st, r, h, pi, b1, prev, have_prev, 1, nb, c0, R, keep);
+            if (F > 1) pipe_step<OPEN, true, false, MODE, true, false, POLY>(pl, st, r, h, pi, b1, prev, have_prev, 1, nb, c0, R, keep, wacc);
             if constexpr (kDepth == 4) {
                 for (t = 2; t + 3 < F; t += 4) {
-                    pipe_step<OPEN, true, false, MODE, true, true, POLY>(pl, st, r, h, pi, b2, prev, have_prev, t, nb, c0, R, keep);
-                    pipe_step<OPEN, true, false, MODE, true, true, POLY>(pl, st, r, h, pi, b3, prev, have_prev, t + 1, nb, c0, R, keep);
-                    pipe_step<OPEN, true, false, MODE, true, true, POLY>(pl, st, r, h, pi, b0, prev, have_prev, t + 2, nb, c0, R, keep);
-                    pipe_step<OPEN, true, false, MODE, true, true, POLY>(pl, st, r, h, pi, b1, prev, have_prev, t + 3, nb, c0, R, keep);
+                    pipe_step<OPEN, true, false, MODE, true, true, POLY>(pl, st, r, h, pi, b2, prev, have_prev, t, nb, c0, R, keep, wacc);
+                    pipe_step<OPEN, true, false, MODE, true, true, POLY>(pl, st, r, h, pi, b3, prev, have_prev, t + 1, nb, c0, R, keep, wacc);
+                    pipe_step<OPEN, true, false, MODE, true, true, POLY>(pl, st, r, h, pi, b0, prev, have_prev, t + 2, nb, c0, R, keep, wacc);
+                    pipe_step<OPEN, true, false, MODE, true, true, POLY>(pl, st, r, h, pi, b1, prev, have_prev, t + 3, nb, c0, R, keep, wacc);
                 }
-                if (t < F) pipe_step<OPEN, true, false, MODE, true, true, POLY>(pl, st, r, h, pi, b2, prev, have_prev, t, nb, c0, R, keep);
-                if (t + 1 < F) pipe_step<OPEN, true, false, MODE, true, true, POLY>(pl, st, r, h, pi, b3, prev, have_prev, t + 1, nb, c0, R, keep);
-                if (t + 2 < F) pipe_step<OPEN, true, false, MODE, true, true, POLY>(pl, st, r, h, pi, b0, prev, have_prev, t + 2, nb, c0, R, keep);
+                if (t < F) pipe_step<OPEN, true, false, MODE, true, true, POLY>(pl, st, r, h, pi, b2, prev, have_prev, t, nb, c0, R, keep, wacc);
+                if (t + 1 < F) pipe_step<OPEN, true, false, MODE, true, true, POLY>(pl, st, r, h, pi, b3, prev, have_prev, t + 1, nb, c0, R, keep, wacc);
+                if (t + 2 < F) pipe_step<OPEN, true, false, MODE, true, true, POLY>(pl, st, r, h, pi, b0, prev, have_prev, t + 2, nb, c0, R, keep, wacc);
             } else {
             for (t = 2; t + 2 < F; t += 3) {
-                pipe_step<OPEN, true, false, MODE, true, true, POLY>(pl, st, r, h, pi, b2, prev, have_prev, t, nb, c0, R, keep);
-                pipe_step<OPEN, true, false, MODE, true, true, POLY>(pl, st, r, h, pi, b0, prev, have_prev, t + 1, nb, c0, R, keep);
-                pipe_step<OPEN, true, false, MODE, true, true, POLY>(pl, st, r, h, pi, b1, prev, have_prev, t + 2, nb, c0, R, keep);
+                pipe_step<OPEN, true, false, MODE, true, true, POLY>(pl, st, r, h, pi, b2, prev, have_prev, t, nb, c0, R, keep, wacc);
+                pipe_step<OPEN, true, false, MODE, true, true, POLY>(pl, st, r, h, pi, b0, prev, have_prev, t + 1, nb, c0, R, keep, wacc);
+                pipe_step<OPEN, true, false, MODE, true, true, POLY>(pl, st, r, h, pi, b1, prev, have_prev, t + 2, nb, c0, R, keep, wacc);
             }
-            if (t < F) pipe_step<OPEN, true, false, MODE, true, true, POLY>(pl, st, r, h, pi, b2, prev, have_prev, t, nb, c0, R, keep);
-            if (t + 1 < F) pipe_step<OPEN, true, false, MODE, true, true, POLY>(pl, st, r, h, pi, b0, prev, have_prev, t + 1, nb, c0, R, keep);
+            if (t < F) pipe_step<OPEN, true, false, MODE, true, true, POLY>(pl, st, r, h, pi, b2, prev, have_prev, t, nb, c0, R, keep, wacc);
+            if (t + 1 < F) pipe_step<OPEN, true, false, MODE, true, true, POLY>(pl, st, r, h, pi, b0, prev, have_prev, t + 1, nb, c0, R, keep, wacc);
             }
             // the halves not stored yet: m = F - 2 .. 2 ceil(F / 2) - 1 (k = m / 2, h = m % 2); a
             // last line of one block stores its first four pieces only
@@ -354,28 +407,28 @@ __device__ __forceinline__ Acc pipe_pass(uint4 *pl, const Stream &st, const Mul 
                 ring_store<true>(R, ring_get(R, m >> 1, m & 1u), MODE == 8 ? (m >> 1) & 1u : m >> 1, m & 1u, F);
         } else if constexpr (kDepth == 4) {
             for (; t + 3 < F; t += 4) {
-                pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R, keep);
-                pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b2, prev, have_prev, t + 1, nb, c0, R, keep);
-                pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b3, prev, have_prev, t + 2, nb, c0, R, keep);
-                pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b0, prev, have_prev, t + 3, nb, c0, R, keep);
+                pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R, keep, wacc);
+                pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b2, prev, have_prev, t + 1, nb, c0, R, keep, wacc);
+                pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b3, prev, have_prev, t + 2, nb, c0, R, keep, wacc);
+                pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b0, prev, have_prev, t + 3, nb, c0, R, keep, wacc);
             }
-            if (t < F) pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R, keep);
-            if (t + 1 < F) pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b2, prev, have_prev, t + 1, nb, c0, R, keep);
-            if (t + 2 < F) pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b3, prev, have_prev, t + 2, nb, c0, R, keep);
+            if (t < F) pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R, keep, wacc);
+            if (t + 1 < F) pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b2, prev, have_prev, t + 1, nb, c0, R, keep, wacc);
+            if (t + 2 < F) pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b3, prev, have_prev, t + 2, nb, c0, R, keep, wacc);
         } else if constexpr (kDepth == 3) {
             for (; t + 2 < F; t += 3) {
-                pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R, keep);
-                pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b2, prev, have_prev, t + 1, nb, c0, R, keep);
-                pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b0, prev, have_prev, t + 2, nb, c0, R, keep);
+                pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R, keep, wacc);
+                pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b2, prev, have_prev, t + 1, nb, c0, R, keep, wacc);
+                pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b0, prev, have_prev, t + 2, nb, c0, R, keep, wacc);
             }
-            if (t < F) pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R, keep);
-            if (t + 1 < F) pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b2, prev, have_prev, t + 1, nb, c0, R, keep);
+            if (t < F) pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R, keep, wacc);
+            if (t + 1 < F) pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b2, prev, have_prev, t + 1, nb, c0, R, keep, wacc);
         } else {
             for (; t + 1 < F; t += 2) {
-                pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R, keep);
-                pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b0, prev, have_prev, t + 1, nb, c0, R, keep);
+                pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R, keep, wacc);
+                pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b0, prev, have_prev, t + 1, nb, c0, R, keep, wacc);
             }
-            if (t < F) pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R, keep);
+            if (t < F) pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R, keep, wacc);
         }
         pending = 4;
     }
@@ -387,12 +440,13 @@ __device__ __forceinline__ Acc pipe_pass(uint4 *pl, const Stream &st, const Mul 
                     k == 1 ? b1.q1 : k == 2 ? b2.q1 : k == 3 ? b3.q1 : b0.q1,
                     k == 1 ? b1.q2 : k == 2 ? b2.q2 : k == 3 ? b3.q2 : b0.q2,
                     k == 1 ? b1.q3 : k == 2 ? b2.q3 : k == 3 ? b3.q3 : b0.q3};
-        if (F > 0) pipe_step<OPEN, true, true, MODE, LINES, false, POLY>(pl, st, r, h, pi, bp, prev, have_prev, F, nb, c0, R, keep);
-        else pipe_step<OPEN, false, true, MODE, LINES, false, POLY>(pl, st, r, h, pi, bp, prev, have_prev, F, nb, c0, R, keep);
+        if (F > 0) pipe_step<OPEN, true, true, MODE, LINES, false, POLY>(pl, st, r, h, pi, bp, prev, have_prev, F, nb, c0, R, keep, wacc);
+        else pipe_step<OPEN, false, true, MODE, LINES, false, POLY>(pl, st, r, h, pi, bp, prev, have_prev, F, nb, c0, R, keep, wacc);
         pending = bl;
     }
     if (have_prev && MODE != 1) st16<(MODE == 7 ? 4 : MODE >= 4 ? MODE - 3 : 0)>(pl + 4 * F - 1, prev);
     if constexpr (!(OPEN && (PIPE_OPEN_CUR || !POLY))) absorb_chunk(h, pi, r, pending); // the last chunk's blocks
+    RG_WST(if (wst && (threadIdx.x & 63) == 0) for (int k = 0; k < 6; ++k) atomicAdd((unsigned long long *)&wst[k < 3 ? k : 8ull * gridDim.x * (blockDim.x / 64) + k - 4], (unsigned long long)wacc[k]);)
     return h;
 }
 
@@ -530,7 +584,11 @@ __device__ __forceinline__ void pipe_seal_packet(const SealArgs &a, uint32_t i, 
     Acc h;
     if (lines) { // wave-uniform
         if (!head) hdr = *reinterpret_cast<const uint4 *>(frame); // block 0 is stored whole: header unchanged
+#ifdef RG_PIPE_WSTAMP
+        h = pipe_pass<false, MODE, true>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, b3, hdr, true, make_ring(frame), false, wst_slot(a.dbg));
+#else
         h = pipe_pass<false, MODE, true>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, b3, hdr, true, make_ring(frame));
+#endif
     } else {
         h = pipe_pass<false, MODE, false>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, b3, hdr, head, Ring{});
     }
@@ -658,7 +716,11 @@ __device__ __forceinline__ void pipe_open_packet(const OpenArgs &a, uint32_t i, 
     (void)key;
 #else
     Acc h;
+#ifdef RG_PIPE_WSTAMP
+    if (lines) h = pipe_pass<true, 0, true>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, b3, hdr, true, make_ring(frame), false, wst_slot(a.dbg));
+#else
     if (lines) h = pipe_pass<true, 0, true>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, b3, hdr, true, make_ring(frame)); // header unchanged
+#endif
     else h = pipe_pass<true, 0, false>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, b3, make_uint4(0, 0, 0, 0), false, Ring{});
     h = combine_segments(h, r, sg.after, G);
     uint32_t tag[4];
@@ -690,7 +752,11 @@ __device__ __forceinline__ void pipe_stamp(uint64_t *dbg, uint64_t t0, uint64_t 
     const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
     if ((threadIdx.x & 63) == 0) {
         uint64_t *o = dbg + 8ull * (blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64);
-#ifndef RG_TILE_MARKS
+#if defined(RG_PIPE_WSTAMP)
+        o[0] = t1 - t0; // slots 1-3: the wait-stamp accumulators
+        o[5] = 5;
+        (void)marks;
+#elif !defined(RG_TILE_MARKS)
         o[0] = t1 - t0; o[1] = marks[0] ? marks[0] - r0 : 0; o[2] = marks[1] ? marks[1] - r0 : 0; o[3] = 0;
         o[5] = 4;
 #else
