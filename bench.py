@@ -80,8 +80,8 @@ def parse():
     ap.add_argument("--e2e", action="store_true", help="also time the pinned host->GPU->host path")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch/validate the ranks, print each rank's plan as JSON and exit before any GPU work")
-    ap.add_argument("--forged", type=float, default=0.0,
-                    help="also time the open with this fraction of forged tags (0 = skip)")
+    ap.add_argument("--forged", default="0.01,0.1",
+                    help="also time the open with these fractions of forged tags, comma-separated (0 = skip)")
     ap.add_argument("--no-cold", dest="cold", action="store_false",
                     help="skip the cold-cache pass (profiling runs: keeps per-kernel averages to the step's regime)")
     ap.add_argument("--no-verify", dest="verify", action="store_false",
@@ -332,6 +332,14 @@ def forged_open_timing(w, b, stream, frac: float, verify: bool):
             "how": "median of 5 event-timed opens enqueued behind a spin kernel, clean and forged batches alike"}
 
 
+def forged_fracs(spec: str) -> list:
+    """--forged: comma-separated fractions in (0, 1]; 0 or empty = no forged-open legs."""
+    out = [float(x) for x in str(spec).split(",") if x.strip()]
+    if any(f < 0 or f > 1 for f in out):
+        raise SystemExit(f"bench.py: --forged fractions must lie in [0, 1], got {spec!r}")
+    return [f for f in out if f > 0]
+
+
 def hbm_copy_rate(stream, nbytes: int = 1 << 30, reps: int = 5):
     """Achievable HBM bandwidth on this GPU for comparison with the 8 TB/s spec peak: a device-to-device
     copy of a 1 GiB buffer (4x the Infinity Cache, so it streams from HBM), (read + written bytes) /
@@ -513,6 +521,7 @@ def main():
                 "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "workload": workload}
         if world > 1:
             plan["legs"] = run_legs(plan["rank"], world, workload, args)
+        plan["forged"] = forged_fracs(args.forged)  # forged-open legs after the timed region
         line = json.dumps(plan) + "\n"
         os.write(1, line.encode())  # one write: ranks sharing the pipe never interleave a line
         return
@@ -652,7 +661,7 @@ def main():
     if args.verify:
         assert (b.status[: w.n] == 0).all().item(), "open failed in the kernel-timing pass"
     cold = cold_cache_timing(eng, w, b, stream, args.verify) if args.cold and w.buf_bytes < MALL_BYTES else None
-    forged = forged_open_timing(w, b, stream, args.forged, args.verify) if args.forged > 0 else None
+    forged = [forged_open_timing(w, b, stream, f, args.verify) for f in forged_fracs(args.forged)] or None
     copy_ceiling = hbm_copy_rate(stream) if rank == 0 else None
     if args.verify:
         strict_check(w, b, stream)

@@ -180,9 +180,10 @@ int rg_last_kernel(rg_ctx *ctx);
  * auto: plan unless the last planned batch of this context held a single size
  * class (re-checked every 32nd call).  Results are identical in every mode.
  * Device-API calls that share a context use one set of planner buffers and one
- * tile-kernel work pool (batches of two or more deal rounds, ~260 Ki packets on
- * 256 CUs, even with the planner off): issue them on one stream (or order them) --
- * the host-memory API has its own per pipeline stream. */
+ * tile-kernel work pool (batches of eight or more deal rounds, CUs x 4 Ki packets =
+ * 1 Mi on 256 CUs, even with the planner off): two device-API launches on one
+ * context on different streams are unsupported at any batch size -- issue them on
+ * one stream (or order them).  The host-memory API has its own per pipeline stream. */
 int rg_set_plan(rg_ctx *ctx, int on);
 /* Segments per packet for the tile kernels: 0 (default) = per size class,
  * aiming at two resident waves per SIMD; 1/2/4 = split every packet into that
@@ -302,7 +303,11 @@ int rg_recv_batch_ex(rg_sessions *s, const rg_pkt_desc *desc, size_t n, uint8_t 
  * Sessions take it as started / sent when inserted; rg_send_batch sets sent and rejects
  * once started + REJECT_AFTER_TIME (180 s) < now (should_expire, lib.rs:207-209). */
 void rg_sessions_set_time(rg_sessions *s, uint64_t now_ns);
-/* the endpoint tag of the session's last authenticated packet; RG_ENOTFOUND before any */
+/* the endpoint tag of the session's last authenticated packet; RG_ENOTFOUND before any.
+ * Kept per session slot, whereas the reference keeps it per peer (peer.endpoint,
+ * rustyguard-core/src/lib.rs:670-671, read by the Keepalive timer, time.rs:135): after a rekey
+ * the new slot has no endpoint until its own first authenticated packet, so a caller with
+ * several sessions per peer carries the endpoint per peer itself (the latest of its slots). */
 int rg_sessions_endpoint(const rg_sessions *s, uint32_t slot, uint64_t *src_out);
 /* the Keepalive timer entry (rustyguard-core/src/time.rs:114-141): clears keepalive_pending
  * and returns 1 when sent + KEEPALIVE_TIMEOUT < now (should_keepalive, lib.rs:201-203): the

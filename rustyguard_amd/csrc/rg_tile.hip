@@ -168,7 +168,7 @@ constexpr uint32_t kMinSegment = 4;
 #define RG_TILE_POOL 1
 #endif
 #ifndef RG_TILE_POOL_MIN
-#define RG_TILE_POOL_MIN 2 // deal rounds from which the grid-wide pool is used
+#define RG_TILE_POOL_MIN 8 // deal rounds from which the grid-wide pool is used (the measured regime)
 #endif
 #ifndef RG_TILE_POOL_AHEAD
 #define RG_TILE_POOL_AHEAD 1 // pool items requested one tile ahead
@@ -282,11 +282,12 @@ __global__ __launch_bounds__(512) void tile_kernel(SealArgs sa, OpenArgs oa, Til
     const uint32_t my_slot = half == 0 ? blockIdx.x : S - 1 - blockIdx.x;
     const uint32_t rounds = (sc.total_groups + S - 1) / S;
     const bool dyn = RG_TILE_DYN && halves == 2 && __ballot(sc.K > 1) == 0; // same in every wave
-    // From two deal rounds on, the last eighth of them (at least one) goes to a pool shared by the whole
+    // From eight deal rounds on, the last eighth of them goes to a pool shared by the whole
     // grid: the XCDs do not run at one rate (per-CU finish times at config 4 spread by 8 %, by XCD), so
     // the workgroups that run out of their own tiles first take these, one tile per device-scope atomic
     // on tp.gq[0], requested one tile ahead.  Measured: config 5 on one GPU (64 rounds) +1.5 %, config 4
-    // (8 rounds) +0.7 % (with each draw waited for on the spot, config 4 lost 1 %).
+    // (8 rounds) +0.7 % (with each draw waited for on the spot, config 4 lost 1 %).  Below eight rounds
+    // (unmeasured: one pooled round would be half or a third of the tiles) every tile stays local.
     const uint32_t R = (RG_TILE_POOL && dyn && tp.gq && rounds >= RG_TILE_POOL_MIN) ? max(1u, rounds / 8) : 0u;
     const uint32_t rounds_local = rounds - R;
     const uint32_t pool = R ? (sc.total_groups - rounds_local * S) * 4u : 0u; // tiles in the global pool

@@ -35,7 +35,13 @@ def test_single_gpu_defaults_to_cfg2():
     r = _run(["--dry-run"])
     assert r.returncode == 0, r.stderr[-2000:]
     (line,) = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
-    assert line == {"rank": 0, "world": 1, "gpus": 1, "local_rank": 0, "workload": "cfg2"}
+    # the default line also times the open with 1 % and 10 % forged tags (forged_open)
+    assert line == {"rank": 0, "world": 1, "gpus": 1, "local_rank": 0, "workload": "cfg2", "forged": [0.01, 0.1]}
+    r = _run(["--dry-run", "--forged", "0"])
+    (line,) = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert line["forged"] == []
+    r = _run(["--dry-run", "--forged", "1.5"])
+    assert r.returncode != 0
 
 
 def test_world_size_mismatch_is_an_error():
