@@ -47,6 +47,28 @@ __device__ __forceinline__ uint64_t fdiv(uint64_t a, uint64_t b) {
     return (q + 1) * b <= a ? q + 1 : q;
 }
 
+// ------------------------------------------------------ frame stores
+// With an arena below 2 GiB (WIN) every frame store is a buffer store through one descriptor over the
+// arena, and a store that is not payload gets an offset past the descriptor's range, which the
+// hardware drops (no sink traffic; config 3 +1 %, profiles/r3_sc1_ab.txt).  Larger arenas store
+// through 64-bit pointers, the non-payload stores into a per-lane sink.
+constexpr uint32_t kDrop = 0x80000000u;    // past num_records: dropped by the range check
+constexpr int kFlatAux = RG_STORE_SC1 ? 16 : 0;
+struct FStore {
+    uint8_t *buf;
+    __amdgpu_buffer_rsrc_t rs;
+    uint4 *junk;
+};
+template <bool WIN> __device__ __forceinline__ void fstore(const FStore &S, const uint4 *p, bool keep, uint32_t j,
+                                                          const uint4 &v) {
+    if constexpr (WIN) {
+        const uint32_t off = keep ? (uint32_t)(reinterpret_cast<const uint8_t *>(p) - S.buf) : kDrop;
+        __builtin_amdgcn_raw_buffer_store_b128(v4u{v.x, v.y, v.z, v.w}, S.rs, (int)off, 0, kFlatAux);
+    } else {
+        *const_cast<uint4 *>(keep ? p : S.junk + j) = v;
+    }
+}
+
 // ------------------------------------------------------ unit boundaries
 // Work of a packet: its one-time-key block and its 64-byte chunks (from the
 // descriptor alone).
@@ -194,8 +216,8 @@ __device__ __forceinline__ void add_h(FlatLds &L, uint32_t k, const Acc &h) {
 // previous step's ciphertext (pi) inside this step's keystream rounds, open
 // absorbs this chunk's ciphertext; the pending piece is published when the
 // packet changes.  Afterwards chunk j + 3 is requested into b.
-template <bool OPEN>
-__device__ __forceinline__ void flat_step(FLane &s, FChunk &b, uint32_t j, FlatLds &L, uint8_t *buf, uint4 *junk,
+template <bool OPEN, bool WIN>
+__device__ __forceinline__ void flat_step(FLane &s, FChunk &b, uint32_t j, FlatLds &L, uint8_t *buf, const FStore &FS,
                                           uint32_t m, uint32_t lane) {
     const bool active = j < s.nsteps;
     uint32_t cnt = 0;
@@ -230,10 +252,10 @@ __device__ __forceinline__ void flat_step(FLane &s, FChunk &b, uint32_t j, FlatL
     if (s.cur.k == 0xFFFFFFFFu)
 #endif
     {
-        *(cnt > 0 ? dst + 0 : junk + 0) = x.q0;
-        *(cnt > 1 ? dst + 1 : junk + 1) = x.q1;
-        *(cnt > 2 ? dst + 2 : junk + 2) = x.q2;
-        *(cnt > 3 ? dst + 3 : junk + 3) = x.q3;
+        fstore<WIN>(FS, dst + 0, cnt > 0, 0, x.q0);
+        fstore<WIN>(FS, dst + 1, cnt > 1, 1, x.q1);
+        fstore<WIN>(FS, dst + 2, cnt > 2, 2, x.q2);
+        fstore<WIN>(FS, dst + 3, cnt > 3, 3, x.q3);
     }
     if constexpr (OPEN) {
         if (active && s.cur.t + 1 == s.cur.c) { // the packet's last chunk: its final piece
@@ -374,7 +396,7 @@ __device__ __forceinline__ uint32_t flat_stage(FlatLds &L, uint32_t k, const rg_
     return (nb + 3) >> 2;
 }
 
-template <bool OPEN> __global__ __launch_bounds__(64 * kFlatWaves) void flat_kernel(FlatArgs A) {
+template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) void flat_kernel(FlatArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t flat_lds[];
     const uint32_t lane = threadIdx.x & 63, wv = uniform_u32(threadIdx.x >> 6);
     FlatLds &L = reinterpret_cast<FlatLds *>(flat_lds)[wv];
@@ -386,7 +408,10 @@ template <bool OPEN> __global__ __launch_bounds__(64 * kFlatWaves) void flat_ker
     const uint32_t *const keys = OPEN ? A.oa.keys : A.sa.keys;
     const rg_pkt_desc *const desc = OPEN ? A.oa.desc : A.sa.desc;
     uint8_t *const status = OPEN ? A.oa.status : A.sa.status;
-    uint4 *const junk = A.junk + ((uint64_t)wid * 64 + lane) * 4;
+    FStore FS;
+    FS.buf = buf;
+    FS.rs = __builtin_amdgcn_make_buffer_rsrc(buf, (short)0, 0x7FFFFFFF, 0x00020000);
+    FS.junk = WIN ? nullptr : A.junk + ((uint64_t)wid * 64 + lane) * 4;
     // diagnostics (debug mode 3): per wave, s_memtime at the end of each phase of its first sub-unit
     uint64_t *const dbg = OPEN ? A.oa.dbg : A.sa.dbg;
     uint64_t mk[8] = {__builtin_amdgcn_s_memtime(), 0, 0, 0, 0, 0, 0, 0};
@@ -704,7 +729,8 @@ template <bool OPEN> __global__ __launch_bounds__(64 * kFlatWaves) void flat_ker
                     L.rec[k].z |= kLiveBit;
                     if constexpr (!OPEN) {
                         // DataHeader {4, receiver, counter} (rustyguard-core/src/lib.rs:286-290)
-                        if (A.sa.receivers) *reinterpret_cast<uint4 *>(buf + doff[q]) = make_uint4(4u, rcv[q], n1, n2);
+                        if (A.sa.receivers)
+                            fstore<WIN>(FS, reinterpret_cast<const uint4 *>(buf + doff[q]), true, 0, make_uint4(4u, rcv[q], n1, n2));
                     }
                 } else if (status) {
                     status[i] = st;
@@ -778,12 +804,12 @@ template <bool OPEN> __global__ __launch_bounds__(64 * kFlatWaves) void flat_ker
             {
                 uint32_t j = 0;
                 for (; j + 3 <= S; j += 3) {
-                    flat_step<OPEN>(s, b0, j, L, buf, junk, m, lane);
-                    flat_step<OPEN>(s, b1, j + 1, L, buf, junk, m, lane);
-                    flat_step<OPEN>(s, b2, j + 2, L, buf, junk, m, lane);
+                    flat_step<OPEN, WIN>(s, b0, j, L, buf, FS, m, lane);
+                    flat_step<OPEN, WIN>(s, b1, j + 1, L, buf, FS, m, lane);
+                    flat_step<OPEN, WIN>(s, b2, j + 2, L, buf, FS, m, lane);
                 }
-                if (j < S) flat_step<OPEN>(s, b0, j, L, buf, junk, m, lane);
-                if (j + 1 < S) flat_step<OPEN>(s, b1, j + 1, L, buf, junk, m, lane);
+                if (j < S) flat_step<OPEN, WIN>(s, b0, j, L, buf, FS, m, lane);
+                if (j + 1 < S) flat_step<OPEN, WIN>(s, b1, j + 1, L, buf, FS, m, lane);
             }
             RG_FLAT_MARK(4);
             uint32_t ck = ~0u, after = 0;
@@ -846,8 +872,8 @@ template <bool OPEN> __global__ __launch_bounds__(64 * kFlatWaves) void flat_ker
                 uint32_t tag[4];
                 if constexpr (!OPEN) {
                     acc_finish(h, swk.x, swk.y, swk.z, swk.w, tag);
-                    *reinterpret_cast<uint4 *>(buf + (((uint64_t)rc.y << 32) | rc.x) + 16 + P) =
-                        make_uint4(tag[0], tag[1], tag[2], tag[3]);
+                    fstore<WIN>(FS, reinterpret_cast<const uint4 *>(buf + (((uint64_t)rc.y << 32) | rc.x) + 16 + P), true, 0,
+                                make_uint4(tag[0], tag[1], tag[2], tag[3]));
                     if (status) status[i] = RG_PKT_OK;
                 } else {
                     acc_finish(h, 0, 0, 0, 0, tag);
@@ -889,10 +915,10 @@ template <bool OPEN> __global__ __launch_bounds__(64 * kFlatWaves) void flat_ker
                             const Stream stm = make_stream(fk.key, 0u, fk.n1, fk.n2);
                             uint32_t ks[16];
                             stream_block(stm, oc + 1, ks);
-                            if (b0 < onb) p[0] = xor4(m0, ks + 0);
-                            if (b0 + 1 < onb) p[1] = xor4(m1, ks + 4);
-                            if (b0 + 2 < onb) p[2] = xor4(m2, ks + 8);
-                            if (b0 + 3 < onb) p[3] = xor4(m3, ks + 12);
+                            if (b0 < onb) fstore<WIN>(FS, p + 0, true, 0, xor4(m0, ks + 0));
+                            if (b0 + 1 < onb) fstore<WIN>(FS, p + 1, true, 0, xor4(m1, ks + 4));
+                            if (b0 + 2 < onb) fstore<WIN>(FS, p + 2, true, 0, xor4(m2, ks + 8));
+                            if (b0 + 3 < onb) fstore<WIN>(FS, p + 3, true, 0, xor4(m3, ks + 12));
                         }
                         own = -1;
                     };
@@ -947,8 +973,11 @@ hipError_t launch_flat(const SealArgs *sa, const OpenArgs *oa, bool balance, uin
     A.junk = junk;
     A.balance = balance ? 1u : 0u;
     const uint32_t lds = kFlatWaves * (uint32_t)sizeof(FlatLds);
-    if (sa) hipLaunchKernelGGL(flat_kernel<false>, dim3(blocks), dim3(64 * kFlatWaves), lds, s, A);
-    else hipLaunchKernelGGL(flat_kernel<true>, dim3(blocks), dim3(64 * kFlatWaves), lds, s, A);
+    const bool win = (sa ? sa->buf_len : oa->buf_len) < 0x7FFFFFF0ull; // frame offsets below 2 GiB
+    if (sa && win) hipLaunchKernelGGL((flat_kernel<false, true>), dim3(blocks), dim3(64 * kFlatWaves), lds, s, A);
+    else if (sa) hipLaunchKernelGGL((flat_kernel<false, false>), dim3(blocks), dim3(64 * kFlatWaves), lds, s, A);
+    else if (win) hipLaunchKernelGGL((flat_kernel<true, true>), dim3(blocks), dim3(64 * kFlatWaves), lds, s, A);
+    else hipLaunchKernelGGL((flat_kernel<true, false>), dim3(blocks), dim3(64 * kFlatWaves), lds, s, A);
     return hipGetLastError();
 }
 
@@ -956,9 +985,10 @@ uint32_t flat_junk_bytes(int cus) { return (uint32_t)(cus > 0 ? cus : 1) * kFlat
 
 hipError_t prepare_flat_kernels() {
     const int lds = (int)(kFlatWaves * sizeof(FlatLds));
-    hipError_t e = hipFuncSetAttribute((const void *)flat_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    if (e == hipSuccess)
-        e = hipFuncSetAttribute((const void *)flat_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    const void *f[4] = {(const void *)flat_kernel<false, true>, (const void *)flat_kernel<false, false>,
+                        (const void *)flat_kernel<true, true>, (const void *)flat_kernel<true, false>};
+    hipError_t e = hipSuccess;
+    for (int k = 0; k < 4 && e == hipSuccess; ++k) e = hipFuncSetAttribute(f[k], hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     return e;
 }
 

@@ -115,16 +115,10 @@ constexpr bool PIPE_OPEN_CUR = RG_PIPE_OPEN_CUR != 0;
 #define RG_PIPE_LOAD_FIRST 0
 #endif
 constexpr bool PIPE_LOAD_FIRST = RG_PIPE_LOAD_FIRST != 0;
-// experiment: ring stores written through to memory (1) or non-temporal (2), so that fewer dirty
-// lines are left in L2 for the end-of-kernel write-back
-#ifndef RG_PIPE_WT
-#define RG_PIPE_WT 0
-#endif
 // diagnostics only (tools/build_variant.sh): 1 = line stores dropped, 2 = LDS ring dropped
 #ifndef RG_PIPE_ABL
 #define RG_PIPE_ABL 0
 #endif
-constexpr int PIPE_WT = RG_PIPE_WT;
 constexpr uint32_t kPipeLinesFlag = 4u;      // launch flag bit (bits 0-1: log2 lanes per packet)
 constexpr uint32_t kRingBytes = 64u * 256u; // per wave
 // (plain vector types: HIP's uint4 has no assignment in a qualified address space)
@@ -133,32 +127,70 @@ typedef __attribute__((address_space(1))) v4u glb_u4;
 __device__ __forceinline__ v4u to_v4(const uint4 &a) { return v4u{a.x, a.y, a.z, a.w}; }
 __device__ __forceinline__ uint32_t ring_g(uint32_t p) { return (p & 1u) ^ (((p >> 1) & 1u) * 10u) ^ (((p >> 2) & 1u) * 4u); }
 
+// Frame stores of a line-store wave go through a buffer resource based at the wave's lowest frame:
+// 32-bit offsets (16 VGPRs fewer than the 64-bit line pointers: 282 -> 268 for the seal, 305 -> 264
+// for the open), compiler-visible, so hipcc's vmcnt waits stay exact, and the cache policy in one
+// place (write-through with RG_STORE_SC1, measured no faster: rg_device.h).
+constexpr int kFrameAux = RG_STORE_SC1 ? 16 : 0; // buffer-instruction cache bits: 16 = sc1
+
 struct Ring {
-    lds_u4 *wr;       // this lane's frame record
-    lds_u4 *rd;       // line-major reads: frame lane / 8 (+ 8 q + 32 h), slot base
-    glb_u4 *fr[2][4]; // frame 32 h + 8 q + lane / 8, byte 16 (lane % 8) of line 0
-    uint32_t gw, gr;  // slot swizzles: this lane's frame (writes), frame lane / 8 (reads)
+    lds_u4 *wr;          // this lane's frame record
+    lds_u4 *rd;          // line-major reads: frame lane / 8 (+ 8 q + 32 h), slot base
+    uint32_t fo[2][4];   // byte offset of frame 32 h + 8 q + lane / 8, + 16 (lane % 8), in the wave's window
+    uint32_t self;       // byte offset of this lane's frame in the window
+    uint64_t base;       // the window's base address (wave-uniform)
+    __amdgpu_buffer_rsrc_t rs; // the window: the wave's frames
+    uint32_t gw, gr;     // slot swizzles: this lane's frame (writes), frame lane / 8 (reads)
 };
 
-__device__ __forceinline__ Ring make_ring(uint8_t *frame) {
+// The window of a wave whose 64 lanes all hold a frame of `len` bytes: based at the lowest frame,
+// false when the frames span 2 GiB or more (the wave then stores lane by lane, without the ring).
+__device__ __forceinline__ bool frame_window(const uint8_t *frame, uint32_t len, uint64_t &base) {
+    const uint64_t f = reinterpret_cast<uint64_t>(frame);
+    const uint64_t f0 = uniform_u64(f);
+    const int64_t dlt = (int64_t)(f - f0);
+    const bool near = dlt > -(int64_t)(1u << 30) && dlt < (int64_t)(1u << 30);
+    if (__ballot(!near) != 0) return false;
+    // biased to [0, 2^31): prefix maxima of v and of its complement give the max and the min
+    const uint32_t v = (uint32_t)(dlt + (int64_t)(1u << 30));
+    const uint32_t vmax = lane63(wave_scan_max(v)), vmin = 0x7FFFFFFFu - lane63(wave_scan_max(0x7FFFFFFFu - v));
+    if ((uint64_t)(vmax - vmin) + len >= (1ull << 31)) return false;
+    base = f0 + (uint64_t)vmin - (1ull << 30);
+    return true;
+}
+
+__device__ __forceinline__ Ring make_ring(uint8_t *frame, uint64_t base) {
     extern __shared__ __attribute__((aligned(16))) uint8_t pipe_lds[];
     const uint32_t lane = threadIdx.x & 63;
-    lds_u4 *base = (lds_u4 *)(pipe_lds + (threadIdx.x >> 6) * kRingBytes);
+    lds_u4 *lb = (lds_u4 *)(pipe_lds + (threadIdx.x >> 6) * kRingBytes);
     Ring R;
-    R.wr = base + 16 * lane;
+    R.wr = lb + 16 * lane;
     R.gw = ring_g(lane);
-    R.rd = base + 16 * (lane >> 3);
+    R.rd = lb + 16 * (lane >> 3);
     R.gr = ring_g(lane >> 3);
-    const uint64_t f = reinterpret_cast<uint64_t>(frame);
+    R.self = (uint32_t)(reinterpret_cast<uint64_t>(frame) - base);
+    R.base = base;
+    R.rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(base), (short)0, 0x7FFFFFFF, 0x00020000);
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int src = 32 * h + 8 * q + (int)(lane >> 3);
-            const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)f, src), hi = (uint32_t)__shfl((int)(uint32_t)(f >> 32), src);
-            R.fr[h][q] = (glb_u4 *)((((uint64_t)hi << 32) | lo) + 16 * (lane & 7u));
-        }
+        for (int q = 0; q < 4; ++q)
+            R.fo[h][q] = (uint32_t)__shfl((int)R.self, 32 * h + 8 * q + (int)(lane >> 3)) + 16 * (lane & 7u);
     return R;
+}
+
+// the same window with its descriptor rebuilt from readfirstlane values: a descriptor that reaches its
+// use through a join of branches hipcc cannot prove uniform becomes a per-lane waterfall loop
+__device__ __forceinline__ Ring pin_window(const Ring &R) {
+    Ring o = R;
+    o.base = uniform_u64(R.base);
+    o.rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(o.base), (short)0, 0x7FFFFFFF, 0x00020000);
+    return o;
+}
+
+// a 16-byte piece of this lane's frame at byte `off` of the frame (line-store waves)
+__device__ __forceinline__ void frame_store(const Ring &R, uint32_t off, const uint4 &x) {
+    __builtin_amdgcn_raw_buffer_store_b128(to_v4(x), R.rs, (int)(R.self + off), 0, kFrameAux);
 }
 
 // block t (4 pieces) of this lane's frame into set t & 3
@@ -193,16 +225,8 @@ __device__ __forceinline__ void ring_store(const Ring &R, const Ring4 &x, uint32
         if (((lane >> 2) & 1u) && 2 * k + 1 >= nblk) return;
     }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        glb_u4 *dst = (h ? R.fr[1][q] : R.fr[0][q]) + 8 * k;
-        // (the s_nop: a VALU write to the data registers of a store wider than 64 bits needs a wait
-        // state, which the hazard pass does not insert behind inline asm)
-        if constexpr (PIPE_WT == 1) // device-scope write-through (sc1): the line leaves L2 clean
-            asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(dst), "v"(x.v[q]) : "memory");
-        else if constexpr (PIPE_WT == 2) // non-temporal (streaming) whole-line stores
-            asm volatile("global_store_dwordx4 %0, %1, off nt\n\ts_nop 1" ::"v"(dst), "v"(x.v[q]) : "memory");
-        else *dst = x.v[q];
-    }
+    for (int q = 0; q < 4; ++q)
+        __builtin_amdgcn_raw_buffer_store_b128(x.v[q], R.rs, (int)((h ? R.fo[1][q] : R.fo[0][q]) + 128 * k), 0, kFrameAux);
 }
 
 // Diagnostic build only (RG_PIPE_WSTAMP, tools/wstamps.py): per wave, cycles of the line-store steps
@@ -319,10 +343,18 @@ __device__ __forceinline__ void pipe_step(uint4 *pl, const Stream &st, const Mul
         have_prev = true;
     } else if constexpr (TAIL) {
         const uint32_t cnt = nb & 3u;
-        if (have_prev) st16<NT>(dst - 1, prev);
-        st16<NT>(dst + 0, x.q0); // cnt >= 1
-        if (cnt > 1) st16<NT>(dst + 1, x.q1);
-        if (cnt > 2) st16<NT>(dst + 2, x.q2);
+        if constexpr (LINES) { // one lane per packet: pl = frame + 16, dst = frame byte 16 + 64 t
+            const uint32_t o = 16 + 64 * t;
+            if (have_prev) frame_store(R, o - 16, prev);
+            frame_store(R, o, x.q0); // cnt >= 1
+            if (cnt > 1) frame_store(R, o + 16, x.q1);
+            if (cnt > 2) frame_store(R, o + 32, x.q2);
+        } else {
+            if (have_prev) st16<NT>(dst - 1, prev);
+            st16<NT>(dst + 0, x.q0); // cnt >= 1
+            if (cnt > 1) st16<NT>(dst + 1, x.q1);
+            if (cnt > 2) st16<NT>(dst + 2, x.q2);
+        }
         have_prev = false;
     } else {
         if constexpr (ABSORB) st16<NT>(dst - 1, prev); // inside the loop there always is one
@@ -361,7 +393,8 @@ __device__ __forceinline__ void pipe_step(uint4 *pl, const Stream &st, const Mul
 template <bool OPEN, int MODE = 0, bool LINES = false, bool POLY = true>
 __device__ __forceinline__ Acc pipe_pass(uint4 *pl, const Stream &st, const Mul &r, uint32_t nb, uint32_t c0,
                                          Chunk &b0, Chunk &b1, Chunk &b2, Chunk &b3, uint4 head, bool has_head,
-                                         const Ring &R, bool keep = false, uint64_t *wst = nullptr) {
+                                         const Ring &R0, bool keep = false, uint64_t *wst = nullptr) {
+    const Ring R = LINES ? pin_window(R0) : R0;
     const uint32_t F = nb >> 2, bl = nb & 3u; // full chunks, blocks in the partial last chunk
     uint64_t wacc[6] = {0, 0, 0, 0, 0, 0};
     (void)wst;
@@ -444,7 +477,9 @@ __device__ __forceinline__ Acc pipe_pass(uint4 *pl, const Stream &st, const Mul 
         else pipe_step<OPEN, false, true, MODE, LINES, false, POLY>(pl, st, r, h, pi, bp, prev, have_prev, F, nb, c0, R, keep, wacc);
         pending = bl;
     }
-    if (have_prev && MODE != 1) st16<(MODE == 7 ? 4 : MODE >= 4 ? MODE - 3 : 0)>(pl + 4 * F - 1, prev);
+    if constexpr (LINES) {
+        if (have_prev) frame_store(R, 64 * F, prev); // pl + 4 F - 1
+    } else if (have_prev && MODE != 1) st16<(MODE == 7 ? 4 : MODE >= 4 ? MODE - 3 : 0)>(pl + 4 * F - 1, prev);
     if constexpr (!(OPEN && (PIPE_OPEN_CUR || !POLY))) absorb_chunk(h, pi, r, pending); // the last chunk's blocks
     RG_WST(if (wst && (threadIdx.x & 63) == 0) for (int k = 0; k < 6; ++k) atomicAdd((unsigned long long *)&wst[k < 3 ? k : 8ull * gridDim.x * (blockDim.x / 64) + k - 4], (unsigned long long)wacc[k]);)
     return h;
@@ -546,6 +581,8 @@ __device__ __forceinline__ void pipe_seal_packet(const SealArgs &a, uint32_t i, 
     bool lines = false;
     if constexpr (MODE == 0 || MODE == 8)
         lines = lines_ok && G == 1 && __ballot(valid && P == uniform_u32(P)) == ~0ull;
+    uint64_t wbase = 0;
+    if (lines) lines = frame_window(a.buf + d.offset, P + 32, wbase); // wave-uniform
     if (!valid) {
         if (a.status && j == 0) a.status[i] = d.key_idx == RG_KEY_SKIP ? RG_PKT_REJECTED : RG_PKT_INVALID;
         return;
@@ -582,12 +619,14 @@ __device__ __forceinline__ void pipe_seal_packet(const SealArgs &a, uint32_t i, 
     const bool head = a.receivers != nullptr && j == 0;
     uint4 hdr = make_uint4(4u, head ? a.receivers[d.key_idx] : 0u, n1, n2);
     Acc h;
+    Ring R{};
     if (lines) { // wave-uniform
         if (!head) hdr = *reinterpret_cast<const uint4 *>(frame); // block 0 is stored whole: header unchanged
+        R = make_ring(frame, wbase);
 #ifdef RG_PIPE_WSTAMP
-        h = pipe_pass<false, MODE, true>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, b3, hdr, true, make_ring(frame), false, wst_slot(a.dbg));
+        h = pipe_pass<false, MODE, true>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, b3, hdr, true, R, false, wst_slot(a.dbg));
 #else
-        h = pipe_pass<false, MODE, true>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, b3, hdr, true, make_ring(frame));
+        h = pipe_pass<false, MODE, true>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, b3, hdr, true, R);
 #endif
     } else {
         h = pipe_pass<false, MODE, false>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, b3, hdr, head, Ring{});
@@ -598,7 +637,8 @@ __device__ __forceinline__ void pipe_seal_packet(const SealArgs &a, uint32_t i, 
     if (j != 0) return;
     uint32_t tag[4];
     pipe_tag(h, r, P, ks + 4, tag);
-    *reinterpret_cast<uint4 *>(frame + 16 + P) = make_uint4(tag[0], tag[1], tag[2], tag[3]);
+    if (lines) frame_store(pin_window(R), 16 + P, make_uint4(tag[0], tag[1], tag[2], tag[3]));
+    else *reinterpret_cast<uint4 *>(frame + 16 + P) = make_uint4(tag[0], tag[1], tag[2], tag[3]);
     if (a.status) a.status[i] = RG_PKT_OK;
 }
 
@@ -677,7 +717,9 @@ __device__ __forceinline__ void pipe_open_packet(const OpenArgs &a, uint32_t i, 
         }
     }
     // block stores through the LDS ring: every lane of the wave a data packet of one size
-    const bool lines = lines_ok && G == 1 && __ballot(st == 0xFF && W == uniform_u32(W)) == ~0ull;
+    bool lines = lines_ok && G == 1 && __ballot(st == 0xFF && W == uniform_u32(W)) == ~0ull;
+    uint64_t wbase = 0;
+    if (lines) lines = frame_window(frame, W, wbase); // wave-uniform
     if (st != 0xFF) {
         if (j == 0) {
             a.status[i] = (uint8_t)st;
@@ -708,7 +750,7 @@ __device__ __forceinline__ void pipe_open_packet(const OpenArgs &a, uint32_t i, 
         uint32_t tag[4];
         pipe_tag(h, r, P, ks + 4, tag);
         const uint32_t df = (tag[0] ^ want.x) | (tag[1] ^ want.y) | (tag[2] ^ want.z) | (tag[3] ^ want.w);
-        if constexpr (L) (void)pipe_pass<true, 0, true, false>(pl, stm, r, sg.nb, sg.c0, p0, p1, p2, p3, hdr, true, make_ring(frame), df != 0);
+        if constexpr (L) (void)pipe_pass<true, 0, true, false>(pl, stm, r, sg.nb, sg.c0, p0, p1, p2, p3, hdr, true, make_ring(frame, wbase), df != 0);
         else (void)pipe_pass<true, 0, false, false>(pl, stm, r, sg.nb, sg.c0, p0, p1, p2, p3, make_uint4(0, 0, 0, 0), false, Ring{}, df != 0);
         return df;
     };
@@ -717,9 +759,9 @@ __device__ __forceinline__ void pipe_open_packet(const OpenArgs &a, uint32_t i, 
 #else
     Acc h;
 #ifdef RG_PIPE_WSTAMP
-    if (lines) h = pipe_pass<true, 0, true>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, b3, hdr, true, make_ring(frame), false, wst_slot(a.dbg));
+    if (lines) h = pipe_pass<true, 0, true>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, b3, hdr, true, make_ring(frame, wbase), false, wst_slot(a.dbg));
 #else
-    if (lines) h = pipe_pass<true, 0, true>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, b3, hdr, true, make_ring(frame)); // header unchanged
+    if (lines) h = pipe_pass<true, 0, true>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, b3, hdr, true, make_ring(frame, wbase)); // header unchanged
 #endif
     else h = pipe_pass<true, 0, false>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, b3, make_uint4(0, 0, 0, 0), false, Ring{});
     h = combine_segments(h, r, sg.after, G);

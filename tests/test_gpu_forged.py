@@ -8,7 +8,7 @@ their fast store paths:
 * config-2 shape (uniform 1504-byte payloads at a 1536-byte stride, >= 64 packets per wave): the
   pipelined kernel stores whole lines through its LDS ring, so other lanes write a lane's frame;
 * tile batches of more than CUs x 512 uniform frames at a 1536-byte stride: the LDS-staged kernel's
-  line-aligned (SH = 1) windows, two deal rounds and the grid-wide pool;
+  line-aligned (SH = 1) windows over two deal rounds, and config 4 (eight rounds: the grid-wide pool);
 * IMIX (config 3) on the flattened chunk stream, where a lane's chunk range spans packets.
 
 1 %, 10 % and 100 % of the frames are forged at a random byte of payload or tag; the GPU output
@@ -95,7 +95,7 @@ def test_forged_cfg2_geometry(engine, staged, frac):
 @pytest.mark.parametrize("plan", [2, 0])
 def test_forged_tile_geometry(engine, plan, frac):
     """2 x CUs x 512 + 777 uniform frames at 1536-byte stride: the LDS-staged tile kernel with
-    line-aligned windows over two deal rounds and a partial third (grid-wide pool), planner auto/off."""
+    line-aligned windows over two deal rounds and a partial third (below the pool's eight), planner auto/off."""
     engine.set_staged(2)
     engine.set_plan(plan)
     try:
@@ -107,7 +107,8 @@ def test_forged_tile_geometry(engine, plan, frac):
 
 @pytest.mark.parametrize("frac", FRACS)
 def test_forged_cfg4_geometry(engine, frac):
-    """Config 4 (256 sessions x 4 Ki, per-packet key gather) under the automatic choice (tiles)."""
+    """Config 4 (256 sessions x 4 Ki, per-packet key gather) under the automatic choice (tiles, eight deal
+    rounds: the last one from the grid-wide pool)."""
     _check(engine, workloads.build("cfg4"), frac, seed=14)
 
 
