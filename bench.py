@@ -529,12 +529,23 @@ def main():
 
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # Rehearsal of the N > 1 path on a one-GPU box (RG_BENCH_SHARE_GPU=1): every rank on device 0, the
+    # bookkeeping collectives over gloo on CPU tensors (RCCL refuses two ranks on one GPU).  Never a
+    # scaling measurement: the ranks share one GPU, and the line says so.
+    share = os.environ.get("RG_BENCH_SHARE_GPU") == "1"
+    if share:
+        local = 0
     torch.cuda.set_device(local)
     dist = None
+    coll_dev = "cuda"
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if share:
+            dist.init_process_group("gloo")
+            coll_dev = "cpu"
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from rustyguard_amd import workloads
     from rustyguard_amd.aead import Engine
@@ -666,7 +677,7 @@ def main():
     if args.verify:
         strict_check(w, b, stream)
 
-    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
     if dist is not None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     tmax = float(t.item())
@@ -765,6 +776,9 @@ def main():
         out["cpu_baseline"] = port
         if ossl:
             out["cpu_openssl"] = ossl
+    if share and world > 1:
+        out["rehearsal"] = (f"RG_BENCH_SHARE_GPU=1: {world} ranks shared one GPU over gloo -- a functional rehearsal of "
+                            "the N > 1 path, not a scaling measurement")
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:
