@@ -115,6 +115,18 @@ constexpr bool PIPE_OPEN_CUR = RG_PIPE_OPEN_CUR != 0;
 #define RG_PIPE_LOAD_FIRST 0
 #endif
 constexpr bool PIPE_LOAD_FIRST = RG_PIPE_LOAD_FIRST != 0;
+// quad block stores instead of the LDS ring (below): 247 GPU tests green, measured equal or 1-2 % slower
+// on config 2 (profiles/r3_cfg2_quad_ab.txt): the DPP transpose costs what the ring does
+#ifndef RG_PIPE_QUAD
+#define RG_PIPE_QUAD 0
+#endif
+constexpr bool PIPE_QUAD = RG_PIPE_QUAD != 0;
+// experiment: the four line stores of a step issued one per two double rounds of its keystream block
+// (compiler-visible buffer stores, so hipcc counts them in its vmcnt waits)
+#ifndef RG_PIPE_SPREAD
+#define RG_PIPE_SPREAD 0
+#endif
+constexpr bool PIPE_SPREAD = RG_PIPE_SPREAD != 0;
 // diagnostics only (tools/build_variant.sh): 1 = line stores dropped, 2 = LDS ring dropped
 #ifndef RG_PIPE_ABL
 #define RG_PIPE_ABL 0
@@ -137,6 +149,7 @@ struct Ring {
     lds_u4 *wr;          // this lane's frame record
     lds_u4 *rd;          // line-major reads: frame lane / 8 (+ 8 q + 32 h), slot base
     uint32_t fo[2][4];   // byte offset of frame 32 h + 8 q + lane / 8, + 16 (lane % 8), in the wave's window
+    uint32_t qo[4];      // quad stores: byte offset of frame (lane & ~3) + q, + 16 (lane % 4)
     uint32_t self;       // byte offset of this lane's frame in the window
     uint64_t base;       // the window's base address (wave-uniform)
     __amdgpu_buffer_rsrc_t rs; // the window: the wave's frames
@@ -175,8 +188,68 @@ __device__ __forceinline__ Ring make_ring(uint8_t *frame, uint64_t base) {
     for (int h = 0; h < 2; ++h)
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-            R.fo[h][q] = (uint32_t)__shfl((int)R.self, 32 * h + 8 * q + (int)(lane >> 3)) + 16 * (lane & 7u);
+            R.fo[h][q] = PIPE_QUAD ? 0u : (uint32_t)__shfl((int)R.self, 32 * h + 8 * q + (int)(lane >> 3)) + 16 * (lane & 7u);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        R.qo[q] = PIPE_QUAD ? (uint32_t)__shfl((int)R.self, (int)(lane & ~3u) + q) + 16 * (lane & 3u) : 0u;
     return R;
+}
+
+// ------------------------------------------------------ quad block stores
+// (RG_PIPE_QUAD, an option: no LDS ring.)  Each step makes one frame-aligned 64-byte
+// block per lane (pieces 4t .. 4t+3 of its frame).  A 4 x 4 transpose of the 16-byte pieces inside each
+// lane quad (two DPP quad_perm butterfly stages, v_cndmask with a DPP source) leaves lane j of a quad
+// with piece j of the quad's frames 0..3, so each of the step's four stores writes 16 whole 64-byte
+// half-lines (four lanes each) instead of one 16-byte piece into each of 64 frames.  The ring's four
+// ds_write_b128 + four ds_read_b128 per step cost ~12 k cycles per config-2 wave
+// (profiles/r3_cfg2_attribution.txt); the transpose is VALU only, 32 DPP moves + 32 selects per step,
+// and measured as costly (148.9 k against 148.1 k cycles per wave, profiles/r3_cfg2_quad_ab.txt).
+template <int CTRL> __device__ __forceinline__ uint32_t qperm(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
+}
+__device__ __forceinline__ void quad_t4(uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d) {
+    const uint32_t lane = threadIdx.x & 3u;
+    const bool odd = lane & 1u, hi = lane & 2u;
+    // (the DPP moves are convergent: computed unconditionally, or hipcc branches around them)
+    // stage 1, partner lane ^ 1 (quad_perm [1,0,3,2]): pieces p with (p ^ lane) & 1 come from it, as piece p ^ 1
+    const uint32_t xa = qperm<0xB1>(a), xb = qperm<0xB1>(b), xc = qperm<0xB1>(c), xd = qperm<0xB1>(d);
+    const uint32_t n0 = odd ? xb : a, n1 = odd ? b : xa, n2 = odd ? xd : c, n3 = odd ? d : xc;
+    // stage 2, partner lane ^ 2 (quad_perm [2,3,0,1])
+    const uint32_t y0 = qperm<0x4E>(n0), y1 = qperm<0x4E>(n1), y2 = qperm<0x4E>(n2), y3 = qperm<0x4E>(n3);
+    a = hi ? y2 : n0;
+    b = hi ? y3 : n1;
+    c = hi ? n2 : y0;
+    d = hi ? n3 : y1;
+}
+// block b of this lane's frame = pieces p0 .. p3; pieces from `valid` on are not the frame's (dropped)
+__device__ __forceinline__ void quad_block_store(const Ring &R, uint32_t b, uint4 p0, uint4 p1, uint4 p2, uint4 p3,
+                                                 uint32_t valid = 4) {
+    quad_t4(p0.x, p1.x, p2.x, p3.x);
+    quad_t4(p0.y, p1.y, p2.y, p3.y);
+    quad_t4(p0.z, p1.z, p2.z, p3.z);
+    quad_t4(p0.w, p1.w, p2.w, p3.w);
+    const bool ok = (threadIdx.x & 3u) < valid;
+    __builtin_amdgcn_raw_buffer_store_b128(to_v4(p0), R.rs, (int)(ok ? R.qo[0] + 64 * b : 0x80000000u), 0, kFrameAux);
+    __builtin_amdgcn_raw_buffer_store_b128(to_v4(p1), R.rs, (int)(ok ? R.qo[1] + 64 * b : 0x80000000u), 0, kFrameAux);
+    __builtin_amdgcn_raw_buffer_store_b128(to_v4(p2), R.rs, (int)(ok ? R.qo[2] + 64 * b : 0x80000000u), 0, kFrameAux);
+    __builtin_amdgcn_raw_buffer_store_b128(to_v4(p3), R.rs, (int)(ok ? R.qo[3] + 64 * b : 0x80000000u), 0, kFrameAux);
+}
+
+// the frame's last pieces, stored by the caller once the tag is known (quad block stores)
+struct QTail {
+    uint4 p0, p1, p2, p3;
+    uint32_t n; // pieces held, 1 .. 4
+};
+// pieces + the tag: block b (and b + 1 when they make five)
+__device__ __forceinline__ void quad_tail_store(const Ring &R, uint32_t b, const QTail &tl, const uint4 &tag) {
+    const uint4 z = make_uint4(0, 0, 0, 0);
+    if (tl.n == 4) { // wave-uniform
+        quad_block_store(R, b, tl.p0, tl.p1, tl.p2, tl.p3, 4);
+        quad_block_store(R, b + 1, tag, z, z, z, 1);
+    } else {
+        quad_block_store(R, b, tl.p0, tl.n > 1 ? tl.p1 : tag, tl.n > 2 ? tl.p2 : tl.n == 2 ? tag : z,
+                         tl.n == 3 ? tag : z, tl.n + 1);
+    }
 }
 
 // the same window with its descriptor rebuilt from readfirstlane values: a descriptor that reaches its
@@ -275,7 +348,8 @@ __device__ __forceinline__ uint64_t *wst_slot(uint64_t *dbg) {
 template <bool OPEN, bool ABSORB, bool TAIL, int MODE = 0, bool LINES = false, bool FLUSH = false, bool POLY = true>
 __device__ __forceinline__ void pipe_step(uint4 *pl, const Stream &st, const Mul &r, Acc &h, Chunk &pi, Chunk &buf,
                                           uint4 &prev, bool &have_prev, uint32_t t, uint32_t nb, uint32_t c0,
-                                          const Ring &R, bool keep = false, uint64_t *wacc = nullptr) {
+                                          const Ring &R, bool keep = false, uint64_t *wacc = nullptr,
+                                          QTail *tl = nullptr) {
     uint32_t ks[16];
     static_assert(!FLUSH || (LINES && ABSORB && !TAIL), "flush steps");
     Ring4 fl;
@@ -293,6 +367,14 @@ __device__ __forceinline__ void pipe_step(uint4 *pl, const Stream &st, const Mul
         for (int i = 0; i < 16; ++i) ks[i] = t * 16 + i;
         h.h0 ^= pi.q0.x ^ pi.q1.y ^ pi.q2.z ^ pi.q3.w;
     } else stream_block_hooked(st, c0 + t + 1, ks, [&](int dr) {
+        if constexpr (FLUSH && PIPE_SPREAD && RG_PIPE_ABL != 1) { // the line stores, one per two double rounds
+            if (dr == 2 || dr == 4 || dr == 6 || dr == 8) {
+                const int q = dr / 2 - 1;
+                const uint32_t kk = MODE == 8 ? ((t - 2) >> 1) & 1u : (t - 2) >> 1;
+                __builtin_amdgcn_raw_buffer_store_b128(fl.v[q], R.rs, (int)(((t & 1u) ? R.fo[1][q] : R.fo[0][q]) + 128 * kk), 0,
+                                                       kFrameAux);
+            }
+        }
         if constexpr (OPEN && !POLY) {
         } else if constexpr (OPEN && PIPE_OPEN_CUR) { // this chunk's ciphertext (TAIL: its nb % 4 blocks)
             const uint32_t bl = TAIL ? nb & 3u : 4u;
@@ -328,7 +410,11 @@ __device__ __forceinline__ void pipe_step(uint4 *pl, const Stream &st, const Mul
         if constexpr (!(OPEN && PIPE_OPEN_CUR)) pi = OPEN ? buf : x;
         load_chunk<NT>(buf, pl, t + kDepth, nb - 1);
     }
-    if constexpr (LINES && !TAIL) {
+    if constexpr (LINES && !TAIL && PIPE_QUAD) {
+        quad_block_store(R, t, prev, x.q0, x.q1, x.q2); // prev: the header before the first chunk
+        prev = x.q3;
+        have_prev = true;
+    } else if constexpr (LINES && !TAIL) {
 #if RG_PIPE_ABL == 2
         asm volatile("" ::"v"(prev.x), "v"(x.q0.x), "v"(x.q1.x), "v"(x.q2.x));
 #else
@@ -337,13 +423,19 @@ __device__ __forceinline__ void pipe_step(uint4 *pl, const Stream &st, const Mul
 #if RG_PIPE_ABL == 1 // diagnostics only: the ring is read back but its lines are not stored (output invalid)
         if constexpr (FLUSH) asm volatile("" ::"v"(fl.v[0]), "v"(fl.v[1]), "v"(fl.v[2]), "v"(fl.v[3]));
 #else
-        if constexpr (FLUSH) ring_store(R, fl, MODE == 8 ? ((t - 2) >> 1) & 1u : (t - 2) >> 1, t & 1u);
+        if constexpr (FLUSH && !PIPE_SPREAD) ring_store(R, fl, MODE == 8 ? ((t - 2) >> 1) & 1u : (t - 2) >> 1, t & 1u);
 #endif
         prev = x.q3;
         have_prev = true;
     } else if constexpr (TAIL) {
         const uint32_t cnt = nb & 3u;
-        if constexpr (LINES) { // one lane per packet: pl = frame + 16, dst = frame byte 16 + 64 t
+        if constexpr (LINES && PIPE_QUAD) { // block t = prev + the cnt pieces: stored with the tag by the caller
+            tl->p0 = prev;
+            tl->p1 = x.q0;
+            tl->p2 = x.q1;
+            tl->p3 = x.q2;
+            tl->n = 1 + cnt;
+        } else if constexpr (LINES) { // one lane per packet: pl = frame + 16, dst = frame byte 16 + 64 t
             const uint32_t o = 16 + 64 * t;
             if (have_prev) frame_store(R, o - 16, prev);
             frame_store(R, o, x.q0); // cnt >= 1
@@ -393,7 +485,8 @@ __device__ __forceinline__ void pipe_step(uint4 *pl, const Stream &st, const Mul
 template <bool OPEN, int MODE = 0, bool LINES = false, bool POLY = true>
 __device__ __forceinline__ Acc pipe_pass(uint4 *pl, const Stream &st, const Mul &r, uint32_t nb, uint32_t c0,
                                          Chunk &b0, Chunk &b1, Chunk &b2, Chunk &b3, uint4 head, bool has_head,
-                                         const Ring &R0, bool keep = false, uint64_t *wst = nullptr) {
+                                         const Ring &R0, bool keep = false, uint64_t *wst = nullptr,
+                                         QTail *tl = nullptr) {
     const Ring R = LINES ? pin_window(R0) : R0;
     const uint32_t F = nb >> 2, bl = nb & 3u; // full chunks, blocks in the partial last chunk
     uint64_t wacc[6] = {0, 0, 0, 0, 0, 0};
@@ -403,14 +496,14 @@ __device__ __forceinline__ Acc pipe_pass(uint4 *pl, const Stream &st, const Mul 
     uint4 prev = head; // block still to be stored just in front of the current chunk
     bool have_prev = has_head;
     uint32_t pending = 0; // blocks of pi not yet absorbed
-    if constexpr (LINES) wave_sync(); // the previous packet's last read-back is done
+    if constexpr (LINES && !PIPE_QUAD) wave_sync(); // the previous packet's last read-back is done
     if (F > 0) {
         pipe_step<OPEN, false, false, MODE, LINES, false, POLY>(pl, st, r, h, pi, b0, prev, have_prev, 0, nb, c0, R, keep, wacc);
         uint32_t t = 1;
         // whole rounds of kDepth steps only: a step that may be skipped would
         // leave the waitcnt pass a path without its memory operations
         // (vmcnt(0) at the next one); the remainder steps run after the loop
-        if constexpr (LINES) {
+        if constexpr (LINES && !PIPE_QUAD) {
             static_assert(kDepth >= 3, "line stores: three or four chunk buffers");
             // step 1 has no complete line yet; steps 2.. each store half a line
             if (F > 1) pipe_step<OPEN, true, false, MODE, true, false, POLY>(pl, st, r, h, pi, b1, prev, have_prev, 1, nb, c0, R, keep, wacc);
@@ -440,28 +533,28 @@ __device__ __forceinline__ Acc pipe_pass(uint4 *pl, const Stream &st, const Mul 
                 ring_store<true>(R, ring_get(R, m >> 1, m & 1u), MODE == 8 ? (m >> 1) & 1u : m >> 1, m & 1u, F);
         } else if constexpr (kDepth == 4) {
             for (; t + 3 < F; t += 4) {
-                pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R, keep, wacc);
-                pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b2, prev, have_prev, t + 1, nb, c0, R, keep, wacc);
-                pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b3, prev, have_prev, t + 2, nb, c0, R, keep, wacc);
-                pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b0, prev, have_prev, t + 3, nb, c0, R, keep, wacc);
+                pipe_step<OPEN, true, false, MODE, LINES, false, POLY>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R, keep, wacc);
+                pipe_step<OPEN, true, false, MODE, LINES, false, POLY>(pl, st, r, h, pi, b2, prev, have_prev, t + 1, nb, c0, R, keep, wacc);
+                pipe_step<OPEN, true, false, MODE, LINES, false, POLY>(pl, st, r, h, pi, b3, prev, have_prev, t + 2, nb, c0, R, keep, wacc);
+                pipe_step<OPEN, true, false, MODE, LINES, false, POLY>(pl, st, r, h, pi, b0, prev, have_prev, t + 3, nb, c0, R, keep, wacc);
             }
-            if (t < F) pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R, keep, wacc);
-            if (t + 1 < F) pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b2, prev, have_prev, t + 1, nb, c0, R, keep, wacc);
-            if (t + 2 < F) pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b3, prev, have_prev, t + 2, nb, c0, R, keep, wacc);
+            if (t < F) pipe_step<OPEN, true, false, MODE, LINES, false, POLY>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R, keep, wacc);
+            if (t + 1 < F) pipe_step<OPEN, true, false, MODE, LINES, false, POLY>(pl, st, r, h, pi, b2, prev, have_prev, t + 1, nb, c0, R, keep, wacc);
+            if (t + 2 < F) pipe_step<OPEN, true, false, MODE, LINES, false, POLY>(pl, st, r, h, pi, b3, prev, have_prev, t + 2, nb, c0, R, keep, wacc);
         } else if constexpr (kDepth == 3) {
             for (; t + 2 < F; t += 3) {
-                pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R, keep, wacc);
-                pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b2, prev, have_prev, t + 1, nb, c0, R, keep, wacc);
-                pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b0, prev, have_prev, t + 2, nb, c0, R, keep, wacc);
+                pipe_step<OPEN, true, false, MODE, LINES, false, POLY>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R, keep, wacc);
+                pipe_step<OPEN, true, false, MODE, LINES, false, POLY>(pl, st, r, h, pi, b2, prev, have_prev, t + 1, nb, c0, R, keep, wacc);
+                pipe_step<OPEN, true, false, MODE, LINES, false, POLY>(pl, st, r, h, pi, b0, prev, have_prev, t + 2, nb, c0, R, keep, wacc);
             }
-            if (t < F) pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R, keep, wacc);
-            if (t + 1 < F) pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b2, prev, have_prev, t + 1, nb, c0, R, keep, wacc);
+            if (t < F) pipe_step<OPEN, true, false, MODE, LINES, false, POLY>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R, keep, wacc);
+            if (t + 1 < F) pipe_step<OPEN, true, false, MODE, LINES, false, POLY>(pl, st, r, h, pi, b2, prev, have_prev, t + 1, nb, c0, R, keep, wacc);
         } else {
             for (; t + 1 < F; t += 2) {
-                pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R, keep, wacc);
-                pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b0, prev, have_prev, t + 1, nb, c0, R, keep, wacc);
+                pipe_step<OPEN, true, false, MODE, LINES, false, POLY>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R, keep, wacc);
+                pipe_step<OPEN, true, false, MODE, LINES, false, POLY>(pl, st, r, h, pi, b0, prev, have_prev, t + 1, nb, c0, R, keep, wacc);
             }
-            if (t < F) pipe_step<OPEN, true, false, MODE, false, false, POLY>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R, keep, wacc);
+            if (t < F) pipe_step<OPEN, true, false, MODE, LINES, false, POLY>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R, keep, wacc);
         }
         pending = 4;
     }
@@ -473,11 +566,17 @@ __device__ __forceinline__ Acc pipe_pass(uint4 *pl, const Stream &st, const Mul 
                     k == 1 ? b1.q1 : k == 2 ? b2.q1 : k == 3 ? b3.q1 : b0.q1,
                     k == 1 ? b1.q2 : k == 2 ? b2.q2 : k == 3 ? b3.q2 : b0.q2,
                     k == 1 ? b1.q3 : k == 2 ? b2.q3 : k == 3 ? b3.q3 : b0.q3};
-        if (F > 0) pipe_step<OPEN, true, true, MODE, LINES, false, POLY>(pl, st, r, h, pi, bp, prev, have_prev, F, nb, c0, R, keep, wacc);
-        else pipe_step<OPEN, false, true, MODE, LINES, false, POLY>(pl, st, r, h, pi, bp, prev, have_prev, F, nb, c0, R, keep, wacc);
+        if (F > 0) pipe_step<OPEN, true, true, MODE, LINES, false, POLY>(pl, st, r, h, pi, bp, prev, have_prev, F, nb, c0, R, keep, wacc, tl);
+        else pipe_step<OPEN, false, true, MODE, LINES, false, POLY>(pl, st, r, h, pi, bp, prev, have_prev, F, nb, c0, R, keep, wacc, tl);
         pending = bl;
     }
-    if constexpr (LINES) {
+    if constexpr (LINES && PIPE_QUAD) {
+        if (have_prev) { // no partial chunk: block F is prev (+ the tag)
+            tl->p0 = prev;
+            tl->p1 = tl->p2 = tl->p3 = make_uint4(0, 0, 0, 0);
+            tl->n = 1;
+        }
+    } else if constexpr (LINES) {
         if (have_prev) frame_store(R, 64 * F, prev); // pl + 4 F - 1
     } else if (have_prev && MODE != 1) st16<(MODE == 7 ? 4 : MODE >= 4 ? MODE - 3 : 0)>(pl + 4 * F - 1, prev);
     if constexpr (!(OPEN && (PIPE_OPEN_CUR || !POLY))) absorb_chunk(h, pi, r, pending); // the last chunk's blocks
@@ -620,13 +719,14 @@ __device__ __forceinline__ void pipe_seal_packet(const SealArgs &a, uint32_t i, 
     uint4 hdr = make_uint4(4u, head ? a.receivers[d.key_idx] : 0u, n1, n2);
     Acc h;
     Ring R{};
+    QTail tl{};
     if (lines) { // wave-uniform
         if (!head) hdr = *reinterpret_cast<const uint4 *>(frame); // block 0 is stored whole: header unchanged
         R = make_ring(frame, wbase);
 #ifdef RG_PIPE_WSTAMP
-        h = pipe_pass<false, MODE, true>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, b3, hdr, true, R, false, wst_slot(a.dbg));
+        h = pipe_pass<false, MODE, true>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, b3, hdr, true, R, false, wst_slot(a.dbg), &tl);
 #else
-        h = pipe_pass<false, MODE, true>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, b3, hdr, true, R);
+        h = pipe_pass<false, MODE, true>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, b3, hdr, true, R, false, nullptr, &tl);
 #endif
     } else {
         h = pipe_pass<false, MODE, false>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, b3, hdr, head, Ring{});
@@ -637,8 +737,10 @@ __device__ __forceinline__ void pipe_seal_packet(const SealArgs &a, uint32_t i, 
     if (j != 0) return;
     uint32_t tag[4];
     pipe_tag(h, r, P, ks + 4, tag);
-    if (lines) frame_store(pin_window(R), 16 + P, make_uint4(tag[0], tag[1], tag[2], tag[3]));
-    else *reinterpret_cast<uint4 *>(frame + 16 + P) = make_uint4(tag[0], tag[1], tag[2], tag[3]);
+    const uint4 tagv = make_uint4(tag[0], tag[1], tag[2], tag[3]);
+    if (lines && PIPE_QUAD) quad_tail_store(pin_window(R), sg.nb >> 2, tl, tagv); // the frame's last block(s)
+    else if (lines) frame_store(pin_window(R), 16 + P, tagv);
+    else *reinterpret_cast<uint4 *>(frame + 16 + P) = tagv;
     if (a.status) a.status[i] = RG_PKT_OK;
 }
 
@@ -750,20 +852,29 @@ __device__ __forceinline__ void pipe_open_packet(const OpenArgs &a, uint32_t i, 
         uint32_t tag[4];
         pipe_tag(h, r, P, ks + 4, tag);
         const uint32_t df = (tag[0] ^ want.x) | (tag[1] ^ want.y) | (tag[2] ^ want.z) | (tag[3] ^ want.w);
-        if constexpr (L) (void)pipe_pass<true, 0, true, false>(pl, stm, r, sg.nb, sg.c0, p0, p1, p2, p3, hdr, true, make_ring(frame, wbase), df != 0);
-        else (void)pipe_pass<true, 0, false, false>(pl, stm, r, sg.nb, sg.c0, p0, p1, p2, p3, make_uint4(0, 0, 0, 0), false, Ring{}, df != 0);
+        if constexpr (L) {
+            const Ring Rm = make_ring(frame, wbase);
+            QTail tl{};
+            (void)pipe_pass<true, 0, true, false>(pl, stm, r, sg.nb, sg.c0, p0, p1, p2, p3, hdr, true, Rm, df != 0, nullptr, &tl);
+            if constexpr (PIPE_QUAD) quad_tail_store(pin_window(Rm), sg.nb >> 2, tl, want);
+        } else (void)pipe_pass<true, 0, false, false>(pl, stm, r, sg.nb, sg.c0, p0, p1, p2, p3, make_uint4(0, 0, 0, 0), false, Ring{}, df != 0);
         return df;
     };
     const uint32_t diff = lines ? verify_decrypt(std::true_type{}) : verify_decrypt(std::false_type{});
     (void)key;
 #else
     Acc h;
+    QTail tl{};
+    Ring Ro{};
+    if (lines) Ro = make_ring(frame, wbase);
 #ifdef RG_PIPE_WSTAMP
-    if (lines) h = pipe_pass<true, 0, true>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, b3, hdr, true, make_ring(frame, wbase), false, wst_slot(a.dbg));
+    if (lines) h = pipe_pass<true, 0, true>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, b3, hdr, true, Ro, false, wst_slot(a.dbg), &tl);
 #else
-    if (lines) h = pipe_pass<true, 0, true>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, b3, hdr, true, make_ring(frame, wbase)); // header unchanged
+    if (lines) h = pipe_pass<true, 0, true>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, b3, hdr, true, Ro, false, nullptr, &tl); // header unchanged
 #endif
     else h = pipe_pass<true, 0, false>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, b3, make_uint4(0, 0, 0, 0), false, Ring{});
+    // the frame's last block(s), the received tag written back unchanged
+    if (lines && PIPE_QUAD) quad_tail_store(pin_window(Ro), sg.nb >> 2, tl, want);
     h = combine_segments(h, r, sg.after, G);
     uint32_t tag[4];
     pipe_tag(h, r, P, ks + 4, tag);
