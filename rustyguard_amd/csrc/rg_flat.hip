@@ -95,11 +95,25 @@ struct FlatLds {
     uint32_t ch[64][5];           // scratch: the lanes' last-packet markers (stride 5)
 };
 constexpr uint32_t kLiveBit = 0x80000000u, kFail = 2u;
+// workgroup-cooperative unit search (round 3): groups of kCoopGroup packets, work of a packet
+// RG_FLAT_WPKT + RG_FLAT_WCHK x chunks (a key block costs less than its share of the lanes' chunk steps:
+// see flat_coop_ok and DESIGN.md §4.6)
+#ifndef RG_FLAT_COOP
+#define RG_FLAT_COOP 1
+#endif
+#ifndef RG_FLAT_WPKT
+#define RG_FLAT_WPKT 1
+#endif
+#ifndef RG_FLAT_WCHK
+#define RG_FLAT_WCHK 8
+#endif
+constexpr uint32_t kCoopGroup = 4096;
+constexpr uint32_t kCoopLds = 256; // shared slots: wave totals, cut counts
 #ifndef RG_FLAT_WAVES
 #define RG_FLAT_WAVES 4 // waves per workgroup, one workgroup per CU: one wave per SIMD
 #endif
 constexpr uint32_t kFlatWaves = RG_FLAT_WAVES;
-static_assert(kFlatWaves * sizeof(FlatLds) <= kLdsPerCu, "flat LDS image");
+static_assert(kFlatWaves * sizeof(FlatLds) + 256 <= kLdsPerCu, "flat LDS image");
 
 struct FChunk {
     uint4 q0, q1, q2, q3;
@@ -357,6 +371,8 @@ struct FlatArgs {
     uint4 *junk;     // [waves][64 lanes][4] sink of the stores that are not payload
     uint32_t units;  // = waves of the grid
     uint32_t balance; // 1: units of equal work inside each group of kFlatGroup packets; 0: equal packet counts
+    uint32_t coop;    // units cut by the workgroup inside groups of kCoopGroup packets (flat_coop_ok)
+    uint32_t wpkt, wchk; // coop work of a packet: wpkt + wchk x its 64-byte chunks
 };
 
 // Descriptor-level checks of a packet (the reference's order, see rg_pipe.hip):
@@ -430,7 +446,89 @@ template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) voi
     for (uint32_t u = wid; u < NU; u += nw) {
         // ---- this unit's packets [s, e) and, when it is read from a group, its first sub-unit staged
         uint32_t s0, e0, staged = 0;
-        if ((uint64_t)n <= (uint64_t)kFlatGroup * NU) {
+        if (A.coop) {
+            // Round 3: the four waves of a workgroup cut their four units together, inside a group of
+            // kCoopGroup (4096) packets, each wave scanning 1024 of them (16 per lane, as the one-wave
+            // search does with its 1024-packet group): per-group variations of the total work are
+            // then averaged over four times as many packets, and the units' chunk counts stay inside
+            // six 64-lane steps at config 3.  Host-checked (flat_coop_ok): one unit per wave, the
+            // group's units a multiple of four, n a multiple of kCoopGroup.
+            uint32_t *const sh = reinterpret_cast<uint32_t *>(flat_lds + kFlatWaves * sizeof(FlatLds));
+            const uint32_t kgc = uniform_u32(A.coop);               // units per group
+            const uint32_t g = uniform_u32(u / kgc), j = uniform_u32(u - g * kgc), j0 = j - wv;
+            const uint32_t gb = g * kCoopGroup + wv * kFlatGroup;    // this wave's 1024 packets
+            rg_pkt_desc d[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) d[q] = desc[gb + lane + 64 * q];
+            uint32_t *const tw = &L.kr[0][0];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) tw[lane + 64 * q] = A.wpkt + A.wchk * (flat_work(d[q], OPEN) - 1u);
+            wave_sync();
+            uint32_t e[16];
+            {
+                const uint4 *t4 = reinterpret_cast<const uint4 *>(tw) + 4 * lane;
+                const uint4 a0 = t4[0], a1 = t4[1], a2 = t4[2], a3 = t4[3];
+                e[0] = a0.x; e[1] = a0.y; e[2] = a0.z; e[3] = a0.w;
+                e[4] = a1.x; e[5] = a1.y; e[6] = a1.z; e[7] = a1.w;
+                e[8] = a2.x; e[9] = a2.y; e[10] = a2.z; e[11] = a2.w;
+                e[12] = a3.x; e[13] = a3.y; e[14] = a3.z; e[15] = a3.w;
+            }
+            wave_sync();
+#pragma unroll
+            for (int q = 1; q < 16; ++q) e[q] += e[q - 1];
+            const uint32_t lsum = e[15];
+            const uint32_t lx = wave_scan_incl(lsum) - lsum;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) e[q] += lx;
+            if (lane == 0) sh[wv] = lane63(lx + lsum); // this wave's total
+            __syncthreads();
+            uint32_t off = 0, tot = 0; // work of the group's packets before this wave's; the group's
+#pragma unroll
+            for (uint32_t w = 0; w < kFlatWaves; ++w) {
+                const uint32_t tw_ = uniform_u32(sh[w]);
+                off += w < wv ? tw_ : 0u;
+                tot += tw_;
+            }
+            // the workgroup's five cut points, as packet counts of this wave's quarter below each target
+            // (midpoint rule: packet i goes to the unit its work midpoint falls in)
+            uint32_t cnt[5];
+            {
+                uint32_t t2[5];
+#pragma unroll
+                for (int b = 0; b < 5; ++b) t2[b] = uniform_u32(2 * (uint32_t)fdiv((uint64_t)tot * (j0 + b), kgc));
+                const uint32_t sh1 = wave_shr1(e[15]);
+                uint32_t prev = lane ? sh1 : 0u;
+                uint32_t c[5] = {0, 0, 0, 0, 0};
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    const uint32_t mid2 = e[q] + prev + 2 * off;
+                    prev = e[q];
+#pragma unroll
+                    for (int b = 0; b < 5; ++b) c[b] += mid2 < t2[b] ? 1u : 0u;
+                }
+#pragma unroll
+                for (int b = 0; b < 5; ++b) cnt[b] = lane63(wave_scan_incl(c[b]));
+            }
+            if (lane == 0) {
+#pragma unroll
+                for (int b = 0; b < 5; ++b) sh[8 + 5 * wv + b] = cnt[b];
+            }
+            __syncthreads();
+            uint32_t cut0 = 0, cut1 = 0;
+#pragma unroll
+            for (uint32_t w = 0; w < kFlatWaves; ++w) {
+                cut0 += uniform_u32(sh[8 + 5 * w + wv]);
+                cut1 += uniform_u32(sh[8 + 5 * w + wv + 1]);
+            }
+            if (j == 0) cut0 = 0;
+            if (j + 1 == kgc) cut1 = kCoopGroup;
+            __syncthreads(); // the shared slots are read before any wave reuses them
+            // the first sub-unit is staged from memory below (L2-resident: this workgroup just read it);
+            // staging it from the four waves' registers into each other's images measured 2x slower
+            s0 = g * kCoopGroup + cut0;
+            e0 = g * kCoopGroup + cut1;
+            wave_sync(); // the key-record scratch is read before the sub-unit is staged into it
+        } else if ((uint64_t)n <= (uint64_t)kFlatGroup * NU) {
             // Units of group g (kFlatGroup packets): those whose nominal start u n / NU falls in it;
             // inside the group the cut points split its work evenly (midpoint rule).  No global
             // pass: the wave reads the group's descriptors (16 per lane) and scans them itself.
@@ -962,6 +1060,17 @@ template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) voi
 #undef RG_FLAT_MARK
 }
 
+// The workgroup-cooperative unit search applies when every workgroup's four units lie in one group of
+// kCoopGroup packets: n a multiple of kCoopGroup and units x kCoopGroup / n a multiple of four.
+// Returns the units per group (0: the one-wave search).
+static uint32_t flat_coop_ok(uint32_t n, uint32_t units, bool balance) {
+    if (!RG_FLAT_COOP || !balance || kFlatWaves != 4 || n < kCoopGroup || n % kCoopGroup != 0) return 0;
+    const uint64_t x = (uint64_t)units * kCoopGroup;
+    if (x % n != 0) return 0;
+    const uint64_t kgc = x / n;
+    return kgc % 4 == 0 && kgc >= 4 ? (uint32_t)kgc : 0u;
+}
+
 hipError_t launch_flat(const SealArgs *sa, const OpenArgs *oa, bool balance, uint4 *junk, int cus, hipStream_t s) {
     const uint32_t n = sa ? sa->n : oa->n;
     if (n == 0) return hipSuccess;
@@ -972,7 +1081,10 @@ hipError_t launch_flat(const SealArgs *sa, const OpenArgs *oa, bool balance, uin
     A.units = blocks * kFlatWaves;
     A.junk = junk;
     A.balance = balance ? 1u : 0u;
-    const uint32_t lds = kFlatWaves * (uint32_t)sizeof(FlatLds);
+    A.coop = flat_coop_ok(n, A.units, balance);
+    A.wpkt = RG_FLAT_WPKT;
+    A.wchk = RG_FLAT_WCHK;
+    const uint32_t lds = kFlatWaves * (uint32_t)sizeof(FlatLds) + kCoopLds;
     const bool win = (sa ? sa->buf_len : oa->buf_len) < 0x7FFFFFF0ull; // frame offsets below 2 GiB
     if (sa && win) hipLaunchKernelGGL((flat_kernel<false, true>), dim3(blocks), dim3(64 * kFlatWaves), lds, s, A);
     else if (sa) hipLaunchKernelGGL((flat_kernel<false, false>), dim3(blocks), dim3(64 * kFlatWaves), lds, s, A);
@@ -984,7 +1096,7 @@ hipError_t launch_flat(const SealArgs *sa, const OpenArgs *oa, bool balance, uin
 uint32_t flat_junk_bytes(int cus) { return (uint32_t)(cus > 0 ? cus : 1) * kFlatWaves * 64 * 64; }
 
 hipError_t prepare_flat_kernels() {
-    const int lds = (int)(kFlatWaves * sizeof(FlatLds));
+    const int lds = (int)(kFlatWaves * sizeof(FlatLds) + kCoopLds);
     const void *f[4] = {(const void *)flat_kernel<false, true>, (const void *)flat_kernel<false, false>,
                         (const void *)flat_kernel<true, true>, (const void *)flat_kernel<true, false>};
     hipError_t e = hipSuccess;

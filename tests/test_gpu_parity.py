@@ -425,6 +425,41 @@ def test_flat_subunits_vs_oracle(engine, plan, per_unit):
     _reset(engine)
 
 
+@pytest.mark.parametrize("n", [16384, 65536])
+def test_flat_coop_search_vs_oracle(engine, n):
+    """Round 3: when n is a multiple of 4096 and the units of a 4096-packet group are a multiple of four
+    (CUs x 4 units), the four waves of a workgroup cut their units together (rg_flat.hip, A.coop).
+    Random sizes 0..2048 B over three keys, 40 forged frames: every byte and status against the
+    oracle."""
+    import torch
+
+    units = 4 * torch.cuda.get_device_properties(0).multi_processor_count
+    if (units * 4096) % n or ((units * 4096) // n) % 4:
+        pytest.skip("the cooperative search does not apply at this CU count")
+    engine.set_staged(3)
+    engine.set_plan(1)
+    rng = np.random.default_rng(n)
+    keys, rec, desc, ctr, buf = _random_batch(rng, n, nkeys=3)
+    want = buf.copy()
+    oracle.seal_batch(keys, rec, desc, ctr, want, nthreads=8)
+    got, st = _gpu_seal(engine, keys, rec, desc, ctr, buf)
+    assert (st == aead.PKT_OK).all()
+    assert np.array_equal(got, want)
+    od = desc.copy()
+    od["len"] += 32
+    forged = rng.choice(n, 40, replace=False)
+    tampered = got.copy()
+    for i in forged:
+        tampered[int(od[i]["offset"]) + int(od[i]["len"]) - 1] ^= 1
+    back, st, co = _gpu_open(engine, keys, od, tampered)
+    want_back = tampered.copy()
+    wst, wctr = oracle.open_batch(keys, od, want_back, nthreads=8)
+    assert np.array_equal(st, wst) and (wst[forged] == oracle.DECRYPT_ERR).all()
+    assert np.array_equal(co[wst == 0], wctr[wst == 0])
+    assert np.array_equal(back, want_back)
+    _reset(engine)
+
+
 @pytest.mark.parametrize("mode", MODES, ids=_mode_id)
 def test_open_failures_leave_frames_untouched(engine, mode):
     _configure(engine, mode)
