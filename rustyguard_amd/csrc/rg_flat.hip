@@ -493,21 +493,33 @@ template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) voi
             // (midpoint rule: packet i goes to the unit its work midpoint falls in)
             uint32_t cnt[5];
             {
+                // targets 2 tot (j0 + b) / kgc: any rounding is fine as long as every workgroup of the
+                // group computes the same function of (tot, boundary index) -- they do, so a boundary
+                // shared by two workgroups lands on the same packet in both
+                const double per = (double)tot * __builtin_amdgcn_rcp((double)kgc);
                 uint32_t t2[5];
 #pragma unroll
-                for (int b = 0; b < 5; ++b) t2[b] = uniform_u32(2 * (uint32_t)fdiv((uint64_t)tot * (j0 + b), kgc));
+                for (int b = 0; b < 5; ++b) t2[b] = uniform_u32(2 * (uint32_t)(per * (double)(j0 + b)));
                 const uint32_t sh1 = wave_shr1(e[15]);
-                uint32_t prev = lane ? sh1 : 0u;
-                uint32_t c[5] = {0, 0, 0, 0, 0};
+                const uint32_t prev0 = lane ? sh1 : 0u;
+                const uint32_t lo2 = 2 * off, hi2 = 2 * (off + uniform_u32(sh[wv]));
 #pragma unroll
-                for (int q = 0; q < 16; ++q) {
-                    const uint32_t mid2 = e[q] + prev + 2 * off;
-                    prev = e[q];
+                for (int b = 0; b < 5; ++b) {
+                    // this wave's packets have midpoints in [lo2, hi2): a target outside needs no count
+                    if (t2[b] <= lo2) {
+                        cnt[b] = 0;
+                    } else if (t2[b] > hi2) {
+                        cnt[b] = kFlatGroup;
+                    } else {
+                        uint32_t prev = prev0, c = 0;
 #pragma unroll
-                    for (int b = 0; b < 5; ++b) c[b] += mid2 < t2[b] ? 1u : 0u;
+                        for (int q = 0; q < 16; ++q) {
+                            c += e[q] + prev + lo2 < t2[b] ? 1u : 0u;
+                            prev = e[q];
+                        }
+                        cnt[b] = lane63(wave_scan_incl(c));
+                    }
                 }
-#pragma unroll
-                for (int b = 0; b < 5; ++b) cnt[b] = lane63(wave_scan_incl(c[b]));
             }
             if (lane == 0) {
 #pragma unroll
