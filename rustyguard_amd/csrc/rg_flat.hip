@@ -115,6 +115,13 @@ constexpr uint32_t kCoopLds = 256; // shared slots: wave totals, cut counts
 constexpr uint32_t kFlatWaves = RG_FLAT_WAVES;
 static_assert(kFlatWaves * sizeof(FlatLds) + 256 <= kLdsPerCu, "flat LDS image");
 
+#ifndef RG_FLAT_NTLOAD
+#define RG_FLAT_NTLOAD 0
+#endif
+#ifndef RG_FLAT_ALIGN
+#define RG_FLAT_ALIGN 0
+#endif
+
 struct FChunk {
     uint4 q0, q1, q2, q3;
 };
@@ -126,10 +133,18 @@ __device__ __forceinline__ void fload(FChunk &c, const uint4 *pl, uint32_t t, ui
 #ifdef RG_FLAT_ABL_NOLOAD // diagnostics only: no payload loads (output invalid)
     c.q0.x ^= b; c.q1.y ^= b; c.q2.z ^= b; c.q3.w ^= last; return;
 #endif
+#if RG_FLAT_NTLOAD // streaming loads: the payload is read once, so its lines go first in L2
+    auto nt = [&](uint32_t i) {
+        const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(pl + min(i, last)));
+        return make_uint4(v.x, v.y, v.z, v.w);
+    };
+    c.q0 = nt(b + 0); c.q1 = nt(b + 1); c.q2 = nt(b + 2); c.q3 = nt(b + 3);
+#else
     c.q0 = pl[min(b + 0, last)];
     c.q1 = pl[min(b + 1, last)];
     c.q2 = pl[min(b + 2, last)];
     c.q3 = pl[min(b + 3, last)];
+#endif
 }
 
 // a lane's position in the sub-unit's chunk stream
@@ -200,6 +215,11 @@ struct FLane {
     uint32_t pe;
     int pb;
     uint32_t rn[4]; // seal: r of the compute cursor's packet, kept from its key read for the pk switch
+#if RG_FLAT_ALIGN
+    uint4 d1, d2, d3;  // pieces 1..3 of the previous chunk waiting for their segment's other part
+    const uint4 *dd;   // where that chunk goes
+    uint32_t dm;       // which of them wait (bits 1..3)
+#endif
 };
 
 // one square-and-multiply step of the carry power (pb is wave-uniform)
@@ -266,10 +286,31 @@ __device__ __forceinline__ void flat_step(FLane &s, FChunk &b, uint32_t j, FlatL
     if (s.cur.k == 0xFFFFFFFFu)
 #endif
     {
+#if RG_FLAT_ALIGN
+        // 64-byte segments whole within one step: a chunk at 16-byte phase ph straddles two segments, so
+        // its pieces 4 - ph .. 3 wait for the next chunk's step and are stored just before its first
+        // pieces (a packet's last chunk and the lane's last step store everything).  Stores one step
+        // apart into the same segment leave it partially written in L2, where the payload reads evict it
+        // (written back twice: profiles/r3_cfg3_traffic_attribution.txt).
+        const uint32_t ph = (uint32_t)(reinterpret_cast<uintptr_t>(dst) >> 4) & 3u;
+        const bool fin = s.cur.t + 1 == s.cur.c || j + 1 == s.nsteps;
+        const uint32_t head = fin ? 4u : 4u - ph; // pieces stored now (ph = 0: all)
+        fstore<WIN>(FS, s.dd + 1, (s.dm & 2u) != 0, 1, s.d1);
+        fstore<WIN>(FS, s.dd + 2, (s.dm & 4u) != 0, 2, s.d2);
+        fstore<WIN>(FS, s.dd + 3, (s.dm & 8u) != 0, 3, s.d3);
+        fstore<WIN>(FS, dst + 0, cnt > 0, 0, x.q0);
+        fstore<WIN>(FS, dst + 1, cnt > 1 && head > 1, 1, x.q1);
+        fstore<WIN>(FS, dst + 2, cnt > 2 && head > 2, 2, x.q2);
+        fstore<WIN>(FS, dst + 3, cnt > 3 && head > 3, 3, x.q3);
+        s.dm = (cnt > 1 && head <= 1 ? 2u : 0u) | (cnt > 2 && head <= 2 ? 4u : 0u) | (cnt > 3 && head <= 3 ? 8u : 0u);
+        s.dd = dst;
+        s.d1 = x.q1; s.d2 = x.q2; s.d3 = x.q3;
+#else
         fstore<WIN>(FS, dst + 0, cnt > 0, 0, x.q0);
         fstore<WIN>(FS, dst + 1, cnt > 1, 1, x.q1);
         fstore<WIN>(FS, dst + 2, cnt > 2, 2, x.q2);
         fstore<WIN>(FS, dst + 3, cnt > 3, 3, x.q3);
+#endif
     }
     if constexpr (OPEN) {
         if (active && s.cur.t + 1 == s.cur.c) { // the packet's last chunk: its final piece
@@ -892,6 +933,11 @@ template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) voi
             s.pi = FChunk{};
             s.pi_cnt = 0;
             s.pk = s.cur.k;
+#if RG_FLAT_ALIGN
+            s.d1 = s.d2 = s.d3 = make_uint4(0, 0, 0, 0);
+            s.dd = s.cur.pl;
+            s.dm = 0;
+#endif
             // the carry's power: the packet of the lane's last chunk, when it goes on past the lane
             {
                 s.pe = 0;

@@ -9,6 +9,10 @@
 //   wr_frame  : lane-per-frame 16-B stores, whole frames
 //   wr_split  : lane-per-frame, the frame's bytes [0,16) and [16,1536) written by two
 //               kernels (the header / payload split of a seal), both counted
+//   ph_{wr,rd}_{0,16} [spin] : round 3 -- the flattened kernel's pattern: one wave per SIMD, each lane
+//               owns 1536 contiguous bytes at phase 0 or 16 from the 64-B grid and moves 64 B per step
+//               (four 16-B accesses), with `spin` x 1000 VALU instructions between steps; does a
+//               16-B phase cost HBM bytes when the halves of a 64-B segment arrive one step apart?
 // Prints {"kernel", "bytes_read", "bytes_written", "us"}; bytes are what the kernel
 // touches, so counter / bytes is the calibration factor.
 #include <hip/hip_runtime.h>
@@ -65,6 +69,31 @@ __global__ __launch_bounds__(256) void wr_frame(uint4 *p, uint32_t q0, uint32_t 
     for (uint32_t i = q0; i < q1; ++i) q[i] = make_uint4(f, i, 2, 3);
 }
 
+constexpr uint32_t kPhSteps = 24, kPhLanes = 65536; // 100.7 MB per launch, 1024 waves
+template <uint32_t PH, bool WR> __global__ __launch_bounds__(256) void k_phase(uint4 *p, uint4 *sink, int spin) {
+    const uint32_t gl = blockIdx.x * 256 + threadIdx.x;
+    uint4 *q = reinterpret_cast<uint4 *>(reinterpret_cast<uint8_t *>(p) + PH + (size_t)gl * 64 * kPhSteps);
+    uint32_t a = gl, b = gl ^ 7, c = gl * 3, d = 11;
+    uint4 acc = make_uint4(0, 0, 0, 0);
+    for (uint32_t t = 0; t < kPhSteps; ++t) {
+        for (int k = 0; k < 250 * spin; ++k)
+            asm volatile("v_add_u32 %0, %0, %1\n\tv_xor_b32 %1, %1, %2\n\tv_alignbit_b32 %2, %2, %2, 7\n\tv_add_u32 %3, %3, %0"
+                         : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+        if (WR) {
+            q[4 * t + 0] = make_uint4(a, t, 0, 1);
+            q[4 * t + 1] = make_uint4(b, t, 1, 2);
+            q[4 * t + 2] = make_uint4(c, t, 2, 3);
+            q[4 * t + 3] = make_uint4(d, t, 3, 4);
+        } else {
+            for (int i = 0; i < 4; ++i) {
+                const uint4 v = q[4 * t + i];
+                acc.x ^= v.x; acc.y ^= v.y ^ a; acc.z ^= v.z; acc.w ^= v.w;
+            }
+        }
+    }
+    if ((acc.x & acc.y & acc.z & acc.w) == 0xFFFFFFFFu || (a ^ b ^ c ^ d) == 0x12345678u) sink[0] = acc;
+}
+
 int main(int argc, char **argv) {
     const char *k = argc > 1 ? argv[1] : "rd_coal";
     uint4 *buf, *sink;
@@ -95,6 +124,16 @@ int main(int argc, char **argv) {
         hipLaunchKernelGGL(wr_frame, dim3(fblocks), dim3(256), 0, 0, buf, 0u, 1u);
         hipLaunchKernelGGL(wr_frame, dim3(fblocks), dim3(256), 0, 0, buf, 1u, kQ);
         wr = (size_t)kFrames * kStride;
+    } else if (!strncmp(k, "ph_", 3)) {
+        const int spin = argc > 2 ? atoi(argv[2]) : 1;
+        const bool w = !strncmp(k, "ph_wr", 5), p16 = strstr(k, "_16") != nullptr;
+        void (*f)(uint4 *, uint4 *, int) = w ? (p16 ? k_phase<16, true> : k_phase<0, true>)
+                                             : (p16 ? k_phase<16, false> : k_phase<0, false>);
+        const int lds = 160 * 1024; // one 4-wave workgroup per CU: one wave per SIMD
+        CHECK(hipFuncSetAttribute((const void *)f, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+        CHECK(hipEventRecord(e0, 0)); // (re-recorded: the attribute call is not timed)
+        hipLaunchKernelGGL(f, dim3(kPhLanes / 256), dim3(256), lds, 0, buf, sink, spin);
+        (w ? wr : rd) = (size_t)kPhLanes * 64 * kPhSteps;
     } else {
         fprintf(stderr, "unknown kernel %s\n", k);
         return 2;

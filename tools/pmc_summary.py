@@ -11,5 +11,5 @@ for d in sys.argv[1:]:
         for r in csv.DictReader(open(f)):
             agg[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
         for k, v in agg.items():
-            if any(x in k for x in ("seal", "open", "chacha", "tile", "pipe", "flat", "rd_", "wr_")):
+            if any(x in k for x in ("seal", "open", "chacha", "tile", "pipe", "flat", "rd_", "wr_", "k_phase")):
                 print(d, k[:48], {c: round(sum(x) / len(x), 1) for c, x in sorted(v.items())})
