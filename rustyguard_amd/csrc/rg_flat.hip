@@ -85,9 +85,12 @@ __device__ __forceinline__ uint32_t flat_work(const rg_pkt_desc &d, bool open) {
 #define RG_FLAT_MAX_PK 128 // packets per sub-unit (phase A holds their key loads in registers)
 #endif
 constexpr uint32_t kFlatMaxPk = RG_FLAT_MAX_PK;
+#ifndef RG_FLAT_KR
+#define RG_FLAT_KR 16 // key-record stride in dwords (20: lanes reading consecutive packets' rows hit distinct banks)
+#endif
 struct FlatLds {
     uint4 rec[kFlatMaxPk + 1];    // {offset lo, offset hi, nb | kLiveBit, cs}; rec[m].w = D
-    uint32_t kr[kFlatMaxPk][16];  // key[8], counter lo/hi, r[4] (unclamped), desc len, desc key_idx
+    uint32_t kr[kFlatMaxPk][RG_FLAT_KR]; // key[8], counter lo/hi, r[4] (unclamped), desc len, desc key_idx
     uint32_t sw[kFlatMaxPk][4];   // seal: s; open: tag - s (mod 2^128)
     uint32_t hs[kFlatMaxPk][8];   // [6] kFail (open: the tag did not verify)
     unsigned long long ps[kFlatMaxPk][5]; // sum of the packet's Horner pieces, radix 2^32 limbs (LDS atomics)
