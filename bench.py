@@ -667,8 +667,10 @@ def main():
         b.open(stream=stream, counters_out=False)
         e[3].record(stream)
     torch.cuda.synchronize()
-    seal_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / reps
-    open_ms = sum(e[2].elapsed_time(e[3]) for e in evs) / reps
+    seal_each = sorted(e[0].elapsed_time(e[1]) for e in evs)
+    open_each = sorted(e[2].elapsed_time(e[3]) for e in evs)
+    seal_ms = sum(seal_each) / reps
+    open_ms = sum(open_each) / reps
     if args.verify:
         assert (b.status[: w.n] == 0).all().item(), "open failed in the kernel-timing pass"
     cold = cold_cache_timing(eng, w, b, stream, args.verify) if args.cold and w.buf_bytes < MALL_BYTES else None
@@ -729,6 +731,8 @@ def main():
         "mpkt_s": round(total_pkts / tmax / 1e6, 3),
         "seal_ms": round(seal_ms, 5),
         "open_ms": round(open_ms, 5),
+        "seal_ms_median": round(seal_each[reps // 2], 5),  # the median beside the mean
+        "open_ms_median": round(open_each[reps // 2], 5),
         "seal_gib_s": round(payload / (seal_ms / 1e3) / 2**30 * world, 3),
         "open_gib_s": round(payload / (open_ms / 1e3) / 2**30 * world, 3),
         "seal_mpkt_s": round(w.n / (seal_ms / 1e3) / 1e6 * world, 3),
