@@ -911,6 +911,9 @@ __device__ __forceinline__ void pipe_stamp(uint64_t *dbg, uint64_t t0, uint64_t 
         (void)marks;
 #elif !defined(RG_TILE_MARKS)
         o[0] = t1 - t0; o[1] = marks[0] ? marks[0] - r0 : 0; o[2] = marks[1] ? marks[1] - r0 : 0; o[3] = 0;
+#ifdef RG_PIPE_LB2 // co-residency record: HW_ID (wave, SIMD, CU, SH, SE) and XCC_ID
+        o[3] = ((uint64_t)(uint32_t)__builtin_amdgcn_s_getreg(0xF814) << 32) | (uint32_t)__builtin_amdgcn_s_getreg(0xF804);
+#endif
         o[5] = 4;
 #else
         o[0] = marks[0];
@@ -1018,7 +1021,12 @@ __device__ __forceinline__ void pipe_walk(uint32_t n, uint32_t lg0, const PipePl
 }
 
 // flags: bits 0-1 log2 lanes per packet (without a plan), kPipeLinesFlag: the LDS ring is reserved
-template <int MODE> __global__ __launch_bounds__(256) void pipe_seal_kernel(SealArgs a, uint32_t flags, PipePlan pp) {
+#ifdef RG_PIPE_LB2
+#define RG_PIPE_LB __launch_bounds__(256, 2)
+#else
+#define RG_PIPE_LB __launch_bounds__(256)
+#endif
+template <int MODE> __global__ RG_PIPE_LB void pipe_seal_kernel(SealArgs a, uint32_t flags, PipePlan pp) {
     const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
     uint64_t marks[2] = {0, 0};
     const bool lines = RG_PIPE_LINES && (flags & kPipeLinesFlag) != 0;
@@ -1028,7 +1036,7 @@ template <int MODE> __global__ __launch_bounds__(256) void pipe_seal_kernel(Seal
     if (a.dbg) pipe_stamp(a.dbg, t0, r0, marks);
 }
 
-__global__ __launch_bounds__(256) void pipe_open_kernel(OpenArgs a, uint32_t flags, PipePlan pp) {
+__global__ RG_PIPE_LB void pipe_open_kernel(OpenArgs a, uint32_t flags, PipePlan pp) {
     const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
     uint64_t marks[2] = {0, 0};
     const bool lines = RG_PIPE_LINES && (flags & kPipeLinesFlag) != 0;
