@@ -42,6 +42,16 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, MI355X_MICROARCH.md "Chip-level para
 # occupancy): ChaCha20 keystream bytes/s over the whole chip, and clamped Poly1305 bytes/s
 CHACHA_PEAK_GBS = 2610.0
 POLY_PEAK_GBS = 15765.0
+# ... measured at these shader clocks (profiles/r1c_microbench.json "clock": 2.25-2.41 GHz, 2.39 at the best
+# occupancy).  The AEAD kernels hold a lower clock under their own load; their clocks from per-wave
+# s_memtime / s_memrealtime stamps of diagnostic builds (the product library has no stamps):
+MICRO_CLOCK_GHZ = 2.39
+KERNEL_CLOCK_GHZ = {
+    "cfg2": (2.135, "profiles/r4_cfg2_twowave.txt (one wave per SIMD, 2.130-2.137 GHz)"),
+    "cfg3": (2.18, "profiles/r3_valu_cfg3.json (flattened kernel stamps)"),
+    "cfg4": (2.09, "profiles/r3_valu_cfg4.json (GRBM quotient over a ~1 ms dispatch)"),
+    "cfg5": (2.09, "as cfg4: the same tile kernel on 8 Mi packets"),
+}
 
 
 def valu_ceiling_gbs(desc_len, is_open: bool) -> float:
@@ -78,6 +88,9 @@ def parse():
                     help="CPU baseline budget: port and OpenSSL, 1 thread and all cores, 5 runs each (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="all-core thread count (0 = this host's share)")
     ap.add_argument("--e2e", action="store_true", help="also time the pinned host->GPU->host path")
+    ap.add_argument("--single-process", action="store_true",
+                    help="one process and one thread drive all --gpus N GPUs (rg_group: config 5's split, "
+                         "rg_{seal,open}_batch_dev_multi) instead of one rank per GPU")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch/validate the ranks, print each rank's plan as JSON and exit before any GPU work")
     ap.add_argument("--forged", default="0.01,0.1",
@@ -448,6 +461,34 @@ def strict_check(w, b, stream):
         assert np.array_equal(fr[16:16 + len(exp[k])], exp[k]), f"open did not restore packet {k}"
 
 
+def bench_single_process(args):
+    """--single-process: the bench line of one process driving --gpus N GPUs through an rg_group."""
+    import torch
+
+    if "WORLD_SIZE" in os.environ and os.environ["WORLD_SIZE"] != "1":
+        print("bench.py: --single-process is one process; do not launch it under torch.distributed.run",
+              file=sys.stderr)
+        sys.exit(2)
+    share = os.environ.get("RG_BENCH_SHARE_GPU") == "1"
+    ndev = torch.cuda.device_count()
+    if not share and ndev < args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but {ndev} GPU(s) visible", file=sys.stderr)
+        sys.exit(2)
+    devices = [0] * args.gpus if share else list(range(args.gpus))
+    sp = single_process_run(devices, args.steps, args.warmup, args.verify)
+    out = {"metric": METRIC, "value": sp["gib_s"], "unit": "GiB/s", "n_gpus": args.gpus, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": sp["ms_per_step"], "higher_is_better": True, "scaling": "strong",
+           "vs_baseline": None, "dtype": "u32",
+           "data": "synthetic (SplitMix64 payload, fixed-seed keys; rustyguard_amd/workloads.py)",
+           "config": {"workload": "cfg5: " + __import__("rustyguard_amd.workloads", fromlist=["CONFIGS"]).CONFIGS["cfg5"]
+                                  + f" (strong split over {args.gpus} GPU(s), one process, one thread)",
+                      "parallelism": f"group{args.gpus} (one rg_ctx per GPU, no collective)"},
+           "mpkt_s": sp["mpkt_s"], "single_process": sp}
+    if share:
+        out["rehearsal"] = f"RG_BENCH_SHARE_GPU=1: {args.gpus} contexts on one GPU -- not a scaling measurement"
+    print(json.dumps(out), flush=True)
+
+
 def run_legs(rank: int, world: int, workload: str, args) -> list:
     """What a rank runs after the timed steps.  With N > 1 rank 0 also makes the line self-contained:
     the same workload's whole batch on its one GPU (the strong-scaling base, `base_1gpu`) and the CPU
@@ -456,6 +497,7 @@ def run_legs(rank: int, world: int, workload: str, args) -> list:
     if rank == 0:
         if world > 1 and workload == "cfg5":
             legs.append("base_1gpu")
+            legs.append("single_process")
         if args.cpu_seconds > 0:
             legs.append("cpu_baseline")
     return legs
@@ -492,6 +534,63 @@ def base_one_gpu(eng, steps: int = 3):
     return out
 
 
+def single_process_run(devices, steps: int, warmup: int, verify: bool = True):
+    """One process and one thread driving every GPU of `devices` (include/rg_aead.h "several GPUs, one
+    thread": an rg_group with a context per device): config 5's strong split, shard k on device k, device
+    resident; a step is the seal of every shard then the open of every shard, each enqueued on the
+    shard's own stream by rg_seal_batch_dev_multi / rg_open_batch_dev_multi.  Timed by the host clock
+    between full synchronisations of every device (as the step loop above)."""
+    import torch
+
+    from rustyguard_amd import workloads
+    from rustyguard_amd.aead import Group
+    from rustyguard_amd.device import DeviceBatch
+
+    g = Group(devices)
+    n = len(devices)
+    batches, streams = [], []
+    for k, d in enumerate(devices):
+        w = workloads.build("cfg5", k, n)
+        with torch.cuda.device(d):
+            s = torch.cuda.Stream(device=d)
+            b = DeviceBatch(g.engine(k), w, device=f"cuda:{d}")
+            b.fill(stream=s)
+        batches.append(b)
+        streams.append(s)
+    seal = Group.shards([{"keys": b.keys, "receivers": b.receivers, "desc": b.desc_seal, "counters": b.counters,
+                          "buf": b.buf, "status": b.status, "stream": s} for b, s in zip(batches, streams)], True)
+    opn = Group.shards([{"keys": b.keys, "desc": b.desc_open, "buf": b.buf, "status": b.status, "stream": s}
+                        for b, s in zip(batches, streams)], False)
+
+    def sync():
+        for d in sorted(set(devices)):
+            torch.cuda.synchronize(d)
+
+    def step():
+        g.seal_dev(seal)
+        g.open_dev(opn)
+
+    for _ in range(max(warmup, 1)):
+        step()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    el = time.perf_counter() - t0
+    ok = all(bool((b.status[: b.w.n] == 0).all().item()) for b in batches) if verify else None
+    payload = sum(b.w.payload_bytes for b in batches)
+    out = {"devices": list(devices), "contexts": n, "steps": steps, "packets": sum(b.w.n for b in batches),
+           "gib_s": round(2 * payload * steps / el / 2**30, 3), "ms_per_step": round(el / steps * 1e3, 4),
+           "mpkt_s": round(2 * sum(b.w.n for b in batches) * steps / el / 1e6, 3), "statuses_ok": ok,
+           "how": "one thread: rg_seal_batch_dev_multi + rg_open_batch_dev_multi per step over an rg_group, "
+                  "host clock between full device synchronisations"}
+    del batches, seal, opn
+    g.close()
+    torch.cuda.empty_cache()
+    return out
+
+
 def load_traffic(workload: str):
     p = os.path.join(REPO, "profiles", f"pmc_{workload}.json")
     if os.path.exists(p):
@@ -505,6 +604,9 @@ def main():
     if args.gpus < 1:
         print("bench.py: --gpus must be >= 1", file=sys.stderr)
         sys.exit(2)
+    if args.single_process:
+        bench_single_process(args)
+        return
     if "WORLD_SIZE" not in os.environ and args.gpus > 1 and args.workload != "cfg1":
         sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -546,6 +648,9 @@ def main():
             coll_dev = "cpu"
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    # CPU-side barrier for the end of the run: ranks waiting for rank 0's extra legs must not hold a
+    # spinning RCCL kernel on their GPUs while rank 0's single-process leg runs there
+    cpu_group = dist.new_group(backend="gloo") if dist is not None else None
 
     from rustyguard_amd import workloads
     from rustyguard_amd.aead import Engine
@@ -758,7 +863,22 @@ def main():
                             "unit": "GB/s of payload", "frac": round(pay_gbs / ceil_gbs, 4) if ceil_gbs else None,
                             "basis": f"ChaCha20 {CHACHA_PEAK_GBS:.0f} GB/s + Poly1305 {POLY_PEAK_GBS:.0f} GB/s chip "
                                      "rates measured by tools/microbench.hip; one-time-key block per packet"}
+    clk = KERNEL_CLOCK_GHZ.get(workload)
+    if clk and ceil_gbs:
+        # the same fraction against the ceiling scaled to the clock the kernel actually holds: what share of
+        # the VALU issue rate available at that clock the seal uses
+        out["valu_roofline"]["kernel_clock_ghz"] = clk[0]
+        out["valu_roofline"]["basis_clock_ghz"] = MICRO_CLOCK_GHZ
+        out["valu_roofline"]["frac_at_kernel_clock"] = round(pay_gbs / (ceil_gbs * clk[0] / MICRO_CLOCK_GHZ), 4)
+        out["valu_roofline"]["clock_source"] = clk[1]
     if cold:
+        # the cold-cache leg's own HBM roofline fraction (the step above runs on a cache-resident batch)
+        cold_dom_ms = cold["seal_ms"] if dominant == "seal" else cold["open_ms"]
+        cold["roofline"] = {"kernel": dominant, "achieved": round(dom_alg / (cold_dom_ms / 1e3) / 1e9, 2),
+                            "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": round(dom_alg / (cold_dom_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
+        cold["vs_warm"] = {"seal": round(cold["seal_ms"] / seal_ms, 3), "open": round(cold["open_ms"] / open_ms, 3),
+                           "gib_s": round(cold["gib_s"] / (2 * payload / ((seal_ms + open_ms) / 1e3) / 2**30), 3)}
         out["cold_cache"] = cold
     if forged:
         out["forged_open"] = forged
@@ -775,6 +895,11 @@ def main():
         out["base_1gpu"] = base
         out["base_1gpu_gib_s"] = base["gib_s"]
         out["speedup"] = round(value / base["gib_s"], 3) if base["gib_s"] else None
+    if "single_process" in legs:
+        # the same split driven by ONE process and ONE thread over every GPU (rg_group), beside the
+        # one-process-per-GPU value above; the other ranks wait on a CPU barrier meanwhile
+        devs = [0] * world if share else list(range(world))
+        out["single_process"] = single_process_run(devs, max(3, min(args.steps, 10)), 2, args.verify)
     if "cpu_baseline" in legs:
         port, ossl = cpu_baselines(w, args.cpu_seconds, all_core_threads(args.cpu_threads))
         out["cpu_baseline"] = port
@@ -786,7 +911,7 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:
-        dist.barrier()  # the other ranks wait for rank 0's extra legs
+        dist.barrier(group=cpu_group)  # the other ranks wait (on the CPU) for rank 0's extra legs
         dist.destroy_process_group()
 
 

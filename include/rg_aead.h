@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define RG_ABI_VERSION 4
+#define RG_ABI_VERSION 5
 
 typedef struct rg_ctx rg_ctx;
 
@@ -190,19 +190,22 @@ int rg_set_plan(rg_ctx *ctx, int on);
  * many contiguous segments on separate waves (Poly1305 partial sums combined
  * as sum_j A_j r^{N_j}). */
 int rg_set_segments(rg_ctx *ctx, int segments);
-/* Diagnostics only (profiling the seal kernel, output is NOT a valid seal in
- * modes 1, 2, 4-6): 0 = normal, 1 = compute only (no payload loads/stores),
- * 2 = memory only, 3 = stamps, 4/5/6 = non-temporal loads / stores / both
- * (pipelined kernel). */
+/* Diagnostics.  The product library accepts only mode 0 and a NULL stamp buffer
+ * (RG_EINVAL otherwise): no context of it can emit frames that are not sealed.
+ * Diagnostic builds (-DRG_DIAG, tools/build_variant.sh, never shipped) add seal
+ * modes whose output is NOT a valid seal -- 1 compute only (no payload
+ * loads/stores), 2 memory only, 4/5/6 non-temporal loads / stores / both,
+ * 7 no payload stores, 8 line stores alternating between two lines per frame
+ * (pipelined kernel) -- and mode 3, per-wave stamps of the real kernels. */
 int rg_set_debug_mode(rg_ctx *ctx, int mode);
-/* Per-wave s_memtime stamps are written to this device buffer, 8 x u64 per
- * wave: mode 3 on the tile kernels (setup, store, dma-issue, dma-wait, chunk,
- * tail, valid, real-time ticks at 100 MHz); any non-zero mode on the
- * pipelined kernel (cycles, 0, 0, 0, start tick, 4, valid, real-time ticks);
- * mode 3 on the flattened kernel (s_memtime at the end of each phase) plus a
- * second block of rows after the first CUs x 4 (wall-clock start and end), so
- * size the buffer for 2 x CUs x 4 x 8 u64 there.  Modes 7 and 8 (pipelined seal):
- * no payload stores / line stores alternating between two lines per frame. */
+/* Diagnostic builds only: per-wave s_memtime stamps are written to this device
+ * buffer, 8 x u64 per wave: mode 3 on the tile kernels (setup, store,
+ * dma-issue, dma-wait, chunk, tail, valid, real-time ticks at 100 MHz); any
+ * non-zero mode on the pipelined kernel (cycles, two unit marks, XCC_ID << 32 |
+ * HW_ID, start tick, 4, valid, real-time ticks); mode 3 on the flattened
+ * kernel (s_memtime at the end of each phase) plus a second block of rows after
+ * the first CUs x 4 (wall-clock start and end), so size the buffer for
+ * 2 x CUs x 4 x 8 u64 there. */
 int rg_set_debug_buffer(rg_ctx *ctx, void *dev_ptr);
 
 /* ----------------------------------------- host-memory batch (blocking) */
@@ -262,9 +265,18 @@ typedef struct rg_sessions rg_sessions;
 int rg_sessions_create(rg_ctx *ctx, uint32_t capacity, rg_sessions **out);
 void rg_sessions_destroy(rg_sessions *s);
 /* Install a transport session (HandshakeState::split output, prim.rs:299-313);
- * returns the slot index (>= 0) or a negative rg_status. */
+ * returns the slot index (>= 0) or a negative rg_status.  The session is its own peer
+ * (its endpoint is its own); rg_sessions_insert_peer names the peer. */
 int rg_sessions_insert(rg_sessions *s, uint32_t local_id, uint32_t remote_id, const uint8_t send_key[32],
                        const uint8_t recv_key[32]);
+/* rg_sessions_insert for a session of peer `peer` (any caller-chosen id but RG_PEER_NONE): the
+ * peer's sessions -- its current transport and the ones a rekey leaves behind -- share one endpoint
+ * record, as the reference keeps peer.endpoint per peer (PeerState, rustyguard-core/src/lib.rs:
+ * 160-181, set by decrypt_packet at :670-671, read by the Keepalive timer, time.rs:135).  The
+ * peer's record outlives its sessions (a new session of a known peer starts with its endpoint). */
+#define RG_PEER_NONE 0xFFFFFFFFu
+int rg_sessions_insert_peer(rg_sessions *s, uint32_t local_id, uint32_t remote_id, const uint8_t send_key[32],
+                            const uint8_t recv_key[32], uint32_t peer);
 int rg_sessions_remove(rg_sessions *s, uint32_t slot);
 int rg_sessions_lookup(const rg_sessions *s, uint32_t local_id); /* slot or RG_ENOTFOUND */
 /* EncryptionKey::counter() (prim.rs:396-398) / overwrite, e.g. for REKEY tests */
@@ -303,16 +315,20 @@ int rg_recv_batch_ex(rg_sessions *s, const rg_pkt_desc *desc, size_t n, uint8_t 
  * Sessions take it as started / sent when inserted; rg_send_batch sets sent and rejects
  * once started + REJECT_AFTER_TIME (180 s) < now (should_expire, lib.rs:207-209). */
 void rg_sessions_set_time(rg_sessions *s, uint64_t now_ns);
-/* the endpoint tag of the session's last authenticated packet; RG_ENOTFOUND before any.
- * Kept per session slot, whereas the reference keeps it per peer (peer.endpoint,
- * rustyguard-core/src/lib.rs:670-671, read by the Keepalive timer, time.rs:135): after a rekey
- * the new slot has no endpoint until its own first authenticated packet, so a caller with
- * several sessions per peer carries the endpoint per peer itself (the latest of its slots). */
+/* the endpoint tag of the last authenticated packet of the session's peer (any of the peer's
+ * sessions, rg_sessions_insert_peer; the session itself when inserted without a peer);
+ * RG_ENOTFOUND before any.  rg_peer_endpoint reads a peer's record directly. */
 int rg_sessions_endpoint(const rg_sessions *s, uint32_t slot, uint64_t *src_out);
+int rg_peer_endpoint(const rg_sessions *s, uint32_t peer, uint64_t *src_out);
 /* the Keepalive timer entry (rustyguard-core/src/time.rs:114-141): clears keepalive_pending
  * and returns 1 when sent + KEEPALIVE_TIMEOUT < now (should_keepalive, lib.rs:201-203): the
  * caller then seals an empty payload (P = 0) for the session with rg_send_batch. */
 int rg_sessions_keepalive_due(rg_sessions *s, uint32_t slot);
+/* rg_sessions_keepalive_due with the address the keepalive goes to: the session's peer endpoint
+ * (peer.endpoint, time.rs:135) in *dst_out when due.  Returns 1 (due, *dst_out set), 0 (not
+ * due), RG_ENOTFOUND (due but the peer never authenticated a packet: the reference's
+ * "should not be scheduled" expect) or another negative rg_status. */
+int rg_sessions_keepalive(rg_sessions *s, uint32_t slot, uint64_t *dst_out);
 
 /* Device-resident variants of rg_send_batch / rg_recv_batch_ex: frames, descriptors and
  * statuses in device memory, the session state on the host.  Work is enqueued on `stream`
@@ -342,17 +358,51 @@ int rg_recv_batch_dev(rg_sessions *s, const rg_pkt_desc *desc, size_t n, uint8_t
 int rg_recv_batch_dev_finish(rg_sessions *s, const uint64_t *src, uint8_t *status_out, uint32_t *slots_out,
                              uint8_t *flags_out);
 
-/* ------------------------------------------------------------ test hooks */
-/* Not for production use.  rg_debug_read_arena copies up to `bytes` of one of the context's
- * key-bearing device buffers to host memory -- which = 0: the per-message drop-in's arena (its
- * job record holds the key while a call runs and is zeroed before the call returns), 1: the
- * batched host API's key table, 2: the MAC key states -- and returns the number of bytes copied
- * (>= 0) or a negative rg_status.  Key-bearing buffers are zeroed before they are freed or
- * regrown (rg_destroy, rg_sessions_destroy), as the reference zeroizes keys on drop
- * (rustyguard-crypto/src/prim.rs:227-231).  rg_debug_fail_reserve(n) makes the n-th following
- * device or pinned-host buffer allocation of any context fail (0 = off), for error-path tests. */
-int rg_debug_read_arena(rg_ctx *ctx, int which, void *dst, size_t bytes);
-void rg_debug_fail_reserve(int nth);
+/* ------------------------------------------- several GPUs, one thread */
+/* The reference's host is one thread owning one Sessions (RefCell, rustyguard-core/src/lib.rs:
+ * 349-352; send_message / recv_message :542-583, :605-681).  A group lets that one thread drive
+ * several GPUs: one context per entry of devices[] (a device may repeat: several contexts on one
+ * GPU).  A batch given to a group is split into contiguous index ranges of about equal AEAD work
+ * (payload bytes + one 64-byte key block per packet; rg_split_batch), one per context; every
+ * context's H2D -> kernel -> D2H pipeline is enqueued on its own streams from the calling thread,
+ * round-robin, and the call returns when all are done.  Results are those of one context: the
+ * packets are independent, counters are reserved before the split (rg_send_batch)
+ * and the in-order anti-replay pass runs after the gather (rg_recv_batch_ex). */
+typedef struct rg_group rg_group;
+int rg_group_create(const int *devices, int n, rg_group **out);
+void rg_group_destroy(rg_group *g);
+int rg_group_size(const rg_group *g);
+rg_ctx *rg_group_ctx(rg_group *g, int i); /* the i-th context (tuning knobs, device calls); NULL if out of range */
+/* The split: bounds[0] = 0 <= bounds[1] <= ... <= bounds[parts] = n, part k = [bounds[k], bounds[k+1]),
+ * cut where the running work (len, minus 32 when open, + 64 per packet) crosses k / parts of the total. */
+int rg_split_batch(const rg_pkt_desc *desc, size_t n, int open, int parts, size_t *bounds);
+/* rg_seal_batch_host / rg_open_batch_host over the group (same arguments and results). */
+int rg_seal_batch_host_multi(rg_group *g, const uint8_t *keys, const uint32_t *receivers, uint32_t nkeys,
+                             const rg_pkt_desc *desc, const uint64_t *counters, size_t n, uint8_t *buf,
+                             size_t buf_len, uint8_t *status);
+int rg_open_batch_host_multi(rg_group *g, const uint8_t *keys, uint32_t nkeys, const rg_pkt_desc *desc, size_t n,
+                             uint8_t *buf, size_t buf_len, uint8_t *status, uint64_t *counters_out);
+/* Device-resident shards: shard i lives on context i's device (its own keys, descriptors, frames,
+ * statuses and stream there); rg_seal_batch_dev / rg_open_batch_dev enqueued for every shard, from
+ * this thread, without waiting (counters_out and receivers may be NULL as there). */
+typedef struct rg_dev_shard {
+    const uint8_t *keys;
+    const uint32_t *receivers; /* seal only */
+    uint32_t nkeys;
+    const rg_pkt_desc *desc;
+    const uint64_t *counters; /* seal only */
+    size_t n;
+    uint8_t *buf;
+    size_t buf_len;
+    uint8_t *status;
+    uint64_t *counters_out; /* open only */
+    void *stream;
+} rg_dev_shard;
+int rg_seal_batch_dev_multi(rg_group *g, const rg_dev_shard *shards);
+int rg_open_batch_dev_multi(rg_group *g, const rg_dev_shard *shards);
+/* A session table whose host-frame batches (rg_send_batch, rg_recv_batch[_ex]) run on the whole
+ * group; the device-frame calls (rg_send_batch_dev, rg_recv_batch_dev) refuse such a table. */
+int rg_sessions_create_group(rg_group *g, uint32_t capacity, rg_sessions **out);
 
 /* ------------------------------------------------ synthetic workloads */
 /* Device fill of payload bytes: inner bytes [0, inner_len[i]) of packet i

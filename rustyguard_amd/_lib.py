@@ -12,6 +12,7 @@ import os
 from . import build as _build
 
 _lib = None
+_test_lib = None
 
 c_u8p = ctypes.c_void_p
 c_vp = ctypes.c_void_p
@@ -73,6 +74,23 @@ SIGNATURES = {
     "rg_recv_batch_dev": (c_int, [c_vp, c_vp, c_size, c_vp, c_size, c_vp, c_vp]),
     "rg_recv_batch_dev_finish": (c_int, [c_vp, c_vp, c_u8p, c_vp, c_u8p]),
     "rg_synth_fill_dev": (c_int, [c_vp, c_vp, c_vp, c_size, c_u8p, c_size, c_u64, c_vp]),
+    "rg_sessions_insert_peer": (c_int, [c_vp, c_u32, c_u32, c_u8p, c_u8p, c_u32]),
+    "rg_peer_endpoint": (c_int, [c_vp, c_u32, c_vp]),
+    "rg_sessions_keepalive": (c_int, [c_vp, c_u32, c_vp]),
+    "rg_group_create": (c_int, [c_vp, c_int, ctypes.POINTER(c_vp)]),
+    "rg_group_destroy": (None, [c_vp]),
+    "rg_group_size": (c_int, [c_vp]),
+    "rg_group_ctx": (c_vp, [c_vp, c_int]),
+    "rg_split_batch": (c_int, [c_vp, c_size, c_int, c_int, c_vp]),
+    "rg_seal_batch_host_multi": (c_int, [c_vp, c_u8p, c_vp, c_u32, c_vp, c_vp, c_size, c_u8p, c_size, c_u8p]),
+    "rg_open_batch_host_multi": (c_int, [c_vp, c_u8p, c_u32, c_vp, c_size, c_u8p, c_size, c_u8p, c_vp]),
+    "rg_seal_batch_dev_multi": (c_int, [c_vp, c_vp]),
+    "rg_open_batch_dev_multi": (c_int, [c_vp, c_vp]),
+    "rg_sessions_create_group": (c_int, [c_vp, c_u32, ctypes.POINTER(c_vp)]),
+}
+
+# include/rg_aead_test.h: exported by the test library (librg_aead_test.so) only
+TEST_SIGNATURES = {
     "rg_debug_read_arena": (c_int, [c_vp, c_int, c_vp, c_size]),
     "rg_debug_fail_reserve": (None, [c_int]),
 }
@@ -86,26 +104,40 @@ def lib_path() -> str:
     return _build.LIB
 
 
+def _load(path: str, sigs: dict, build_if_missing: bool):
+    if not os.path.exists(path):
+        if not build_if_missing:
+            raise RgError(f"{os.path.basename(path)} missing at {path}; run python -m rustyguard_amd.build")
+        _build.build()
+    L = ctypes.CDLL(path)
+    for name, (res, args) in sigs.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    return L
+
+
 def lib(build_if_missing: bool = True):
-    """Load librg_aead.so; raise loudly if it cannot be loaded."""
+    """Load librg_aead.so (the product library); raise loudly if it cannot be loaded."""
     global _lib
     if _lib is None:
         path = os.environ.get("RG_AEAD_LIB") or _build.LIB  # override: experimental builds only
-        if not os.path.exists(path):
-            if not build_if_missing:
-                raise RgError(f"librg_aead.so missing at {path}; run python -m rustyguard_amd.build")
-            _build.build()
-        L = ctypes.CDLL(path)
-        for name, (res, args) in SIGNATURES.items():
-            f = getattr(L, name)
-            f.restype = res
-            f.argtypes = args
-        _lib = L
+        _lib = _load(path, SIGNATURES, build_if_missing)
     return _lib
 
 
-def check(rc: int, what: str) -> int:
+def lib_test(build_if_missing: bool = True):
+    """Load librg_aead_test.so: the product kernels plus the test hooks of include/rg_aead_test.h.
+    Only the tests that check key wiping and allocation failures use it; its contexts are its own
+    (a handle of one library is never passed to the other)."""
+    global _test_lib
+    if _test_lib is None:
+        _test_lib = _load(_build.TEST_LIB, {**SIGNATURES, **TEST_SIGNATURES}, build_if_missing)
+    return _test_lib
+
+
+def check(rc: int, what: str, L=None) -> int:
     if rc < 0:
-        err = lib().rg_last_error()
+        err = (L or lib()).rg_last_error()
         raise RgError(f"{what} failed ({rc}): {err.decode() if err else ''}")
     return rc

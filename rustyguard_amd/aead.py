@@ -86,10 +86,12 @@ def _nbytes(t) -> int:
 class Engine:
     """One rg_ctx: a HIP device plus its staging buffers (one per process/GPU)."""
 
-    def __init__(self, device: int = 0):
-        self._L = lib()
+    def __init__(self, device: int = 0, library=None):
+        """library: the loaded C library (default: the product librg_aead.so; tests of the test hooks pass
+        _lib.lib_test())."""
+        self._L = library if library is not None else lib()
         h = ctypes.c_void_p()
-        check(self._L.rg_create(device, ctypes.byref(h)), "rg_create")
+        self._check(self._L.rg_create(device, ctypes.byref(h)), "rg_create")
         self._h = h
         self.device = device
 
@@ -108,17 +110,24 @@ class Engine:
     def handle(self):
         return self._h
 
+    @property
+    def library(self):
+        return self._L
+
+    def _check(self, rc: int, what: str) -> int:
+        return check(rc, what, self._L)
+
     def set_lanes_per_packet(self, lanes: int):
-        check(self._L.rg_set_lanes_per_packet(self._h, lanes), "rg_set_lanes_per_packet")
+        self._check(self._L.rg_set_lanes_per_packet(self._h, lanes), "rg_set_lanes_per_packet")
 
     def set_staged(self, kernel: int):
         """Kernel family: -1 = automatic by batch size (default), 0 = pipelined lane kernel,
         1/2 = LDS-staged tile kernel with that many 64-byte chunks per window."""
-        check(self._L.rg_set_staged(self._h, kernel), "rg_set_staged")
+        self._check(self._L.rg_set_staged(self._h, kernel), "rg_set_staged")
 
     def kernel_for(self, n: int) -> int:
         """The kernel family a batch of n packets runs on (rg_get_kernel)."""
-        return check(self._L.rg_get_kernel(self._h, n), "rg_get_kernel")
+        return self._check(self._L.rg_get_kernel(self._h, n), "rg_get_kernel")
 
     def last_kernel(self) -> int:
         """The kernel family the most recent batched launch ran (rg_last_kernel; -1 before any)."""
@@ -126,41 +135,41 @@ class Engine:
 
     def set_plan(self, mode):
         """Size-class planner before the batched kernels: 0/False off, 1/True on, 2 auto (default)."""
-        check(self._L.rg_set_plan(self._h, int(mode)), "rg_set_plan")
+        self._check(self._L.rg_set_plan(self._h, int(mode)), "rg_set_plan")
 
     def set_segments(self, k: int):
         """Segments per packet for the tile kernels: 0 = automatic, 1/2/4 = forced."""
-        check(self._L.rg_set_segments(self._h, k), "rg_set_segments")
+        self._check(self._L.rg_set_segments(self._h, k), "rg_set_segments")
 
     def set_debug_mode(self, mode: int):
         """Diagnostics: 1 = compute-only seal, 2 = memory-only seal, 3 = stamps, 4/5/6 = non-temporal
         loads / stores / both on the pipelined kernel (outputs invalid except in mode 3)."""
-        check(self._L.rg_set_debug_mode(self._h, mode), "rg_set_debug_mode")
+        self._check(self._L.rg_set_debug_mode(self._h, mode), "rg_set_debug_mode")
 
     def set_debug_buffer(self, tensor):
         """Diagnostics: device buffer receiving per-wave stamps (include/rg_aead.h)."""
-        check(self._L.rg_set_debug_buffer(self._h, _vp(tensor) if tensor is not None else None),
+        self._check(self._L.rg_set_debug_buffer(self._h, _vp(tensor) if tensor is not None else None),
               "rg_set_debug_buffer")
 
     def set_wg_per_cu(self, wg: int):
-        check(self._L.rg_set_wg_per_cu(self._h, wg), "rg_set_wg_per_cu")
+        self._check(self._L.rg_set_wg_per_cu(self._h, wg), "rg_set_wg_per_cu")
 
     def lanes_per_packet(self, n: int) -> int:
-        return check(self._L.rg_get_lanes_per_packet(self._h, n), "rg_get_lanes_per_packet")
+        return self._check(self._L.rg_get_lanes_per_packet(self._h, n), "rg_get_lanes_per_packet")
 
     # ---------------------------------------------------- device-resident
     def seal_dev(self, keys, receivers, desc, counters, buf, status=None, stream=None):
         """Enqueue a batched seal on `stream`; all tensors on this device."""
         n = _ndesc(desc)
         nkeys = _nbytes(keys) // 32
-        check(self._L.rg_seal_batch_dev(self._h, _vp(keys), _vp(receivers), nkeys, _vp(desc), _vp(counters), n,
+        self._check(self._L.rg_seal_batch_dev(self._h, _vp(keys), _vp(receivers), nkeys, _vp(desc), _vp(counters), n,
                                         _vp(buf), _nbytes(buf), _vp(status), _stream_handle(stream)),
               "rg_seal_batch_dev")
 
     def open_dev(self, keys, desc, buf, status, counters_out=None, stream=None):
         n = _ndesc(desc)
         nkeys = _nbytes(keys) // 32
-        check(self._L.rg_open_batch_dev(self._h, _vp(keys), nkeys, _vp(desc), n, _vp(buf), _nbytes(buf),
+        self._check(self._L.rg_open_batch_dev(self._h, _vp(keys), nkeys, _vp(desc), n, _vp(buf), _nbytes(buf),
                                         _vp(status), _vp(counters_out), _stream_handle(stream)),
               "rg_open_batch_dev")
 
@@ -170,7 +179,7 @@ class Engine:
         n = _ndesc(desc)
         nkeys = _nbytes(keys) // 32
         cap = _nbytes(rx_table) // 8
-        check(self._L.rg_open_batch_dev_rx(self._h, _vp(keys), nkeys, _vp(rx_table), cap, _vp(desc), n, _vp(buf),
+        self._check(self._L.rg_open_batch_dev_rx(self._h, _vp(keys), nkeys, _vp(rx_table), cap, _vp(desc), n, _vp(buf),
                                            _nbytes(buf), _vp(status), _vp(counters_out), _vp(key_idx_out),
                                            _stream_handle(stream)), "rg_open_batch_dev_rx")
 
@@ -180,13 +189,13 @@ class Engine:
         n = _ndesc(desc)
         key_len = 32 if which == 1 else 16
         nkeys = _nbytes(keys) // key_len
-        check(self._L.rg_mac_verify_batch_dev(self._h, _vp(keys), key_len, nkeys, which, _vp(desc), n, _vp(buf),
+        self._check(self._L.rg_mac_verify_batch_dev(self._h, _vp(keys), key_len, nkeys, which, _vp(desc), n, _vp(buf),
                                               _nbytes(buf), _vp(status), _vp(key_idx_out), _stream_handle(stream)),
               "rg_mac_verify_batch_dev")
 
     def synth_fill_dev(self, desc, inner_len, buf, seed: int, stream=None):
         n = _ndesc(desc)
-        check(self._L.rg_synth_fill_dev(self._h, _vp(desc), _vp(inner_len), n, _vp(buf), _nbytes(buf), seed,
+        self._check(self._L.rg_synth_fill_dev(self._h, _vp(desc), _vp(inner_len), n, _vp(buf), _nbytes(buf), seed,
                                         _stream_handle(stream)), "rg_synth_fill_dev")
 
     # -------------------------------------------------------- host memory
@@ -196,7 +205,7 @@ class Engine:
         counters = np.ascontiguousarray(counters, np.uint64)
         rec = None if receivers is None else np.ascontiguousarray(receivers, np.uint32)
         status = np.zeros(max(len(desc), 1), np.uint8)
-        check(self._L.rg_seal_batch_host(self._h, _vp(keys), _vp(rec), keys.size // 32, _vp(desc), _vp(counters),
+        self._check(self._L.rg_seal_batch_host(self._h, _vp(keys), _vp(rec), keys.size // 32, _vp(desc), _vp(counters),
                                          len(desc), _vp(buf), buf.nbytes, _vp(status)), "rg_seal_batch_host")
         return status[: len(desc)]
 
@@ -206,7 +215,7 @@ class Engine:
         n = len(desc)
         status = np.zeros(max(n, 1), np.uint8)
         ctr = np.zeros(max(n, 1), np.uint64)
-        check(self._L.rg_open_batch_host(self._h, _vp(keys), keys.size // 32, _vp(desc), n, _vp(buf), buf.nbytes,
+        self._check(self._L.rg_open_batch_host(self._h, _vp(keys), keys.size // 32, _vp(desc), n, _vp(buf), buf.nbytes,
                                          _vp(status), _vp(ctr)), "rg_open_batch_host")
         return status[:n], ctr[:n]
 
@@ -216,7 +225,7 @@ class Engine:
         assert len(key) == 32 and len(nonce) == 12
         tag = bytearray(16)
         k, nz, a = bytearray(key), bytearray(nonce), bytearray(aad or b"\0")
-        check(self._L.rg_chacha20poly1305_enc(self._h, _vp(k), _vp(nz), _vp(a), len(aad), _vp(payload) if payload
+        self._check(self._L.rg_chacha20poly1305_enc(self._h, _vp(k), _vp(nz), _vp(a), len(aad), _vp(payload) if payload
                                               else None, len(payload), _vp(tag)), "rg_chacha20poly1305_enc")
         return bytes(tag)
 
@@ -225,7 +234,7 @@ class Engine:
         assert len(key) == 32 and len(nonce) == 24
         tag = bytearray(16)
         k, nz, a = bytearray(key), bytearray(nonce), bytearray(aad or b"\0")
-        check(self._L.rg_xchacha20poly1305_enc(self._h, _vp(k), _vp(nz), _vp(a), len(aad), _vp(payload) if payload
+        self._check(self._L.rg_xchacha20poly1305_enc(self._h, _vp(k), _vp(nz), _vp(a), len(aad), _vp(payload) if payload
                                                else None, len(payload), _vp(tag)), "rg_xchacha20poly1305_enc")
         return bytes(tag)
 
@@ -233,7 +242,7 @@ class Engine:
         """Core::xchacha20poly1305_dec (prim.rs:214-224): decrypts in place or raises DecryptionError."""
         assert len(key) == 32 and len(nonce) == 24 and len(tag) == 16
         k, nz, a, t = bytearray(key), bytearray(nonce), bytearray(aad or b"\0"), bytearray(tag)
-        rc = check(self._L.rg_xchacha20poly1305_dec(self._h, _vp(k), _vp(nz), _vp(a), len(aad), _vp(payload)
+        rc = self._check(self._L.rg_xchacha20poly1305_dec(self._h, _vp(k), _vp(nz), _vp(a), len(aad), _vp(payload)
                                                     if payload else None, len(payload), _vp(t)),
                    "rg_xchacha20poly1305_dec")
         if rc == PKT_DECRYPT_ERR:
@@ -243,7 +252,7 @@ class Engine:
         """Core::chacha20poly1305_dec: decrypts in place or raises DecryptionError."""
         assert len(key) == 32 and len(nonce) == 12 and len(tag) == 16
         k, nz, a, t = bytearray(key), bytearray(nonce), bytearray(aad or b"\0"), bytearray(tag)
-        rc = check(self._L.rg_chacha20poly1305_dec(self._h, _vp(k), _vp(nz), _vp(a), len(aad), _vp(payload) if payload
+        rc = self._check(self._L.rg_chacha20poly1305_dec(self._h, _vp(k), _vp(nz), _vp(a), len(aad), _vp(payload) if payload
                                                    else None, len(payload), _vp(t)), "rg_chacha20poly1305_dec")
         if rc == PKT_DECRYPT_ERR:
             raise DecryptionError()
@@ -311,49 +320,199 @@ class DecryptionKey:
 
 
 # ------------------------------------------------------------------ Sessions
-class Sessions:
-    """Transport half of rustyguard_core::Sessions (batched, host frames)."""
+class Group:
+    """rg_group: one thread driving several GPUs (one context per entry of `devices`; a device may
+    repeat).  Host-memory batches are split into contiguous ranges of about equal AEAD work, one per
+    context, all pipelines enqueued from this thread (include/rg_aead.h, "several GPUs, one thread")."""
 
-    def __init__(self, engine: Engine, capacity: int = 64):
-        self.engine = engine
+    def __init__(self, devices, library=None):
+        self._L = library if library is not None else lib()
+        devs = (ctypes.c_int * len(devices))(*devices)
         h = ctypes.c_void_p()
-        check(lib().rg_sessions_create(engine.handle, capacity, ctypes.byref(h)), "rg_sessions_create")
+        check(self._L.rg_group_create(devs, len(devices), ctypes.byref(h)), "rg_group_create", self._L)
         self._h = h
+        self.devices = list(devices)
+
+    @property
+    def handle(self):
+        return self._h
+
+    @property
+    def library(self):
+        return self._L
+
+    def __len__(self):
+        return len(self.devices)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.rg_group_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def ctx(self, i: int):
+        """Handle of the i-th context (for per-context knobs through the C ABI)."""
+        return ctypes.c_void_p(self._L.rg_group_ctx(self._h, i))
+
+    def engine(self, i: int) -> "Engine":
+        """An Engine view of the i-th context (not owning it: the group destroys its contexts)."""
+        return _ContextView(self, i)
+
+    def seal_host(self, keys: np.ndarray, receivers, desc: np.ndarray, counters: np.ndarray, buf: np.ndarray):
+        assert desc.dtype == DESC_DTYPE and buf.dtype == np.uint8 and buf.flags.c_contiguous
+        keys = np.ascontiguousarray(keys, np.uint8)
+        counters = np.ascontiguousarray(counters, np.uint64)
+        rec = None if receivers is None else np.ascontiguousarray(receivers, np.uint32)
+        status = np.zeros(max(len(desc), 1), np.uint8)
+        check(self._L.rg_seal_batch_host_multi(self._h, _vp(keys), _vp(rec), keys.size // 32, _vp(desc),
+                                               _vp(counters), len(desc), _vp(buf), buf.nbytes, _vp(status)),
+              "rg_seal_batch_host_multi", self._L)
+        return status[: len(desc)]
+
+    def open_host(self, keys: np.ndarray, desc: np.ndarray, buf: np.ndarray):
+        assert desc.dtype == DESC_DTYPE and buf.dtype == np.uint8 and buf.flags.c_contiguous
+        keys = np.ascontiguousarray(keys, np.uint8)
+        n = len(desc)
+        status = np.zeros(max(n, 1), np.uint8)
+        ctr = np.zeros(max(n, 1), np.uint64)
+        check(self._L.rg_open_batch_host_multi(self._h, _vp(keys), keys.size // 32, _vp(desc), n, _vp(buf),
+                                               buf.nbytes, _vp(status), _vp(ctr)), "rg_open_batch_host_multi", self._L)
+        return status[:n], ctr[:n]
+
+    @staticmethod
+    def shards(shards, seal: bool):
+        """The rg_dev_shard array of `shards` (one dict per context: keys, receivers, desc, counters, buf,
+        status, counters_out, stream -- tensors on that context's device), built once for repeated calls."""
+        assert len(shards) > 0
+        return _shard_array(shards, seal=seal)
+
+    def seal_dev(self, shards):
+        """rg_seal_batch_dev_multi: one shard per context (a list of dicts or a Group.shards array), enqueued
+        on each shard's stream without waiting."""
+        arr = shards if isinstance(shards, ctypes.Array) else _shard_array(shards, seal=True)
+        assert len(arr) == len(self.devices)
+        check(self._L.rg_seal_batch_dev_multi(self._h, ctypes.cast(arr, ctypes.c_void_p)), "rg_seal_batch_dev_multi",
+              self._L)
+
+    def open_dev(self, shards):
+        arr = shards if isinstance(shards, ctypes.Array) else _shard_array(shards, seal=False)
+        assert len(arr) == len(self.devices)
+        check(self._L.rg_open_batch_dev_multi(self._h, ctypes.cast(arr, ctypes.c_void_p)), "rg_open_batch_dev_multi",
+              self._L)
+
+
+class _ContextView(Engine):
+    """Engine methods on a context owned by a Group."""
+
+    def __init__(self, group: Group, i: int):
+        h = group._L.rg_group_ctx(group.handle, i)
+        if not h:
+            raise _lib.RgError(f"group has no context {i}")
+        self._L, self._h, self.device, self._group = group.library, ctypes.c_void_p(h), group.devices[i], group
+
+    def close(self):
+        self._h = None  # the group owns the context
+
+
+class _DevShard(ctypes.Structure):
+    """rg_dev_shard (include/rg_aead.h)."""
+    _fields_ = [("keys", ctypes.c_void_p), ("receivers", ctypes.c_void_p), ("nkeys", ctypes.c_uint32),
+                ("desc", ctypes.c_void_p), ("counters", ctypes.c_void_p), ("n", ctypes.c_size_t),
+                ("buf", ctypes.c_void_p), ("buf_len", ctypes.c_size_t), ("status", ctypes.c_void_p),
+                ("counters_out", ctypes.c_void_p), ("stream", ctypes.c_void_p)]
+
+
+def _shard_array(shards, seal: bool):
+    arr = (_DevShard * len(shards))()
+    for k, sh in enumerate(shards):
+        x = arr[k]
+        p = lambda t: _vp(t).value if t is not None else None  # noqa: E731
+        x.keys = p(sh["keys"])
+        x.nkeys = _nbytes(sh["keys"]) // 32
+        x.desc = p(sh["desc"])
+        x.n = _ndesc(sh["desc"])
+        x.buf = p(sh["buf"])
+        x.buf_len = _nbytes(sh["buf"])
+        x.status = p(sh.get("status"))
+        x.stream = _stream_handle(sh.get("stream")).value
+        if seal:
+            x.receivers = p(sh.get("receivers"))
+            x.counters = p(sh["counters"])
+        else:
+            x.counters_out = p(sh.get("counters_out"))
+    return arr
+
+
+def split_batch(desc: np.ndarray, parts: int, open_: bool = False) -> np.ndarray:
+    """rg_split_batch: bounds[0..parts] of the group split (contiguous ranges of about equal work)."""
+    assert desc.dtype == DESC_DTYPE
+    b = np.zeros(parts + 1, np.uint64)
+    check(lib().rg_split_batch(_vp(desc), len(desc), int(open_), parts, _vp(b)), "rg_split_batch")
+    return b.astype(np.int64)
+
+
+class Sessions:
+    """Transport half of rustyguard_core::Sessions (batched, host frames).  On a Group the host-frame
+    batches run on every GPU of the group (rg_sessions_create_group)."""
+
+    def __init__(self, engine, capacity: int = 64):
+        self.engine = engine
+        self._L = engine.library
+        h = ctypes.c_void_p()
+        if isinstance(engine, Group):
+            self._check(self._L.rg_sessions_create_group(engine.handle, capacity, ctypes.byref(h)),
+                        "rg_sessions_create_group")
+        else:
+            self._check(self._L.rg_sessions_create(engine.handle, capacity, ctypes.byref(h)), "rg_sessions_create")
+        self._h = h
+
+    def _check(self, rc: int, what: str) -> int:
+        return check(rc, what, self._L)
 
     def __del__(self):
         try:
             if self._h:
-                lib().rg_sessions_destroy(self._h)
+                self._L.rg_sessions_destroy(self._h)
                 self._h = None
         except Exception:
             pass
 
-    def insert(self, local_id: int, remote_id: int, send_key: bytes, recv_key: bytes) -> int:
+    def insert(self, local_id: int, remote_id: int, send_key: bytes, recv_key: bytes, peer: int | None = None) -> int:
+        """Install a transport session; `peer` (an id of the caller's) makes the sessions of one peer share
+        its endpoint record (PeerState.endpoint, rustyguard-core/src/lib.rs:160-181)."""
         sk, rk = bytearray(send_key), bytearray(recv_key)
-        return check(lib().rg_sessions_insert(self._h, local_id, remote_id, _vp(sk), _vp(rk)), "rg_sessions_insert")
+        if peer is not None:
+            return self._check(self._L.rg_sessions_insert_peer(self._h, local_id, remote_id, _vp(sk), _vp(rk), peer),
+                               "rg_sessions_insert_peer")
+        return self._check(self._L.rg_sessions_insert(self._h, local_id, remote_id, _vp(sk), _vp(rk)), "rg_sessions_insert")
 
     def remove(self, slot: int):
-        check(lib().rg_sessions_remove(self._h, slot), "rg_sessions_remove")
+        self._check(self._L.rg_sessions_remove(self._h, slot), "rg_sessions_remove")
 
     def lookup(self, local_id: int) -> int | None:
-        rc = lib().rg_sessions_lookup(self._h, local_id)
+        rc = self._L.rg_sessions_lookup(self._h, local_id)
         return None if rc < 0 else rc
 
     def send_counter(self, slot: int) -> int:
-        return int(lib().rg_sessions_send_counter(self._h, slot))
+        return int(self._L.rg_sessions_send_counter(self._h, slot))
 
     def set_send_counter(self, slot: int, counter: int):
-        check(lib().rg_sessions_set_send_counter(self._h, slot, counter), "rg_sessions_set_send_counter")
+        self._check(self._L.rg_sessions_set_send_counter(self._h, slot, counter), "rg_sessions_set_send_counter")
 
     def replay(self, slot: int) -> AntiReplay:
-        return AntiReplay(_ptr=lib().rg_sessions_replay(self._h, slot))
+        return AntiReplay(_ptr=self._L.rg_sessions_replay(self._h, slot))
 
     def send_batch(self, slots, desc: np.ndarray, buf: np.ndarray):
         slots = np.ascontiguousarray(slots, np.uint32)
         n = len(desc)
         status = np.zeros(max(n, 1), np.uint8)
         rekey = np.zeros(max(n, 1), np.uint8)
-        check(lib().rg_send_batch(self._h, _vp(slots), _vp(desc), n, _vp(buf), buf.nbytes, _vp(status), _vp(rekey)),
+        self._check(self._L.rg_send_batch(self._h, _vp(slots), _vp(desc), n, _vp(buf), buf.nbytes, _vp(status), _vp(rekey)),
               "rg_send_batch")
         return status[:n], rekey[:n]
 
@@ -367,7 +526,7 @@ class Sessions:
         slots = np.zeros(max(n, 1), np.uint32)
         fl = np.zeros(max(n, 1), np.uint8)
         srcs = None if src is None else np.ascontiguousarray(src, np.uint64)
-        check(lib().rg_recv_batch_ex(self._h, _vp(desc), n, _vp(buf), buf.nbytes, _vp(srcs), _vp(status),
+        self._check(self._L.rg_recv_batch_ex(self._h, _vp(desc), n, _vp(buf), buf.nbytes, _vp(srcs), _vp(status),
                                      _vp(slots), _vp(fl)), "rg_recv_batch_ex")
         return (status[:n], slots[:n], fl[:n]) if flags else (status[:n], slots[:n])
 
@@ -377,14 +536,14 @@ class Sessions:
         slots = np.ascontiguousarray(slots, np.uint32)
         n = _ndesc(desc)
         rekey = np.zeros(max(n, 1), np.uint8)
-        check(lib().rg_send_batch_dev(self._h, _vp(slots), _vp(desc), n, _vp(buf), _nbytes(buf), _vp(status),
+        self._check(self._L.rg_send_batch_dev(self._h, _vp(slots), _vp(desc), n, _vp(buf), _nbytes(buf), _vp(status),
                                       _vp(rekey), _stream_handle(stream)), "rg_send_batch_dev")
         return rekey[:n]
 
     def recv_batch_dev(self, desc, buf, status, stream=None):
         """rg_recv_batch_dev: enqueue the GPU half of a device-resident receive; finish it with
         recv_batch_dev_finish."""
-        check(lib().rg_recv_batch_dev(self._h, _vp(desc), _ndesc(desc), _vp(buf), _nbytes(buf), _vp(status),
+        self._check(self._L.rg_recv_batch_dev(self._h, _vp(desc), _ndesc(desc), _vp(buf), _nbytes(buf), _vp(status),
                                       _stream_handle(stream)), "rg_recv_batch_dev")
 
     def recv_batch_dev_finish(self, n: int, src=None):
@@ -394,27 +553,43 @@ class Sessions:
         slots = np.zeros(max(n, 1), np.uint32)
         fl = np.zeros(max(n, 1), np.uint8)
         srcs = None if src is None else np.ascontiguousarray(src, np.uint64)
-        check(lib().rg_recv_batch_dev_finish(self._h, _vp(srcs), _vp(status), _vp(slots), _vp(fl)),
+        self._check(self._L.rg_recv_batch_dev_finish(self._h, _vp(srcs), _vp(status), _vp(slots), _vp(fl)),
               "rg_recv_batch_dev_finish")
         return status[:n], slots[:n], fl[:n]
 
     def set_time(self, now_ns: int):
         """The table's clock (Sessions::turn's state.now), monotonic nanoseconds."""
-        lib().rg_sessions_set_time(self._h, int(now_ns))
+        self._L.rg_sessions_set_time(self._h, int(now_ns))
 
     def endpoint(self, slot: int):
         """Source tag of the session's last authenticated packet, or None."""
         out = ctypes.c_uint64()
-        rc = lib().rg_sessions_endpoint(self._h, slot, ctypes.byref(out))
+        rc = self._L.rg_sessions_endpoint(self._h, slot, ctypes.byref(out))
         if rc == -4:  # RG_ENOTFOUND
             return None
-        check(rc, "rg_sessions_endpoint")
+        self._check(rc, "rg_sessions_endpoint")
         return int(out.value)
+
+    def peer_endpoint(self, peer: int):
+        """Source tag of the peer's last authenticated packet (any of its sessions), or None."""
+        out = ctypes.c_uint64()
+        rc = self._L.rg_peer_endpoint(self._h, peer, ctypes.byref(out))
+        if rc == -4:  # RG_ENOTFOUND
+            return None
+        self._check(rc, "rg_peer_endpoint")
+        return int(out.value)
+
+    def keepalive(self, slot: int):
+        """rg_sessions_keepalive: the Keepalive timer entry with its destination -- the peer's endpoint
+        (time.rs:135) when a keepalive is due, else None.  Raises when due with no endpoint known."""
+        out = ctypes.c_uint64()
+        rc = self._check(self._L.rg_sessions_keepalive(self._h, slot, ctypes.byref(out)), "rg_sessions_keepalive")
+        return int(out.value) if rc == 1 else None
 
     def keepalive_due(self, slot: int) -> bool:
         """The Keepalive timer entry (time.rs:114-141): clears the pending flag; True when a keepalive
         (an empty payload through send_batch) should go out now."""
-        return bool(check(lib().rg_sessions_keepalive_due(self._h, slot), "rg_sessions_keepalive_due"))
+        return bool(self._check(self._L.rg_sessions_keepalive_due(self._h, slot), "rg_sessions_keepalive_due"))
 
 
 def rx_table(receivers, key_idx, cap: int | None = None) -> np.ndarray:

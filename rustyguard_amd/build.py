@@ -1,33 +1,62 @@
 """Build librg_aead.so (HIP kernels + C ABI) in-tree for gfx950.
 
-``python -m rustyguard_amd.build`` or ``__graft_entry__.build()``.  The .so is
-git-ignored but travels to the GPU box with the gpurun snapshot.
+``python -m rustyguard_amd.build`` or ``__graft_entry__.build()``.  The .so files are
+git-ignored but travel to the GPU box with the gpurun snapshot.
+
+Two libraries come out of one set of kernel objects:
+  lib/librg_aead.so       the product: include/rg_aead.h, no diagnostics, no test hooks
+  lib/librg_aead_test.so  the same kernels + rg_api.cpp with -DRG_TEST_HOOKS
+                          (include/rg_aead_test.h), loaded only by the GPU tests that
+                          check key wiping and allocation failures
+Diagnostic builds (-DRG_DIAG: seal modes, per-wave stamps) are tools/build_variant.sh's.
 """
 from __future__ import annotations
 
 import os
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIBDIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIBDIR, "librg_aead.so")
-SOURCES = ["rg_kernels.hip", "rg_tile.hip", "rg_pipe.hip", "rg_flat.hip", "rg_mac.hip", "rg_api.cpp"]
+TEST_LIB = os.path.join(LIBDIR, "librg_aead_test.so")
+KERNELS = ["rg_kernels.hip", "rg_tile.hip", "rg_pipe.hip", "rg_flat.hip", "rg_mac.hip"]
+API = "rg_api.cpp"
+SOURCES = KERNELS + [API]
 HEADERS = ["rg_device.h", "rg_internal.h"]
 ARCH = os.environ.get("RG_OFFLOAD_ARCH", "gfx950")
 
 
 def _inputs():
-    return [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(REPO, "include", "rg_aead.h")]
+    return ([os.path.join(CSRC, f) for f in SOURCES + HEADERS] +
+            [os.path.join(REPO, "include", h) for h in ("rg_aead.h", "rg_aead_test.h")])
 
 
 def up_to_date() -> bool:
-    if not os.path.exists(LIB):
+    if not (os.path.exists(LIB) and os.path.exists(TEST_LIB)):
         return False
-    t = os.path.getmtime(LIB)
+    t = min(os.path.getmtime(LIB), os.path.getmtime(TEST_LIB))
     return all(os.path.getmtime(p) <= t for p in _inputs())
+
+
+def _compile(hipcc: str, src: str, obj: str, defines, verbose: bool):
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", *defines,
+           "-I", os.path.join(REPO, "include"), "-c", os.path.join(CSRC, src), "-o", obj]
+    if src.endswith(".cpp"):
+        cmd[1:1] = ["-x", "hip"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    return obj
+
+
+def _link(hipcc: str, out: str, objs):
+    tmp = out + ".tmp"
+    subprocess.run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + list(objs), check=True)
+    os.replace(tmp, out)
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
@@ -35,20 +64,14 @@ def build(force: bool = False, verbose: bool = False) -> str:
         return LIB
     os.makedirs(LIBDIR, exist_ok=True)
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    objs = []
-    for src in SOURCES:
-        obj = os.path.join(LIBDIR, src + ".o")
-        cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
-               "-I", os.path.join(REPO, "include"), "-c", os.path.join(CSRC, src), "-o", obj]
-        if src.endswith(".cpp"):
-            cmd[1:1] = ["-x", "hip"]
-        if verbose:
-            print(" ".join(cmd), flush=True)
-        subprocess.run(cmd, check=True)
-        objs.append(obj)
-    tmp = LIB + ".tmp"
-    subprocess.run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs, check=True)
-    os.replace(tmp, LIB)
+    jobs = [(src, os.path.join(LIBDIR, src + ".o"), ()) for src in SOURCES]
+    jobs.append((API, os.path.join(LIBDIR, "rg_api_test.cpp.o"), ("-DRG_TEST_HOOKS=1",)))
+    # the largest kernel files take ~50 s each: compile them side by side
+    with ThreadPoolExecutor(max_workers=min(len(jobs), os.cpu_count() or 1)) as ex:
+        objs = list(ex.map(lambda j: _compile(hipcc, j[0], j[1], j[2], verbose), jobs))
+    kernel_objs = objs[:len(KERNELS)]
+    _link(hipcc, LIB, kernel_objs + [objs[len(KERNELS)]])
+    _link(hipcc, TEST_LIB, kernel_objs + [objs[-1]])
     return LIB
 
 

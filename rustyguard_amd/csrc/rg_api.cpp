@@ -16,6 +16,9 @@
 #include <vector>
 
 #include "rg_internal.h"
+#if RG_TEST_HOOKS
+#include "../../include/rg_aead_test.h"
+#endif
 
 namespace {
 
@@ -37,7 +40,9 @@ int set_err(int code, const char *what, hipError_t e = hipSuccess) {
         if (e_ != hipSuccess) return set_err(RG_EDEVICE, what, e_);          \
     } while (0)
 
-// test hook (rg_debug_fail_reserve): the n-th following allocation of a DevBuf / HostBuf fails
+#if RG_TEST_HOOKS
+// test hook (rg_debug_fail_reserve, test library only): the n-th following allocation of a DevBuf /
+// HostBuf fails
 std::atomic<int> g_fail_reserve{0};
 bool injected_failure() {
     int v = g_fail_reserve.load();
@@ -45,15 +50,24 @@ bool injected_failure() {
         if (g_fail_reserve.compare_exchange_weak(v, v - 1)) return v == 1;
     return false;
 }
+#else
+constexpr bool injected_failure() { return false; }
+#endif
 
 // grow-only device allocation.  `secret` buffers hold key material: they are zeroed before their
-// memory goes back to the allocator (the reference zeroizes keys on drop, prim.rs:227-231).
+// memory goes back to the allocator (the reference zeroizes keys on drop, prim.rs:227-231).  The
+// wipe waits for the whole device first: the buffer's last reader may be a kernel on any stream
+// (a caller's non-blocking stream, or the context's own), which a null-stream hipMemset does not
+// order itself behind.
 struct DevBuf {
     void *p = nullptr;
     size_t cap = 0;
     bool secret = false;
     void drop() {
-        if (p && secret) (void)hipMemset(p, 0, cap);
+        if (p && secret) {
+            (void)hipDeviceSynchronize();
+            (void)hipMemset(p, 0, cap);
+        }
         if (p) (void)hipFree(p);
         p = nullptr;
         cap = 0;
@@ -319,15 +333,26 @@ int rg_set_segments(rg_ctx *ctx, int k) {
     return RG_OK;
 }
 
+// Diagnostics exist only in diagnostic builds (-DRG_DIAG, tools/build_variant.sh): the product library
+// accepts mode 0 and a null stamp buffer and refuses everything else, so no context of it can emit
+// frames that are not sealed (the seal contract, prim.rs:179-188, always encrypts).
 int rg_set_debug_buffer(rg_ctx *ctx, void *dev_ptr) {
     if (!ctx) return set_err(RG_EINVAL, "null context");
+#if RG_DIAG
     ctx->dbg = static_cast<uint64_t *>(dev_ptr);
+#else
+    if (dev_ptr) return set_err(RG_EINVAL, "stamp buffers exist only in diagnostic builds (RG_DIAG)");
+#endif
     return RG_OK;
 }
 
 int rg_set_debug_mode(rg_ctx *ctx, int mode) {
     if (!ctx) return set_err(RG_EINVAL, "null context");
+#if RG_DIAG
     if (mode < 0 || mode > 8) return set_err(RG_EINVAL, "debug mode must be 0..8");
+#else
+    if (mode != 0) return set_err(RG_EINVAL, "debug modes exist only in diagnostic builds (RG_DIAG)");
+#endif
     ctx->debug_mode = mode;
     return RG_OK;
 }
@@ -414,9 +439,10 @@ static hipError_t launch_pipe_any(rg_ctx *ctx, const rg::SealArgs *sa, const rg:
     }
     if (!plan) return rg::launch_pipe(sa, oa, L, nullptr, st);
     rg::Launch Lp = L;
-    // two waves per SIMD by default: one wave's tile prologue (descriptor -> key
-    // -> first chunks) and divergent tails overlap the other's keystream (config 3
-    // +8 % over one wave per SIMD; ChaCha alone gains nothing from a second wave)
+    // two workgroups per CU are asked for, but the kernels' register budget (268 / 264 VGPR+AGPR, above
+    // 256) admits one wave per SIMD, and the occupancy query (pipe_max_wg) caps the request at that:
+    // the planned kernel runs one wave per SIMD.  Two co-resident waves, forced with
+    // __launch_bounds__(256, 2), measured slower on config 2 (profiles/r4_cfg2_twowave.txt).
     const int want_wg = ctx->wg_per_cu > 0 ? ctx->wg_per_cu : 2;
     Lp.wg_per_cu = std::min(want_wg, std::max(1, ctx->pipe_max_wg[oa ? 1 : 0]));
     hipError_t e = pb.reserve(n);
@@ -466,7 +492,7 @@ static hipError_t launch_seal_any(rg_ctx *ctx, const rg::SealArgs &a0, PlanBuf &
     rg::Launch L = launch_cfg(ctx, a.n, false);
     L.staged_g = pick_family(ctx, L.staged_g, pb, st);
     ctx->last_kernel = L.staged_g;
-    // stamps: debug mode 3, or any diagnostic mode of the pipelined kernel
+    // stamps (diagnostic builds): debug mode 3, or any diagnostic mode of the pipelined kernel
     a.dbg = L.debug_mode == 3 || (L.staged_g == 0 && L.debug_mode != 0) ? ctx->dbg : nullptr;
     if (L.staged_g == 3) return launch_flat_any(ctx, &a, nullptr, st);
     if (L.staged_g == 0) return launch_pipe_any(ctx, &a, nullptr, pb, L, st);
@@ -654,91 +680,138 @@ int finish_slot(Slot &s, uint8_t *status, uint64_t *counters_out) {
     return RG_OK;
 }
 
-// Shared driver of the two host entry points.
+// Shared driver of the host entry points: packets [i, end) of the caller's arrays through one
+// context's three-slot H2D -> kernel -> D2H pipeline, one slice per step().  A group (rg_group)
+// drives one run per context and steps them round-robin from one thread.
+struct HostRun {
+    rg_ctx *ctx;
+    bool open;
+    uint32_t nkeys;
+    const rg_pkt_desc *desc;
+    const uint64_t *counters;
+    size_t i, end;
+    uint8_t *buf;
+    size_t buf_len;
+    uint8_t *status;
+    uint64_t *counters_out;
+    bool with_receivers;
+    int which = 0;
+
+    bool done() const { return i >= end; }
+    int step(); // enqueue the next slice (after draining the slot it reuses)
+    int drain() {
+        for (auto &s : ctx->slots) {
+            int rc = finish_slot(s, status, open ? counters_out : nullptr);
+            if (rc) return rc;
+        }
+        return RG_OK;
+    }
+};
+
+int HostRun::step() {
+    RG_HIP(hipSetDevice(ctx->device), "hipSetDevice");
+    // slice [i, j): bounded by packet count and by the byte span of its frames
+    size_t j = i;
+    uint64_t lo = UINT64_MAX, hi = 0;
+    while (j < end && j - i < kSlicePkts) {
+        const rg_pkt_desc &d = desc[j];
+        if (in_arena(d, open, buf_len)) {
+            const uint64_t e = d.offset + (uint64_t)d.len + (open ? 0 : 32);
+            const uint64_t nlo = std::min<uint64_t>(lo, d.offset & ~15ull), nhi = std::max<uint64_t>(hi, e);
+            if (j > i && nhi - nlo > kSliceBytes) break;
+            lo = nlo;
+            hi = nhi;
+        }
+        ++j;
+    }
+    if (lo == UINT64_MAX) lo = hi = 0; // nothing in range: only statuses come back
+    Slot &s = ctx->slots[which];
+    int rc = finish_slot(s, status, counters_out);
+    if (rc) return rc;
+    const size_t m = j - i;
+    const size_t span = hi - lo;
+    RG_HIP(s.d_buf.reserve(span + 16), "alloc slice");
+    RG_HIP(s.d_desc.reserve(m * sizeof(rg_pkt_desc)), "alloc desc");
+    RG_HIP(s.d_status.reserve(m), "alloc status");
+    RG_HIP(s.h_desc.reserve(m * sizeof(rg_pkt_desc)), "alloc h_desc");
+    RG_HIP(s.h_status.reserve(m), "alloc h_status");
+    rg_pkt_desc *hd = static_cast<rg_pkt_desc *>(s.h_desc.p);
+    for (size_t k = 0; k < m; ++k) {
+        hd[k] = desc[i + k];
+        // frames outside the arena get an aligned out-of-range offset: the kernel flags them INVALID
+        hd[k].offset = in_arena(desc[i + k], open, buf_len) ? desc[i + k].offset - lo : kOutOfRange;
+    }
+    hipStream_t st = s.stream;
+    RG_HIP(hipMemcpyAsync(s.d_desc.p, hd, m * sizeof(rg_pkt_desc), hipMemcpyHostToDevice, st), "H2D desc");
+    if (span) RG_HIP(hipMemcpyAsync(s.d_buf.p, buf + lo, span, hipMemcpyHostToDevice, st), "H2D frames");
+    uint8_t *dbuf = static_cast<uint8_t *>(s.d_buf.p);
+    if (!open) {
+        RG_HIP(s.d_ctr.reserve(m * 8), "alloc ctr");
+        RG_HIP(s.h_ctr.reserve(m * 8), "alloc h_ctr");
+        memcpy(s.h_ctr.p, counters + i, m * 8);
+        RG_HIP(hipMemcpyAsync(s.d_ctr.p, s.h_ctr.p, m * 8, hipMemcpyHostToDevice, st), "H2D ctr");
+        rg::SealArgs a{};
+        a.keys = static_cast<const uint32_t *>(ctx->d_keys.p);
+        a.receivers = with_receivers ? static_cast<const uint32_t *>(ctx->d_recv.p) : nullptr;
+        a.desc = static_cast<const rg_pkt_desc *>(s.d_desc.p);
+        a.counters = static_cast<const uint64_t *>(s.d_ctr.p);
+        a.buf = dbuf;
+        a.buf_len = span;
+        a.status = static_cast<uint8_t *>(s.d_status.p);
+        a.nkeys = nkeys;
+        a.n = (uint32_t)m;
+        RG_HIP(launch_seal_any(ctx, a, s.plan, st), "seal launch");
+    } else {
+        RG_HIP(s.d_ctr_out.reserve(m * 8), "alloc ctr_out");
+        RG_HIP(s.h_ctr_out.reserve(m * 8), "alloc h_ctr_out");
+        rg::OpenArgs a{};
+        a.keys = static_cast<const uint32_t *>(ctx->d_keys.p);
+        a.desc = static_cast<const rg_pkt_desc *>(s.d_desc.p);
+        a.buf = dbuf;
+        a.buf_len = span;
+        a.status = static_cast<uint8_t *>(s.d_status.p);
+        a.counters_out = static_cast<uint64_t *>(s.d_ctr_out.p);
+        a.nkeys = nkeys;
+        a.n = (uint32_t)m;
+        RG_HIP(launch_open_any(ctx, a, s.plan, st), "open launch");
+        RG_HIP(hipMemcpyAsync(s.h_ctr_out.p, s.d_ctr_out.p, m * 8, hipMemcpyDeviceToHost, st), "D2H ctr");
+    }
+    if (span) RG_HIP(hipMemcpyAsync(buf + lo, s.d_buf.p, span, hipMemcpyDeviceToHost, st), "D2H frames");
+    RG_HIP(hipMemcpyAsync(s.h_status.p, s.d_status.p, m, hipMemcpyDeviceToHost, st), "D2H status");
+    s.i0 = i;
+    s.i1 = j;
+    s.busy = true;
+    i = j;
+    which = (which + 1) % 3;
+    return RG_OK;
+}
+
+// Runs to completion, stepped round-robin (one context, or every context of a group).  On an error
+// every run still drains what it has in flight (its slots are reused by the next call).
+int run_host(std::vector<HostRun> &runs) {
+    int rc = RG_OK;
+    for (bool more = true; more && rc == RG_OK;) {
+        more = false;
+        for (auto &r : runs) {
+            if (r.done()) continue;
+            rc = r.step();
+            if (rc) break;
+            more |= !r.done();
+        }
+    }
+    for (auto &r : runs) {
+        (void)hipSetDevice(r.ctx->device);
+        const int rc2 = r.drain();
+        if (rc == RG_OK) rc = rc2;
+    }
+    return rc;
+}
+
 int host_batch(rg_ctx *ctx, bool open, uint32_t nkeys, const rg_pkt_desc *desc, const uint64_t *counters, size_t n,
                uint8_t *buf, size_t buf_len, uint8_t *status, uint64_t *counters_out, bool with_receivers) {
-    size_t i = 0;
-    int which = 0;
-    while (i < n) {
-        // slice [i, j): bounded by packet count and by the byte span of its frames
-        size_t j = i;
-        uint64_t lo = UINT64_MAX, hi = 0;
-        while (j < n && j - i < kSlicePkts) {
-            const rg_pkt_desc &d = desc[j];
-            if (in_arena(d, open, buf_len)) {
-                const uint64_t end = d.offset + (uint64_t)d.len + (open ? 0 : 32);
-                const uint64_t nlo = std::min<uint64_t>(lo, d.offset & ~15ull), nhi = std::max<uint64_t>(hi, end);
-                if (j > i && nhi - nlo > kSliceBytes) break;
-                lo = nlo;
-                hi = nhi;
-            }
-            ++j;
-        }
-        if (lo == UINT64_MAX) lo = hi = 0; // nothing in range: only statuses come back
-        Slot &s = ctx->slots[which];
-        int rc = finish_slot(s, status, counters_out);
-        if (rc) return rc;
-        const size_t m = j - i;
-        const size_t span = hi - lo;
-        RG_HIP(s.d_buf.reserve(span + 16), "alloc slice");
-        RG_HIP(s.d_desc.reserve(m * sizeof(rg_pkt_desc)), "alloc desc");
-        RG_HIP(s.d_status.reserve(m), "alloc status");
-        RG_HIP(s.h_desc.reserve(m * sizeof(rg_pkt_desc)), "alloc h_desc");
-        RG_HIP(s.h_status.reserve(m), "alloc h_status");
-        rg_pkt_desc *hd = static_cast<rg_pkt_desc *>(s.h_desc.p);
-        for (size_t k = 0; k < m; ++k) {
-            hd[k] = desc[i + k];
-            // frames outside the arena get an aligned out-of-range offset: the kernel flags them INVALID
-            hd[k].offset = in_arena(desc[i + k], open, buf_len) ? desc[i + k].offset - lo : kOutOfRange;
-        }
-        hipStream_t st = s.stream;
-        RG_HIP(hipMemcpyAsync(s.d_desc.p, hd, m * sizeof(rg_pkt_desc), hipMemcpyHostToDevice, st), "H2D desc");
-        if (span) RG_HIP(hipMemcpyAsync(s.d_buf.p, buf + lo, span, hipMemcpyHostToDevice, st), "H2D frames");
-        uint8_t *dbuf = static_cast<uint8_t *>(s.d_buf.p);
-        if (!open) {
-            RG_HIP(s.d_ctr.reserve(m * 8), "alloc ctr");
-            RG_HIP(s.h_ctr.reserve(m * 8), "alloc h_ctr");
-            memcpy(s.h_ctr.p, counters + i, m * 8);
-            RG_HIP(hipMemcpyAsync(s.d_ctr.p, s.h_ctr.p, m * 8, hipMemcpyHostToDevice, st), "H2D ctr");
-            rg::SealArgs a{};
-            a.keys = static_cast<const uint32_t *>(ctx->d_keys.p);
-            a.receivers = with_receivers ? static_cast<const uint32_t *>(ctx->d_recv.p) : nullptr;
-            a.desc = static_cast<const rg_pkt_desc *>(s.d_desc.p);
-            a.counters = static_cast<const uint64_t *>(s.d_ctr.p);
-            a.buf = dbuf;
-            a.buf_len = span;
-            a.status = static_cast<uint8_t *>(s.d_status.p);
-            a.nkeys = nkeys;
-            a.n = (uint32_t)m;
-            RG_HIP(launch_seal_any(ctx, a, s.plan, st), "seal launch");
-        } else {
-            RG_HIP(s.d_ctr_out.reserve(m * 8), "alloc ctr_out");
-            RG_HIP(s.h_ctr_out.reserve(m * 8), "alloc h_ctr_out");
-            rg::OpenArgs a{};
-            a.keys = static_cast<const uint32_t *>(ctx->d_keys.p);
-            a.desc = static_cast<const rg_pkt_desc *>(s.d_desc.p);
-            a.buf = dbuf;
-            a.buf_len = span;
-            a.status = static_cast<uint8_t *>(s.d_status.p);
-            a.counters_out = static_cast<uint64_t *>(s.d_ctr_out.p);
-            a.nkeys = nkeys;
-            a.n = (uint32_t)m;
-            RG_HIP(launch_open_any(ctx, a, s.plan, st), "open launch");
-            RG_HIP(hipMemcpyAsync(s.h_ctr_out.p, s.d_ctr_out.p, m * 8, hipMemcpyDeviceToHost, st), "D2H ctr");
-        }
-        if (span) RG_HIP(hipMemcpyAsync(buf + lo, s.d_buf.p, span, hipMemcpyDeviceToHost, st), "D2H frames");
-        RG_HIP(hipMemcpyAsync(s.h_status.p, s.d_status.p, m, hipMemcpyDeviceToHost, st), "D2H status");
-        s.i0 = i;
-        s.i1 = j;
-        s.busy = true;
-        i = j;
-        which = (which + 1) % 3;
-    }
-    for (auto &s : ctx->slots) {
-        int rc = finish_slot(s, status, open ? counters_out : nullptr);
-        if (rc) return rc;
-    }
-    return RG_OK;
+    std::vector<HostRun> runs{HostRun{ctx, open, nkeys, desc, counters, 0, n, buf, buf_len, status, counters_out,
+                                      with_receivers}};
+    return run_host(runs);
 }
 
 } // namespace
@@ -780,6 +853,171 @@ int rg_open_batch_host(rg_ctx *ctx, const uint8_t *keys, uint32_t nkeys, const r
     return host_batch(ctx, true, nkeys, desc, nullptr, n, buf, buf_len, status, counters_out, false);
 }
 
+} // extern "C"
+
+// ------------------------------------------------------------ device group
+struct rg_group {
+    std::vector<rg_ctx *> ctx;
+};
+
+namespace {
+
+// work of packet i for the split: its AEAD payload bytes plus one 64-byte one-time-key block
+uint64_t split_work(const rg_pkt_desc &d, bool open) {
+    const uint64_t P = open ? (d.len >= 32 ? d.len - 32 : 0) : d.len;
+    return std::min<uint64_t>(P, rg::kMaxPayload) + 64;
+}
+
+void split_bounds(const rg_pkt_desc *desc, size_t n, bool open, int parts, size_t *bounds) {
+    uint64_t total = 0;
+    for (size_t i = 0; i < n; ++i) total += split_work(desc[i], open);
+    bounds[0] = 0;
+    size_t i = 0;
+    uint64_t run = 0;
+    for (int k = 1; k < parts; ++k) {
+        // the first index whose running work before it reaches k / parts of the total
+        const uint64_t target = (uint64_t)((long double)total * k / parts);
+        while (i < n && run + split_work(desc[i], open) / 2 < target) run += split_work(desc[i++], open);
+        bounds[k] = i;
+    }
+    bounds[parts] = n;
+}
+
+// the caller's current HIP device, put back on the way out: a group call switches devices as it goes,
+// and the caller (a torch program, say) keeps its own device selected
+struct DeviceGuard {
+    int dev = -1;
+    DeviceGuard() { (void)hipGetDevice(&dev); }
+    ~DeviceGuard() {
+        if (dev >= 0) (void)hipSetDevice(dev);
+    }
+};
+
+// every context of the group, locked in index order (a group's calls are serialised per context as
+// a single context's are)
+struct GroupLock {
+    std::vector<std::unique_lock<std::mutex>> held;
+    explicit GroupLock(rg_group *g) {
+        for (rg_ctx *c : g->ctx) held.emplace_back(c->mu);
+    }
+};
+
+int host_multi(rg_group *g, bool open, const uint8_t *keys, const uint32_t *receivers, uint32_t nkeys,
+               const rg_pkt_desc *desc, const uint64_t *counters, size_t n, uint8_t *buf, size_t buf_len,
+               uint8_t *status, uint64_t *counters_out) {
+    DeviceGuard dg;
+    GroupLock lk(g);
+    const int parts = (int)g->ctx.size();
+    std::vector<size_t> b(parts + 1);
+    split_bounds(desc, n, open, parts, b.data());
+    std::vector<HostRun> runs;
+    for (int k = 0; k < parts; ++k) {
+        rg_ctx *c = g->ctx[k];
+        if (b[k] == b[k + 1]) continue;
+        RG_HIP(hipSetDevice(c->device), "hipSetDevice");
+        int rc = upload_keys(c, keys, receivers, nkeys);
+        if (rc) return rc;
+        runs.push_back(HostRun{c, open, nkeys, desc, counters, b[k], b[k + 1], buf, buf_len, status, counters_out,
+                               receivers != nullptr});
+    }
+    return run_host(runs);
+}
+
+} // namespace
+
+extern "C" {
+
+int rg_group_create(const int *devices, int n, rg_group **out) {
+    if (!out) return set_err(RG_EINVAL, "group: null out");
+    *out = nullptr;
+    if (!devices || n <= 0 || n > 64) return set_err(RG_EINVAL, "group: 1..64 devices");
+    rg_group *g = new (std::nothrow) rg_group();
+    if (!g) return set_err(RG_ENOMEM, "alloc group");
+    DeviceGuard dg;
+    for (int i = 0; i < n; ++i) {
+        rg_ctx *c = nullptr;
+        int rc = rg_create(devices[i], &c);
+        if (rc) {
+            rg_group_destroy(g);
+            return rc;
+        }
+        g->ctx.push_back(c);
+    }
+    *out = g;
+    return RG_OK;
+}
+
+void rg_group_destroy(rg_group *g) {
+    if (!g) return;
+    DeviceGuard dg;
+    for (rg_ctx *c : g->ctx) rg_destroy(c);
+    delete g;
+}
+
+int rg_group_size(const rg_group *g) { return g ? (int)g->ctx.size() : set_err(RG_EINVAL, "group: null"); }
+
+rg_ctx *rg_group_ctx(rg_group *g, int i) {
+    if (!g || i < 0 || i >= (int)g->ctx.size()) return nullptr;
+    return g->ctx[i];
+}
+
+int rg_split_batch(const rg_pkt_desc *desc, size_t n, int open, int parts, size_t *bounds) {
+    if (!bounds || parts <= 0 || (n && !desc)) return set_err(RG_EINVAL, "split: bad args");
+    split_bounds(desc, n, open != 0, parts, bounds);
+    return RG_OK;
+}
+
+int rg_seal_batch_host_multi(rg_group *g, const uint8_t *keys, const uint32_t *receivers, uint32_t nkeys,
+                             const rg_pkt_desc *desc, const uint64_t *counters, size_t n, uint8_t *buf,
+                             size_t buf_len, uint8_t *status) {
+    if (!g || g->ctx.empty()) return set_err(RG_EINVAL, "seal_host_multi: null group");
+    if (n == 0) return RG_OK;
+    if (!keys || !desc || !counters || !buf || nkeys == 0) return set_err(RG_EINVAL, "seal_host_multi: bad args");
+    std::vector<uint8_t> tmp;
+    if (!status) {
+        tmp.resize(n);
+        status = tmp.data();
+    }
+    return host_multi(g, false, keys, receivers, nkeys, desc, counters, n, buf, buf_len, status, nullptr);
+}
+
+int rg_open_batch_host_multi(rg_group *g, const uint8_t *keys, uint32_t nkeys, const rg_pkt_desc *desc, size_t n,
+                             uint8_t *buf, size_t buf_len, uint8_t *status, uint64_t *counters_out) {
+    if (!g || g->ctx.empty()) return set_err(RG_EINVAL, "open_host_multi: null group");
+    if (n == 0) return RG_OK;
+    if (!keys || !desc || !buf || !status || nkeys == 0) return set_err(RG_EINVAL, "open_host_multi: bad args");
+    std::vector<uint64_t> tmp;
+    if (!counters_out) {
+        tmp.resize(n);
+        counters_out = tmp.data();
+    }
+    return host_multi(g, true, keys, nullptr, nkeys, desc, nullptr, n, buf, buf_len, status, counters_out);
+}
+
+int rg_seal_batch_dev_multi(rg_group *g, const rg_dev_shard *sh) {
+    if (!g || !sh) return set_err(RG_EINVAL, "seal_dev_multi: bad args");
+    DeviceGuard dg;
+    for (size_t k = 0; k < g->ctx.size(); ++k) {
+        const rg_dev_shard &x = sh[k];
+        int rc = rg_seal_batch_dev(g->ctx[k], x.keys, x.receivers, x.nkeys, x.desc, x.counters, x.n, x.buf, x.buf_len,
+                                   x.status, x.stream);
+        if (rc) return rc;
+    }
+    return RG_OK;
+}
+
+int rg_open_batch_dev_multi(rg_group *g, const rg_dev_shard *sh) {
+    if (!g || !sh) return set_err(RG_EINVAL, "open_dev_multi: bad args");
+    DeviceGuard dg;
+    for (size_t k = 0; k < g->ctx.size(); ++k) {
+        const rg_dev_shard &x = sh[k];
+        int rc = rg_open_batch_dev(g->ctx[k], x.keys, x.nkeys, x.desc, x.n, x.buf, x.buf_len, x.status, x.counters_out,
+                                   x.stream);
+        if (rc) return rc;
+    }
+    return RG_OK;
+}
+
 // ---------------------------------------------------- per-message drop-in
 // nonce: 12 bytes, or 24 for XChaCha20-Poly1305 (xchacha)
 static int general_one(rg_ctx *ctx, bool dec, const uint8_t key[32], const uint8_t *nonce, const uint8_t *aad,
@@ -817,6 +1055,20 @@ static int general_one(rg_ctx *ctx, bool dec, const uint8_t key[32], const uint8
     job.payload_len = len;
     job.tag_off = tag_off;
     memcpy(h, &job, sizeof job);
+    // from here on the key sits in the pinned image (and, after the H2D copy, in the device arena):
+    // wiped on every way out, errors included (the reference zeroizes keys on drop, prim.rs:227-231)
+    struct Wipe {
+        uint8_t *h, *d;
+        size_t n;
+        hipStream_t st;
+        ~Wipe() {
+            (void)hipStreamSynchronize(st); // nothing of this call is still reading the job
+            (void)hipMemsetAsync(d, 0, n, st);
+            (void)hipStreamSynchronize(st);
+            memset(h, 0, n);
+        }
+    } wipe{h, d, job_bytes, ctx->slots[0].stream};
+    memset(&job.key, 0, sizeof job.key); // the stack copy
     uint8_t *hb = h + job_bytes; // arena base as the kernel sees it; padding zeroed (pad16)
     memset(hb, 0, tag_off + 16);
     if (aad_len) memcpy(hb + aad_off, aad, aad_len);
@@ -826,12 +1078,9 @@ static int general_one(rg_ctx *ctx, bool dec, const uint8_t key[32], const uint8
     RG_HIP(hipMemcpyAsync(d, h, arena, hipMemcpyHostToDevice, st), "H2D arena");
     RG_HIP(rg::launch_general(reinterpret_cast<rg::GeneralJob *>(d), 1, d + job_bytes, st), "general launch");
     RG_HIP(hipMemcpyAsync(h, d, arena, hipMemcpyDeviceToHost, st), "D2H arena");
-    // the key does not stay in device memory either (prim.rs:227-231 zeroizes on drop)
-    RG_HIP(hipMemsetAsync(d, 0, job_bytes, st), "wipe arena key");
     RG_HIP(hipStreamSynchronize(st), "general sync");
-    memcpy(&job, h, sizeof job);
-    memset(h, 0, sizeof job); // the key does not stay in the pinned image
-    if (dec && job.status != RG_PKT_OK) return RG_PKT_DECRYPT_ERR; // payload untouched
+    const uint32_t status = reinterpret_cast<const rg::GeneralJob *>(h)->status;
+    if (dec && status != RG_PKT_OK) return RG_PKT_DECRYPT_ERR; // payload untouched
     if (len) memcpy(payload, hb + pay_off, len);
     if (!dec) memcpy(tag, hb + tag_off, 16);
     return RG_OK;
@@ -858,6 +1107,9 @@ int rg_xchacha20poly1305_dec(rg_ctx *ctx, const uint8_t key[32], const uint8_t n
 }
 
 // ------------------------------------------------------------ test hooks
+// Built into the test library only (librg_aead_test.so, -DRG_TEST_HOOKS; include/rg_aead_test.h),
+// never into the product library.
+#if RG_TEST_HOOKS
 int rg_debug_read_arena(rg_ctx *ctx, int which, void *dst, size_t bytes) {
     int rc = check_ctx(ctx);
     if (rc) return rc;
@@ -871,6 +1123,7 @@ int rg_debug_read_arena(rg_ctx *ctx, int which, void *dst, size_t bytes) {
 }
 
 void rg_debug_fail_reserve(int nth) { g_fail_reserve.store(nth > 0 ? nth : 0); }
+#endif
 
 // ------------------------------------------------------------- AntiReplay
 // rustyguard-utils/src/anti_replay.rs:1-64 with usize = u64:
@@ -914,6 +1167,12 @@ struct Session {
     // keepalive is already scheduled; plus the peer endpoint learned from authenticated packets
     uint64_t started = 0, sent = 0;
     bool keepalive_pending = false;
+    bool has_endpoint = false; // sessions without a peer (rg_sessions_insert) keep their own endpoint
+    uint64_t endpoint = 0;
+    uint32_t peer = RG_PEER_NONE;
+};
+// PeerState's endpoint (rustyguard-core/src/lib.rs:160-181, :670-671): shared by the peer's sessions
+struct Peer {
     bool has_endpoint = false;
     uint64_t endpoint = 0;
 };
@@ -953,12 +1212,14 @@ struct SessDev {
 
 struct rg_sessions {
     rg_ctx *ctx = nullptr;
+    rg_group *group = nullptr; // host-frame batches on every context of the group (ctx = its first)
     uint32_t cap = 0;
     uint64_t now = 0; // Sessions' clock (state.now, advanced by turn: lib.rs:396-413), nanoseconds
     std::vector<Session> s;
     std::vector<uint8_t> keys;       // rows [0,cap): send keys, [cap,2cap): recv keys
     std::vector<uint32_t> receivers; // remote ids for send rows
     std::unordered_map<uint32_t, uint32_t> by_local;
+    std::unordered_map<uint32_t, Peer> peers;
     SessDev dev;
 };
 
@@ -987,9 +1248,15 @@ uint8_t replay_step(rg_sessions *s, uint32_t slot, uint64_t ctr, uint8_t st, con
         x.keepalive_pending = true;
         f |= RG_RECV_KEEPALIVE;
     }
-    if (src) {
-        x.endpoint = src[i];
-        x.has_endpoint = true;
+    if (src) { // the peer's endpoint moves (the session's own without a peer)
+        if (x.peer != RG_PEER_NONE) {
+            Peer &p = s->peers[x.peer];
+            p.endpoint = src[i];
+            p.has_endpoint = true;
+        } else {
+            x.endpoint = src[i];
+            x.has_endpoint = true;
+        }
     }
     *fl = f;
     return RG_PKT_OK;
@@ -1056,6 +1323,13 @@ int rg_sessions_create(rg_ctx *ctx, uint32_t capacity, rg_sessions **out) {
     return RG_OK;
 }
 
+int rg_sessions_create_group(rg_group *g, uint32_t capacity, rg_sessions **out) {
+    if (!g || g->ctx.empty()) return set_err(RG_EINVAL, "sessions: null group");
+    int rc = rg_sessions_create(g->ctx[0], capacity, out);
+    if (rc == RG_OK) (*out)->group = g;
+    return rc;
+}
+
 void rg_sessions_destroy(rg_sessions *s) {
     if (!s) return;
     std::fill(s->keys.begin(), s->keys.end(), 0); // zeroize, as prim.rs:227-231 / lib.rs:216-228
@@ -1078,6 +1352,11 @@ void rg_sessions_destroy(rg_sessions *s) {
 
 int rg_sessions_insert(rg_sessions *s, uint32_t local_id, uint32_t remote_id, const uint8_t send_key[32],
                        const uint8_t recv_key[32]) {
+    return rg_sessions_insert_peer(s, local_id, remote_id, send_key, recv_key, RG_PEER_NONE);
+}
+
+int rg_sessions_insert_peer(rg_sessions *s, uint32_t local_id, uint32_t remote_id, const uint8_t send_key[32],
+                            const uint8_t recv_key[32], uint32_t peer) {
     if (!s || !send_key || !recv_key) return set_err(RG_EINVAL, "insert: bad args");
     if (s->dev.rv.pending) return set_err(RG_EINVAL, "insert: a device receive batch is pending");
     if (s->by_local.count(local_id)) return set_err(RG_EINVAL, "insert: local id in use");
@@ -1089,6 +1368,8 @@ int rg_sessions_insert(rg_sessions *s, uint32_t local_id, uint32_t remote_id, co
         x.local_id = local_id;
         x.remote_id = remote_id;
         x.started = x.sent = s->now; // handshake.rs:119-124, :215-216
+        x.peer = peer;
+        if (peer != RG_PEER_NONE) (void)s->peers[peer]; // the record exists from the peer's first session
         memcpy(&s->keys[(size_t)i * 32], send_key, 32);
         memcpy(&s->keys[((size_t)s->cap + i) * 32], recv_key, 32);
         s->receivers[i] = remote_id;
@@ -1136,10 +1417,20 @@ void rg_sessions_set_time(rg_sessions *s, uint64_t now_ns) {
     if (s) s->now = now_ns;
 }
 
+int rg_peer_endpoint(const rg_sessions *s, uint32_t peer, uint64_t *src_out) {
+    if (!s || !src_out || peer == RG_PEER_NONE) return set_err(RG_EINVAL, "peer_endpoint: bad args");
+    auto it = s->peers.find(peer);
+    if (it == s->peers.end() || !it->second.has_endpoint) return RG_ENOTFOUND;
+    *src_out = it->second.endpoint;
+    return RG_OK;
+}
+
 int rg_sessions_endpoint(const rg_sessions *s, uint32_t slot, uint64_t *src_out) {
     if (!s || slot >= s->cap || !s->s[slot].used || !src_out) return set_err(RG_EINVAL, "endpoint: bad slot");
-    if (!s->s[slot].has_endpoint) return RG_ENOTFOUND;
-    *src_out = s->s[slot].endpoint;
+    const Session &x = s->s[slot];
+    if (x.peer != RG_PEER_NONE) return rg_peer_endpoint(s, x.peer, src_out);
+    if (!x.has_endpoint) return RG_ENOTFOUND;
+    *src_out = x.endpoint;
     return RG_OK;
 }
 
@@ -1148,6 +1439,14 @@ int rg_sessions_keepalive_due(rg_sessions *s, uint32_t slot) {
     Session &x = s->s[slot];
     x.keepalive_pending = false;                     // time.rs:118
     return x.sent + kKeepaliveTimeout < s->now ? 1 : 0; // should_keepalive, lib.rs:201-203
+}
+
+int rg_sessions_keepalive(rg_sessions *s, uint32_t slot, uint64_t *dst_out) {
+    if (!dst_out) return set_err(RG_EINVAL, "keepalive: null dst");
+    const int due = rg_sessions_keepalive_due(s, slot);
+    if (due <= 0) return due;
+    const int rc = rg_sessions_endpoint(s, slot, dst_out); // peer.endpoint, time.rs:135
+    return rc == RG_OK ? 1 : rc;
 }
 
 int rg_send_batch(rg_sessions *s, const uint32_t *slots, const rg_pkt_desc *desc, size_t n, uint8_t *buf,
@@ -1178,8 +1477,10 @@ int rg_send_batch(rg_sessions *s, const uint32_t *slots, const rg_pkt_desc *desc
         d[i].key_idx = slot;
         if (rekey_out && x.send_ctr >= RG_REKEY_AFTER_MESSAGES) rekey_out[i] = 1; // lib.rs:564-570
     }
-    int rc = rg_seal_batch_host(s->ctx, s->keys.data(), s->receivers.data(), s->cap, d.data(), ctr.data(), n, buf,
-                                buf_len, status);
+    int rc = s->group ? rg_seal_batch_host_multi(s->group, s->keys.data(), s->receivers.data(), s->cap, d.data(),
+                                                 ctr.data(), n, buf, buf_len, status)
+                      : rg_seal_batch_host(s->ctx, s->keys.data(), s->receivers.data(), s->cap, d.data(), ctr.data(),
+                                           n, buf, buf_len, status);
     if (rc) return rc;
     for (size_t i = 0; i < n; ++i)
         if (host_status[i] != RG_PKT_OK) status[i] = host_status[i];
@@ -1228,7 +1529,10 @@ int rg_recv_batch_ex(rg_sessions *s, const rg_pkt_desc *desc, size_t n, uint8_t 
         host_status[i] = st;
         d[i].key_idx = st == 0xFF ? s->cap + slot_of[i] : RG_KEY_SKIP;
     }
-    int rc = rg_open_batch_host(s->ctx, s->keys.data(), 2 * s->cap, d.data(), n, buf, buf_len, status, nullptr);
+    int rc = s->group ? rg_open_batch_host_multi(s->group, s->keys.data(), 2 * s->cap, d.data(), n, buf, buf_len,
+                                                 status, nullptr)
+                      : rg_open_batch_host(s->ctx, s->keys.data(), 2 * s->cap, d.data(), n, buf, buf_len, status,
+                                           nullptr);
     if (rc) return rc;
     // in-order post-pass (RFC 6479 §3.4.3: only authenticated counters advance the window)
     std::vector<rg_pkt_desc> undo;
@@ -1258,8 +1562,10 @@ int rg_recv_batch_ex(rg_sessions *s, const rg_pkt_desc *desc, size_t n, uint8_t 
         // since the tag is the MAC of that ciphertext, the frame's own (verified) tag; without
         // receivers the header is not rewritten.  The frame is byte-for-byte what arrived.
         std::vector<uint8_t> st2(undo.size());
-        rc = rg_seal_batch_host(s->ctx, s->keys.data(), nullptr, 2 * s->cap, undo.data(), undo_ctr.data(),
-                                undo.size(), buf, buf_len, st2.data());
+        rc = s->group ? rg_seal_batch_host_multi(s->group, s->keys.data(), nullptr, 2 * s->cap, undo.data(),
+                                                 undo_ctr.data(), undo.size(), buf, buf_len, st2.data())
+                      : rg_seal_batch_host(s->ctx, s->keys.data(), nullptr, 2 * s->cap, undo.data(), undo_ctr.data(),
+                                           undo.size(), buf, buf_len, st2.data());
         if (rc) return rc;
         for (uint8_t x : st2)
             if (x != RG_PKT_OK) return set_err(RG_EDEVICE, "recv_batch: restoring a replayed frame failed");
@@ -1270,6 +1576,7 @@ int rg_recv_batch_ex(rg_sessions *s, const rg_pkt_desc *desc, size_t n, uint8_t 
 int rg_send_batch_dev(rg_sessions *s, const uint32_t *slots, const rg_pkt_desc *desc, size_t n, uint8_t *buf,
                       size_t buf_len, uint8_t *status, uint8_t *rekey_out, void *stream) {
     if (!s || !slots || !desc || !buf) return set_err(RG_EINVAL, "send_batch_dev: bad args");
+    if (s->group) return set_err(RG_EINVAL, "send_batch_dev: a group's table takes host frames (rg_send_batch)");
     if (n > 0xFFFFFFFFull) return set_err(RG_EINVAL, "send_batch_dev: too many packets");
     if (n == 0) return RG_OK;
     int rc = check_ctx(s->ctx);
@@ -1318,6 +1625,7 @@ int rg_send_batch_dev(rg_sessions *s, const uint32_t *slots, const rg_pkt_desc *
 int rg_recv_batch_dev(rg_sessions *s, const rg_pkt_desc *desc, size_t n, uint8_t *buf, size_t buf_len,
                       uint8_t *status, void *stream) {
     if (!s || !desc || !buf || !status) return set_err(RG_EINVAL, "recv_batch_dev: bad args");
+    if (s->group) return set_err(RG_EINVAL, "recv_batch_dev: a group's table takes host frames (rg_recv_batch_ex)");
     if (n > 0xFFFFFFFFull) return set_err(RG_EINVAL, "recv_batch_dev: too many packets");
     RecvStage &R = s->dev.rv;
     if (R.pending) return set_err(RG_EINVAL, "recv_batch_dev: finish the pending batch first");

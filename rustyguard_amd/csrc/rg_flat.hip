@@ -116,6 +116,11 @@ constexpr uint32_t kCoopLds = 256; // shared slots: wave totals, cut counts
 #define RG_FLAT_WAVES 4 // waves per workgroup, one workgroup per CU: one wave per SIMD
 #endif
 constexpr uint32_t kFlatWaves = RG_FLAT_WAVES;
+#ifndef RG_FLAT_WG_PER_CU
+#define RG_FLAT_WG_PER_CU 1 // resident workgroups per CU (2: two waves per SIMD)
+#endif
+constexpr uint32_t kFlatWgPerCu = RG_FLAT_WG_PER_CU;
+static_assert(kFlatWgPerCu * (kFlatWaves * sizeof(FlatLds) + 256) <= kLdsPerCu, "flat LDS images per CU");
 static_assert(kFlatWaves * sizeof(FlatLds) + 256 <= kLdsPerCu, "flat LDS image");
 
 #ifndef RG_FLAT_NTLOAD
@@ -1138,7 +1143,7 @@ hipError_t launch_flat(const SealArgs *sa, const OpenArgs *oa, bool balance, uin
     FlatArgs A{};
     if (sa) A.sa = *sa;
     if (oa) A.oa = *oa;
-    const uint32_t blocks = (uint32_t)(cus > 0 ? cus : 1);
+    const uint32_t blocks = (uint32_t)(cus > 0 ? cus : 1) * kFlatWgPerCu;
     A.units = blocks * kFlatWaves;
     A.junk = junk;
     A.balance = balance ? 1u : 0u;
@@ -1154,7 +1159,7 @@ hipError_t launch_flat(const SealArgs *sa, const OpenArgs *oa, bool balance, uin
     return hipGetLastError();
 }
 
-uint32_t flat_junk_bytes(int cus) { return (uint32_t)(cus > 0 ? cus : 1) * kFlatWaves * 64 * 64; }
+uint32_t flat_junk_bytes(int cus) { return (uint32_t)(cus > 0 ? cus : 1) * kFlatWgPerCu * kFlatWaves * 64 * 64; }
 
 hipError_t prepare_flat_kernels() {
     const int lds = (int)(kFlatWaves * sizeof(FlatLds) + kCoopLds);

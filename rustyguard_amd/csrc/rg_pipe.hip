@@ -5,24 +5,30 @@
 // EncryptedMetadata::frame_in_place (rustyguard-core/src/lib.rs:450-470).
 //
 // Why this shape (measured, tools/microbench.hip): a ChaCha20 block costs
-// ~3800 cycles per wave at 1 wave/SIMD and ~3560 at 8 waves/SIMD, so one
-// packet per lane already runs the keystream near the VALU ceiling.  What the
-// plain lane kernel loses is (a) HBM latency -- its prefetch register copy at
-// the loop head makes the wave wait for chunk t+1 one keystream period after
-// issuing it -- and (b) the serial Poly1305 chain, whose multiply-carry
+// ~3800 cycles per wave at 1 wave/SIMD and ~3820 cycles of SIMD time per
+// wave-block at 8 waves/SIMD, so one packet per lane already runs the
+// keystream at the SIMD's VALU issue rate.  What the plain lane kernel loses is
+// (a) HBM latency and (b) the serial Poly1305 chain, whose multiply-carry
 // dependencies leave issue slots empty.  Here
-//  * kDepth (3) chunk buffers rotate (the loop is unrolled kDepth times,
-//    nothing in flight is ever copied): chunk t+3 is requested as soon as
-//    chunk t is written, so a load has three keystream periods to arrive;
-//  * chunk t-1's four Poly1305 blocks are absorbed inside chunk t's keystream
-//    rounds (after double rounds 1, 3, 5, 7), where the ARX chains leave the
-//    multiply chain's latency covered;
+//  * three chunk buffers rotate (the loop is unrolled three times, nothing in
+//    flight is ever copied): chunk t+3 is requested as soon as chunk t is
+//    written, so a load has three keystream periods to arrive;
+//  * chunk t-1's four Poly1305 blocks (open: chunk t's ciphertext) are
+//    absorbed inside chunk t's keystream rounds (after double rounds 1, 3, 5,
+//    7), where the ARX chains leave the multiply chain's latency covered;
 //  * payload loads of a packet are issued before its one-time-key block, so
 //    that block hides the first chunks' latency.
 // A partial last chunk (P % 64 != 0) runs after the loop with per-block
 // predicates; the last chunk's Poly1305 blocks are absorbed after it.
-#include <type_traits>
-
+//
+// Round 4 measured two co-resident waves per SIMD (__launch_bounds__(256, 2),
+// two lanes per packet, HW_ID stamps: profiles/r4_cfg2_twowave.txt): slower.
+// The pair issues no more VALU per cycle than one wave, the memory
+// instructions are not hidden either, and the split adds a one-time-key block
+// and an r^N combine per packet.  One wave per SIMD stays.
+//
+// Diagnostic builds (-DRG_DIAG, tools/build_variant.sh; never the product
+// library) add the seal modes of pipe_step and per-wave stamps.
 #include "rg_device.h"
 #include "rg_internal.h"
 
@@ -32,15 +38,12 @@ struct Chunk {
     uint4 q0, q1, q2, q3;
 };
 
-// Chunks in flight per lane: while chunk t is processed, chunks t+1 .. t+kDepth-1
-// are loaded or loading (the load of chunk t + kDepth is issued at its end).
-#ifndef RG_PIPE_DEPTH
-#define RG_PIPE_DEPTH 3
-#endif
-constexpr int kDepth = RG_PIPE_DEPTH;
-static_assert(kDepth >= 2 && kDepth <= 4, "pipeline depth");
+// Chunks in flight per lane: while chunk t is processed, chunks t+1 .. t+2 are
+// loaded or loading (the load of chunk t + 3 is issued at its end).
+constexpr int kDepth = 3;
 
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
+// NT (diagnostic seal modes only): 1 non-temporal loads, 2 non-temporal stores, 4 stores dropped
 template <int NT> __device__ __forceinline__ uint4 ld16(const uint4 *p) {
     if constexpr (NT & 1) {
         const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(p));
@@ -48,18 +51,13 @@ template <int NT> __device__ __forceinline__ uint4 ld16(const uint4 *p) {
     } else return *p;
 }
 template <int NT> __device__ __forceinline__ void st16(uint4 *p, const uint4 &x) {
-    if constexpr (NT & 4) return; // diagnostics: payload stores dropped
+    if constexpr (NT & 4) return;
     else if constexpr (NT & 2) {
         const v4u v = {x.x, x.y, x.z, x.w};
         __builtin_nontemporal_store(v, reinterpret_cast<v4u *>(p));
     } else *p = x;
 }
-
-// blocks of chunk t (of nb Poly1305 blocks), 0..4
-__device__ __forceinline__ uint32_t chunk_blocks(uint32_t nb, uint32_t t) {
-    const uint32_t b0 = 4 * t;
-    return nb > b0 ? (nb - b0 < 4 ? nb - b0 : 4) : 0;
-}
+template <int MODE> constexpr int mode_nt() { return MODE == 7 ? 4 : (MODE >= 4 && MODE <= 6) ? MODE - 3 : 0; }
 
 // Branch-free chunk load: piece indices are clamped to the packet's last
 // 16-byte block (block 0 of an empty payload is the tag slot, also inside the
@@ -72,10 +70,6 @@ __device__ __forceinline__ void load_chunk(Chunk &c, const uint4 *pl, uint32_t t
     c.q1 = ld16<NT>(pl + min(b + 1, last));
     c.q2 = ld16<NT>(pl + min(b + 2, last));
     c.q3 = ld16<NT>(pl + min(b + 3, last));
-}
-
-__device__ __forceinline__ uint4 sel4(bool c, const uint4 &a, const uint4 &b) {
-    return make_uint4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
 }
 
 __device__ __forceinline__ void absorb_chunk(Acc &h, const Chunk &c, const Mul &r, uint32_t cnt) {
@@ -102,54 +96,23 @@ __device__ __forceinline__ void absorb_chunk(Acc &h, const Chunk &c, const Mul &
 // g = {0, 1, 10, 11, 4, 5, 14, 15}: conflict-free for the frame-major
 // ds_write_b128 (8-lane groups, 128-byte rows) and the line-major
 // ds_read_b128 (16-lane groups, 256-byte rows).
-#ifndef RG_PIPE_LINES
-#define RG_PIPE_LINES 1
-#endif
-// open absorbs each chunk's ciphertext in its own step (loaded three steps ahead), so no loaded
-// chunk is copied into a second register set (a copy of a load in flight makes the wave wait for it)
-#ifndef RG_PIPE_OPEN_CUR
-#define RG_PIPE_OPEN_CUR 1
-#endif
-constexpr bool PIPE_OPEN_CUR = RG_PIPE_OPEN_CUR != 0;
-#ifndef RG_PIPE_LOAD_FIRST
-#define RG_PIPE_LOAD_FIRST 0
-#endif
-constexpr bool PIPE_LOAD_FIRST = RG_PIPE_LOAD_FIRST != 0;
-// quad block stores instead of the LDS ring (below): 247 GPU tests green, measured equal or 1-2 % slower
-// on config 2 (profiles/r3_cfg2_quad_ab.txt): the DPP transpose costs what the ring does
-#ifndef RG_PIPE_QUAD
-#define RG_PIPE_QUAD 0
-#endif
-constexpr bool PIPE_QUAD = RG_PIPE_QUAD != 0;
-// experiment: the four line stores of a step issued one per two double rounds of its keystream block
-// (compiler-visible buffer stores, so hipcc counts them in its vmcnt waits)
-#ifndef RG_PIPE_SPREAD
-#define RG_PIPE_SPREAD 0
-#endif
-constexpr bool PIPE_SPREAD = RG_PIPE_SPREAD != 0;
-// diagnostics only (tools/build_variant.sh): 1 = line stores dropped, 2 = LDS ring dropped
-#ifndef RG_PIPE_ABL
-#define RG_PIPE_ABL 0
-#endif
+// Alternatives measured in round 3 and dropped: a DPP quad
+// transpose with 64-byte half-line stores, line stores spread over the rounds,
+// an LDS-DMA staged chunk stream, lane-per-frame stores without a transpose.
 constexpr uint32_t kPipeLinesFlag = 4u;      // launch flag bit (bits 0-1: log2 lanes per packet)
 constexpr uint32_t kRingBytes = 64u * 256u; // per wave
 // (plain vector types: HIP's uint4 has no assignment in a qualified address space)
 typedef __attribute__((address_space(3))) v4u lds_u4;
-typedef __attribute__((address_space(1))) v4u glb_u4;
 __device__ __forceinline__ v4u to_v4(const uint4 &a) { return v4u{a.x, a.y, a.z, a.w}; }
 __device__ __forceinline__ uint32_t ring_g(uint32_t p) { return (p & 1u) ^ (((p >> 1) & 1u) * 10u) ^ (((p >> 2) & 1u) * 4u); }
 
 // Frame stores of a line-store wave go through a buffer resource based at the wave's lowest frame:
-// 32-bit offsets (16 VGPRs fewer than the 64-bit line pointers: 282 -> 268 for the seal, 305 -> 264
-// for the open), compiler-visible, so hipcc's vmcnt waits stay exact, and the cache policy in one
-// place (write-through with RG_STORE_SC1, measured no faster: rg_device.h).
-constexpr int kFrameAux = RG_STORE_SC1 ? 16 : 0; // buffer-instruction cache bits: 16 = sc1
-
+// 32-bit offsets (16 VGPRs fewer than 64-bit line pointers), compiler-visible, so hipcc's vmcnt
+// waits stay exact.
 struct Ring {
     lds_u4 *wr;          // this lane's frame record
     lds_u4 *rd;          // line-major reads: frame lane / 8 (+ 8 q + 32 h), slot base
     uint32_t fo[2][4];   // byte offset of frame 32 h + 8 q + lane / 8, + 16 (lane % 8), in the wave's window
-    uint32_t qo[4];      // quad stores: byte offset of frame (lane & ~3) + q, + 16 (lane % 4)
     uint32_t self;       // byte offset of this lane's frame in the window
     uint64_t base;       // the window's base address (wave-uniform)
     __amdgpu_buffer_rsrc_t rs; // the window: the wave's frames
@@ -188,68 +151,8 @@ __device__ __forceinline__ Ring make_ring(uint8_t *frame, uint64_t base) {
     for (int h = 0; h < 2; ++h)
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-            R.fo[h][q] = PIPE_QUAD ? 0u : (uint32_t)__shfl((int)R.self, 32 * h + 8 * q + (int)(lane >> 3)) + 16 * (lane & 7u);
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-        R.qo[q] = PIPE_QUAD ? (uint32_t)__shfl((int)R.self, (int)(lane & ~3u) + q) + 16 * (lane & 3u) : 0u;
+            R.fo[h][q] = (uint32_t)__shfl((int)R.self, 32 * h + 8 * q + (int)(lane >> 3)) + 16 * (lane & 7u);
     return R;
-}
-
-// ------------------------------------------------------ quad block stores
-// (RG_PIPE_QUAD, an option: no LDS ring.)  Each step makes one frame-aligned 64-byte
-// block per lane (pieces 4t .. 4t+3 of its frame).  A 4 x 4 transpose of the 16-byte pieces inside each
-// lane quad (two DPP quad_perm butterfly stages, v_cndmask with a DPP source) leaves lane j of a quad
-// with piece j of the quad's frames 0..3, so each of the step's four stores writes 16 whole 64-byte
-// half-lines (four lanes each) instead of one 16-byte piece into each of 64 frames.  The ring's four
-// ds_write_b128 + four ds_read_b128 per step cost ~12 k cycles per config-2 wave
-// (profiles/r3_cfg2_attribution.txt); the transpose is VALU only, 32 DPP moves + 32 selects per step,
-// and measured as costly (148.9 k against 148.1 k cycles per wave, profiles/r3_cfg2_quad_ab.txt).
-template <int CTRL> __device__ __forceinline__ uint32_t qperm(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
-}
-__device__ __forceinline__ void quad_t4(uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d) {
-    const uint32_t lane = threadIdx.x & 3u;
-    const bool odd = lane & 1u, hi = lane & 2u;
-    // (the DPP moves are convergent: computed unconditionally, or hipcc branches around them)
-    // stage 1, partner lane ^ 1 (quad_perm [1,0,3,2]): pieces p with (p ^ lane) & 1 come from it, as piece p ^ 1
-    const uint32_t xa = qperm<0xB1>(a), xb = qperm<0xB1>(b), xc = qperm<0xB1>(c), xd = qperm<0xB1>(d);
-    const uint32_t n0 = odd ? xb : a, n1 = odd ? b : xa, n2 = odd ? xd : c, n3 = odd ? d : xc;
-    // stage 2, partner lane ^ 2 (quad_perm [2,3,0,1])
-    const uint32_t y0 = qperm<0x4E>(n0), y1 = qperm<0x4E>(n1), y2 = qperm<0x4E>(n2), y3 = qperm<0x4E>(n3);
-    a = hi ? y2 : n0;
-    b = hi ? y3 : n1;
-    c = hi ? n2 : y0;
-    d = hi ? n3 : y1;
-}
-// block b of this lane's frame = pieces p0 .. p3; pieces from `valid` on are not the frame's (dropped)
-__device__ __forceinline__ void quad_block_store(const Ring &R, uint32_t b, uint4 p0, uint4 p1, uint4 p2, uint4 p3,
-                                                 uint32_t valid = 4) {
-    quad_t4(p0.x, p1.x, p2.x, p3.x);
-    quad_t4(p0.y, p1.y, p2.y, p3.y);
-    quad_t4(p0.z, p1.z, p2.z, p3.z);
-    quad_t4(p0.w, p1.w, p2.w, p3.w);
-    const bool ok = (threadIdx.x & 3u) < valid;
-    __builtin_amdgcn_raw_buffer_store_b128(to_v4(p0), R.rs, (int)(ok ? R.qo[0] + 64 * b : 0x80000000u), 0, kFrameAux);
-    __builtin_amdgcn_raw_buffer_store_b128(to_v4(p1), R.rs, (int)(ok ? R.qo[1] + 64 * b : 0x80000000u), 0, kFrameAux);
-    __builtin_amdgcn_raw_buffer_store_b128(to_v4(p2), R.rs, (int)(ok ? R.qo[2] + 64 * b : 0x80000000u), 0, kFrameAux);
-    __builtin_amdgcn_raw_buffer_store_b128(to_v4(p3), R.rs, (int)(ok ? R.qo[3] + 64 * b : 0x80000000u), 0, kFrameAux);
-}
-
-// the frame's last pieces, stored by the caller once the tag is known (quad block stores)
-struct QTail {
-    uint4 p0, p1, p2, p3;
-    uint32_t n; // pieces held, 1 .. 4
-};
-// pieces + the tag: block b (and b + 1 when they make five)
-__device__ __forceinline__ void quad_tail_store(const Ring &R, uint32_t b, const QTail &tl, const uint4 &tag) {
-    const uint4 z = make_uint4(0, 0, 0, 0);
-    if (tl.n == 4) { // wave-uniform
-        quad_block_store(R, b, tl.p0, tl.p1, tl.p2, tl.p3, 4);
-        quad_block_store(R, b + 1, tag, z, z, z, 1);
-    } else {
-        quad_block_store(R, b, tl.p0, tl.n > 1 ? tl.p1 : tag, tl.n > 2 ? tl.p2 : tl.n == 2 ? tag : z,
-                         tl.n == 3 ? tag : z, tl.n + 1);
-    }
 }
 
 // the same window with its descriptor rebuilt from readfirstlane values: a descriptor that reaches its
@@ -263,7 +166,7 @@ __device__ __forceinline__ Ring pin_window(const Ring &R) {
 
 // a 16-byte piece of this lane's frame at byte `off` of the frame (line-store waves)
 __device__ __forceinline__ void frame_store(const Ring &R, uint32_t off, const uint4 &x) {
-    __builtin_amdgcn_raw_buffer_store_b128(to_v4(x), R.rs, (int)(R.self + off), 0, kFrameAux);
+    __builtin_amdgcn_raw_buffer_store_b128(to_v4(x), R.rs, (int)(R.self + off), 0, 0);
 }
 
 // block t (4 pieces) of this lane's frame into set t & 3
@@ -299,84 +202,47 @@ __device__ __forceinline__ void ring_store(const Ring &R, const Ring4 &x, uint32
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-        __builtin_amdgcn_raw_buffer_store_b128(x.v[q], R.rs, (int)((h ? R.fo[1][q] : R.fo[0][q]) + 128 * k), 0, kFrameAux);
+        __builtin_amdgcn_raw_buffer_store_b128(x.v[q], R.rs, (int)((h ? R.fo[1][q] : R.fo[0][q]) + 128 * k), 0, 0);
 }
-
-// Diagnostic build only (RG_PIPE_WSTAMP, tools/wstamps.py): per wave, cycles of the line-store steps
-// by their place in the unrolled loop (t % 3), to price the waits hipcc puts in each, and (seal) the
-// cycles in an explicit vmcnt(16) before the XOR (exact for chunk t in steady state).  Each stamp
-// costs ~40 cycles and forbids overlap across it: read the shares, not the run time.
-#ifdef RG_PIPE_WSTAMP
-__device__ __forceinline__ uint64_t wst_now() {
-    uint64_t t;
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-    __builtin_amdgcn_sched_barrier(0);
-    return t;
-}
-#define RG_WST(x) x
-// this wave's accumulators: slots 1-3 of its stamp record (pipe_stamp leaves them alone)
-__device__ __forceinline__ uint64_t *wst_slot(uint64_t *dbg) {
-    return dbg ? dbg + 8ull * (blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64) + 1 : nullptr;
-}
-#else
-#define RG_WST(x)
-#endif
 
 // One step: keystream block t+1 -- with the previous chunk's four Poly1305
-// blocks (pi, always a full chunk) absorbed in its rounds when ABSORB -- XORed
-// into chunk t (buf) and stored; then chunk t+kDepth is requested into buf.  Full
-// steps store unconditionally: a store under a branch leaves the waitcnt pass
-// a path with fewer memory operations, and since vmcnt counts stores as well
-// as loads it would then also wait for the last step's stores to be acked.
+// blocks (pi, always a full chunk; open: this chunk's ciphertext) absorbed in
+// its rounds when ABSORB -- XORed into chunk t (buf) and stored; then chunk
+// t+3 is requested into buf.  Full steps store unconditionally: a store under
+// a branch leaves the waitcnt pass a path with fewer memory operations, and
+// since vmcnt counts stores as well as loads it would then also wait for the
+// last step's stores to be acked.
 // TAIL: the partial last chunk (cnt < 4 blocks), predicated, no prefetch.
 // Stores are shifted by one block so that each step writes one 64-byte
 // frame-aligned block (the payload starts 16 bytes into the frame): the
 // previous chunk's last block (prev; or the header, before the first chunk of
 // a sealed frame) and this chunk's first three.  Lines written piecewise across
 // steps were measured at 1.66x the algorithmic write bytes (profiles/).
-// MODE (seal diagnostics, rg_set_debug_mode): 0 normal; 1 compute only (no
-// payload loads or stores, loop-carried fake data); 2 memory only (no
-// keystream and no Poly1305); 4/5/6 non-temporal loads / stores / both; 7 no payload stores;
-// 8 line stores alternate between lines 0 and 1 of each frame (cache-resident: the store instructions
-// without their HBM writes).
 // LINES: the frame blocks go through the wave's LDS ring (block t goes into
 // the ring; with FLUSH, half t & 1 of line (t - 2) / 2 is read back before the
 // rounds and stored after them).
-// POLY = false (open with the tag verified first, RG_PIPE_MAC_FIRST): no Poly1305 in the rounds, and a
-// lane whose packet failed its tag (keep) writes its ciphertext back unchanged instead of the plaintext.
-template <bool OPEN, bool ABSORB, bool TAIL, int MODE = 0, bool LINES = false, bool FLUSH = false, bool POLY = true>
+// MODE (seal diagnostics, RG_DIAG builds only): 0 normal; 1 compute only (no
+// payload loads or stores, loop-carried fake data); 2 memory only (no
+// keystream and no Poly1305); 4/5/6 non-temporal loads / stores / both; 7 no
+// payload stores; 8 line stores alternate between lines 0 and 1 of each frame
+// (cache-resident: the store instructions without their HBM writes).
+template <bool OPEN, bool ABSORB, bool TAIL, int MODE = 0, bool LINES = false, bool FLUSH = false>
 __device__ __forceinline__ void pipe_step(uint4 *pl, const Stream &st, const Mul &r, Acc &h, Chunk &pi, Chunk &buf,
                                           uint4 &prev, bool &have_prev, uint32_t t, uint32_t nb, uint32_t c0,
-                                          const Ring &R, bool keep = false, uint64_t *wacc = nullptr,
-                                          QTail *tl = nullptr) {
+                                          const Ring &R) {
     uint32_t ks[16];
     static_assert(!FLUSH || (LINES && ABSORB && !TAIL), "flush steps");
     Ring4 fl;
-    RG_WST(uint64_t w_t0 = 0; if constexpr (FLUSH) w_t0 = wst_now();)
     if constexpr (FLUSH) {
         wave_sync(); // block t - 1 was put by every lane
-#if RG_PIPE_ABL == 2 // diagnostics only: no ring (the line stores write this lane's registers; output invalid)
-        fl.v[0] = to_v4(buf.q0); fl.v[1] = to_v4(buf.q1); fl.v[2] = to_v4(buf.q2); fl.v[3] = to_v4(buf.q3);
-#else
         fl = ring_get(R, (t - 2) >> 1, t & 1u);
-#endif
     }
     if constexpr (MODE == 2) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) ks[i] = t * 16 + i;
         h.h0 ^= pi.q0.x ^ pi.q1.y ^ pi.q2.z ^ pi.q3.w;
     } else stream_block_hooked(st, c0 + t + 1, ks, [&](int dr) {
-        if constexpr (FLUSH && PIPE_SPREAD && RG_PIPE_ABL != 1) { // the line stores, one per two double rounds
-            if (dr == 2 || dr == 4 || dr == 6 || dr == 8) {
-                const int q = dr / 2 - 1;
-                const uint32_t kk = MODE == 8 ? ((t - 2) >> 1) & 1u : (t - 2) >> 1;
-                __builtin_amdgcn_raw_buffer_store_b128(fl.v[q], R.rs, (int)(((t & 1u) ? R.fo[1][q] : R.fo[0][q]) + 128 * kk), 0,
-                                                       kFrameAux);
-            }
-        }
-        if constexpr (OPEN && !POLY) {
-        } else if constexpr (OPEN && PIPE_OPEN_CUR) { // this chunk's ciphertext (TAIL: its nb % 4 blocks)
+        if constexpr (OPEN) { // this chunk's ciphertext (TAIL: its nb % 4 blocks)
             const uint32_t bl = TAIL ? nb & 3u : 4u;
             if (dr == 1) acc_block_pred(h, buf.q0, r, bl > 0);
             if (dr == 3) acc_block_pred(h, buf.q1, r, bl > 1);
@@ -391,51 +257,22 @@ __device__ __forceinline__ void pipe_step(uint4 *pl, const Stream &st, const Mul
             if (dr % 2 == 1) pin_acc(h);
         }
     });
-    RG_WST(if constexpr (FLUSH && !OPEN) { const uint64_t a_ = wst_now(); asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); wacc[3 + t % 3] += wst_now() - a_; })
     Chunk x = {xor4(buf.q0, ks + 0), xor4(buf.q1, ks + 4), xor4(buf.q2, ks + 8), xor4(buf.q3, ks + 12)};
-    if constexpr (OPEN && !POLY) { // component-wise: a ternary on uint4 objects selects a pointer (scratch)
-        x.q0 = sel4(keep, buf.q0, x.q0); x.q1 = sel4(keep, buf.q1, x.q1);
-        x.q2 = sel4(keep, buf.q2, x.q2); x.q3 = sel4(keep, buf.q3, x.q3);
-    }
     uint4 *dst = pl + 4 * t;
     if constexpr (MODE == 1) {
         pi = x;
         buf.q0.x += t; buf.q1.y ^= t; buf.q2.z += h.h0; buf.q3.w ^= t; // fake next chunk, loop-carried
         return;
     }
-    constexpr int NT = MODE == 7 ? 4 : MODE >= 4 ? MODE - 3 : 0;
-    if constexpr (PIPE_LOAD_FIRST && !TAIL) {
-        // chunk t + kDepth is requested before this step's stores: vmcnt retires in issue order, so a
-        // load issued behind a store is not usable before that store is acknowledged
-        if constexpr (!(OPEN && PIPE_OPEN_CUR)) pi = OPEN ? buf : x;
-        load_chunk<NT>(buf, pl, t + kDepth, nb - 1);
-    }
-    if constexpr (LINES && !TAIL && PIPE_QUAD) {
-        quad_block_store(R, t, prev, x.q0, x.q1, x.q2); // prev: the header before the first chunk
-        prev = x.q3;
-        have_prev = true;
-    } else if constexpr (LINES && !TAIL) {
-#if RG_PIPE_ABL == 2
-        asm volatile("" ::"v"(prev.x), "v"(x.q0.x), "v"(x.q1.x), "v"(x.q2.x));
-#else
+    constexpr int NT = mode_nt<MODE>();
+    if constexpr (LINES && !TAIL) {
         ring_put(R, t, prev, x.q0, x.q1, x.q2); // prev: the header before the first chunk
-#endif
-#if RG_PIPE_ABL == 1 // diagnostics only: the ring is read back but its lines are not stored (output invalid)
-        if constexpr (FLUSH) asm volatile("" ::"v"(fl.v[0]), "v"(fl.v[1]), "v"(fl.v[2]), "v"(fl.v[3]));
-#else
-        if constexpr (FLUSH && !PIPE_SPREAD) ring_store(R, fl, MODE == 8 ? ((t - 2) >> 1) & 1u : (t - 2) >> 1, t & 1u);
-#endif
+        if constexpr (FLUSH) ring_store(R, fl, MODE == 8 ? ((t - 2) >> 1) & 1u : (t - 2) >> 1, t & 1u);
         prev = x.q3;
         have_prev = true;
     } else if constexpr (TAIL) {
         const uint32_t cnt = nb & 3u;
-        if constexpr (LINES && PIPE_QUAD) { // block t = prev + the cnt pieces: stored with the tag by the caller
-            tl->p0 = prev;
-            tl->p1 = x.q0;
-            tl->p2 = x.q1;
-            tl->p3 = x.q2;
-            tl->n = 1 + cnt;
-        } else if constexpr (LINES) { // one lane per packet: pl = frame + 16, dst = frame byte 16 + 64 t
+        if constexpr (LINES) { // one lane per packet: pl = frame + 16, dst = frame byte 16 + 64 t
             const uint32_t o = 16 + 64 * t;
             if (have_prev) frame_store(R, o - 16, prev);
             frame_store(R, o, x.q0); // cnt >= 1
@@ -457,130 +294,76 @@ __device__ __forceinline__ void pipe_step(uint4 *pl, const Stream &st, const Mul
         prev = x.q3;
         have_prev = true;
     }
-    if constexpr (PIPE_LOAD_FIRST && !TAIL) return;
-    if constexpr (!(OPEN && PIPE_OPEN_CUR)) pi = OPEN ? buf : x;
-#if RG_PIPE_PAD
-    if constexpr (LINES && !FLUSH && !TAIL) {
-        // the two steps before the loop store no line: four loads stand in for the four line stores,
-        // so that the waitcnt pass sees as many operations behind each chunk's loads on the path into
-        // the loop as on its back edge (else it keeps the entry path's shorter counts for every pass)
-        const volatile uint32_t *hp = reinterpret_cast<const volatile uint32_t *>(pl) - 4;
-        uint32_t sink = 0;
-        for (int k = 0; k < 4; ++k) sink += hp[k];
-        asm volatile("" ::"v"(sink));
-    }
-#endif
-    if constexpr (!TAIL) load_chunk<NT>(buf, pl, t + kDepth, nb - 1);
-    RG_WST(if constexpr (FLUSH) wacc[t % 3] += wst_now() - w_t0;)
+    if constexpr (!OPEN) pi = x;
+    if constexpr (!TAIL) load_chunk<NT & 1>(buf, pl, t + kDepth, nb - 1);
 }
 
 // Keystream XOR in place + Poly1305 over the ciphertext of nb 16-byte blocks
 // starting at chunk c0 of the payload (pl points there; keystream blocks from
-// c0 + 1); b0 / b1 (/ b2) hold its chunks 0 / 1 (/ 2) (loads already issued).
+// c0 + 1); b0 / b1 / b2 hold its chunks 0 / 1 / 2 (loads already issued).
 // The first step is peeled (nothing to absorb yet), so that every absorb
-// inside the loop is unconditional; chunk c always lives in buffer c % kDepth.
+// inside the loop is unconditional; chunk c always lives in buffer c % 3.
 // head / has_head: the DataHeader a seal writes in front of the payload (only
 // the lane whose segment starts the payload has one).
 // LINES (a wave of valid packets of one size, has_head set): blocks through the LDS ring.
-template <bool OPEN, int MODE = 0, bool LINES = false, bool POLY = true>
+template <bool OPEN, int MODE = 0, bool LINES = false>
 __device__ __forceinline__ Acc pipe_pass(uint4 *pl, const Stream &st, const Mul &r, uint32_t nb, uint32_t c0,
-                                         Chunk &b0, Chunk &b1, Chunk &b2, Chunk &b3, uint4 head, bool has_head,
-                                         const Ring &R0, bool keep = false, uint64_t *wst = nullptr,
-                                         QTail *tl = nullptr) {
+                                         Chunk &b0, Chunk &b1, Chunk &b2, uint4 head, bool has_head, const Ring &R0) {
     const Ring R = LINES ? pin_window(R0) : R0;
     const uint32_t F = nb >> 2, bl = nb & 3u; // full chunks, blocks in the partial last chunk
-    uint64_t wacc[6] = {0, 0, 0, 0, 0, 0};
-    (void)wst;
     Acc h = {0, 0, 0, 0, 0};
     Chunk pi = {};
     uint4 prev = head; // block still to be stored just in front of the current chunk
     bool have_prev = has_head;
     uint32_t pending = 0; // blocks of pi not yet absorbed
-    if constexpr (LINES && !PIPE_QUAD) wave_sync(); // the previous packet's last read-back is done
+    if constexpr (LINES) wave_sync(); // the previous packet's last read-back is done
     if (F > 0) {
-        pipe_step<OPEN, false, false, MODE, LINES, false, POLY>(pl, st, r, h, pi, b0, prev, have_prev, 0, nb, c0, R, keep, wacc);
+        pipe_step<OPEN, false, false, MODE, LINES>(pl, st, r, h, pi, b0, prev, have_prev, 0, nb, c0, R);
         uint32_t t = 1;
-        // whole rounds of kDepth steps only: a step that may be skipped would
+        // whole rounds of three steps only: a step that may be skipped would
         // leave the waitcnt pass a path without its memory operations
         // (vmcnt(0) at the next one); the remainder steps run after the loop
-        if constexpr (LINES && !PIPE_QUAD) {
-            static_assert(kDepth >= 3, "line stores: three or four chunk buffers");
+        if constexpr (LINES) {
             // step 1 has no complete line yet; steps 2.. each store half a line
-            if (F > 1) pipe_step<OPEN, true, false, MODE, true, false, POLY>(pl, st, r, h, pi, b1, prev, have_prev, 1, nb, c0, R, keep, wacc);
-            if constexpr (kDepth == 4) {
-                for (t = 2; t + 3 < F; t += 4) {
-                    pipe_step<OPEN, true, false, MODE, true, true, POLY>(pl, st, r, h, pi, b2, prev, have_prev, t, nb, c0, R, keep, wacc);
-                    pipe_step<OPEN, true, false, MODE, true, true, POLY>(pl, st, r, h, pi, b3, prev, have_prev, t + 1, nb, c0, R, keep, wacc);
-                    pipe_step<OPEN, true, false, MODE, true, true, POLY>(pl, st, r, h, pi, b0, prev, have_prev, t + 2, nb, c0, R, keep, wacc);
-                    pipe_step<OPEN, true, false, MODE, true, true, POLY>(pl, st, r, h, pi, b1, prev, have_prev, t + 3, nb, c0, R, keep, wacc);
-                }
-                if (t < F) pipe_step<OPEN, true, false, MODE, true, true, POLY>(pl, st, r, h, pi, b2, prev, have_prev, t, nb, c0, R, keep, wacc);
-                if (t + 1 < F) pipe_step<OPEN, true, false, MODE, true, true, POLY>(pl, st, r, h, pi, b3, prev, have_prev, t + 1, nb, c0, R, keep, wacc);
-                if (t + 2 < F) pipe_step<OPEN, true, false, MODE, true, true, POLY>(pl, st, r, h, pi, b0, prev, have_prev, t + 2, nb, c0, R, keep, wacc);
-            } else {
+            if (F > 1) pipe_step<OPEN, true, false, MODE, true>(pl, st, r, h, pi, b1, prev, have_prev, 1, nb, c0, R);
             for (t = 2; t + 2 < F; t += 3) {
-                pipe_step<OPEN, true, false, MODE, true, true, POLY>(pl, st, r, h, pi, b2, prev, have_prev, t, nb, c0, R, keep, wacc);
-                pipe_step<OPEN, true, false, MODE, true, true, POLY>(pl, st, r, h, pi, b0, prev, have_prev, t + 1, nb, c0, R, keep, wacc);
-                pipe_step<OPEN, true, false, MODE, true, true, POLY>(pl, st, r, h, pi, b1, prev, have_prev, t + 2, nb, c0, R, keep, wacc);
+                pipe_step<OPEN, true, false, MODE, true, true>(pl, st, r, h, pi, b2, prev, have_prev, t, nb, c0, R);
+                pipe_step<OPEN, true, false, MODE, true, true>(pl, st, r, h, pi, b0, prev, have_prev, t + 1, nb, c0, R);
+                pipe_step<OPEN, true, false, MODE, true, true>(pl, st, r, h, pi, b1, prev, have_prev, t + 2, nb, c0, R);
             }
-            if (t < F) pipe_step<OPEN, true, false, MODE, true, true, POLY>(pl, st, r, h, pi, b2, prev, have_prev, t, nb, c0, R, keep, wacc);
-            if (t + 1 < F) pipe_step<OPEN, true, false, MODE, true, true, POLY>(pl, st, r, h, pi, b0, prev, have_prev, t + 1, nb, c0, R, keep, wacc);
-            }
+            if (t < F) pipe_step<OPEN, true, false, MODE, true, true>(pl, st, r, h, pi, b2, prev, have_prev, t, nb, c0, R);
+            if (t + 1 < F)
+                pipe_step<OPEN, true, false, MODE, true, true>(pl, st, r, h, pi, b0, prev, have_prev, t + 1, nb, c0, R);
             // the halves not stored yet: m = F - 2 .. 2 ceil(F / 2) - 1 (k = m / 2, h = m % 2); a
             // last line of one block stores its first four pieces only
             wave_sync();
             for (uint32_t m = F >= 2 ? F - 2 : 0; m < 2 * ((F + 1) >> 1); ++m)
                 ring_store<true>(R, ring_get(R, m >> 1, m & 1u), MODE == 8 ? (m >> 1) & 1u : m >> 1, m & 1u, F);
-        } else if constexpr (kDepth == 4) {
-            for (; t + 3 < F; t += 4) {
-                pipe_step<OPEN, true, false, MODE, LINES, false, POLY>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R, keep, wacc);
-                pipe_step<OPEN, true, false, MODE, LINES, false, POLY>(pl, st, r, h, pi, b2, prev, have_prev, t + 1, nb, c0, R, keep, wacc);
-                pipe_step<OPEN, true, false, MODE, LINES, false, POLY>(pl, st, r, h, pi, b3, prev, have_prev, t + 2, nb, c0, R, keep, wacc);
-                pipe_step<OPEN, true, false, MODE, LINES, false, POLY>(pl, st, r, h, pi, b0, prev, have_prev, t + 3, nb, c0, R, keep, wacc);
-            }
-            if (t < F) pipe_step<OPEN, true, false, MODE, LINES, false, POLY>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R, keep, wacc);
-            if (t + 1 < F) pipe_step<OPEN, true, false, MODE, LINES, false, POLY>(pl, st, r, h, pi, b2, prev, have_prev, t + 1, nb, c0, R, keep, wacc);
-            if (t + 2 < F) pipe_step<OPEN, true, false, MODE, LINES, false, POLY>(pl, st, r, h, pi, b3, prev, have_prev, t + 2, nb, c0, R, keep, wacc);
-        } else if constexpr (kDepth == 3) {
-            for (; t + 2 < F; t += 3) {
-                pipe_step<OPEN, true, false, MODE, LINES, false, POLY>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R, keep, wacc);
-                pipe_step<OPEN, true, false, MODE, LINES, false, POLY>(pl, st, r, h, pi, b2, prev, have_prev, t + 1, nb, c0, R, keep, wacc);
-                pipe_step<OPEN, true, false, MODE, LINES, false, POLY>(pl, st, r, h, pi, b0, prev, have_prev, t + 2, nb, c0, R, keep, wacc);
-            }
-            if (t < F) pipe_step<OPEN, true, false, MODE, LINES, false, POLY>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R, keep, wacc);
-            if (t + 1 < F) pipe_step<OPEN, true, false, MODE, LINES, false, POLY>(pl, st, r, h, pi, b2, prev, have_prev, t + 1, nb, c0, R, keep, wacc);
         } else {
-            for (; t + 1 < F; t += 2) {
-                pipe_step<OPEN, true, false, MODE, LINES, false, POLY>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R, keep, wacc);
-                pipe_step<OPEN, true, false, MODE, LINES, false, POLY>(pl, st, r, h, pi, b0, prev, have_prev, t + 1, nb, c0, R, keep, wacc);
+            for (; t + 2 < F; t += 3) {
+                pipe_step<OPEN, true, false, MODE, false>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R);
+                pipe_step<OPEN, true, false, MODE, false>(pl, st, r, h, pi, b2, prev, have_prev, t + 1, nb, c0, R);
+                pipe_step<OPEN, true, false, MODE, false>(pl, st, r, h, pi, b0, prev, have_prev, t + 2, nb, c0, R);
             }
-            if (t < F) pipe_step<OPEN, true, false, MODE, LINES, false, POLY>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R, keep, wacc);
+            if (t < F) pipe_step<OPEN, true, false, MODE, false>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R);
+            if (t + 1 < F) pipe_step<OPEN, true, false, MODE, false>(pl, st, r, h, pi, b2, prev, have_prev, t + 1, nb, c0, R);
         }
         pending = 4;
     }
     if (bl > 0) {
-        // chunk F lives in b(F % kDepth); select by value (a reference select
+        // chunk F lives in b(F % 3); select by value (a reference select
         // between the buffers would move them to scratch memory)
         const uint32_t k = F % kDepth;
-        Chunk bp = {k == 1 ? b1.q0 : k == 2 ? b2.q0 : k == 3 ? b3.q0 : b0.q0,
-                    k == 1 ? b1.q1 : k == 2 ? b2.q1 : k == 3 ? b3.q1 : b0.q1,
-                    k == 1 ? b1.q2 : k == 2 ? b2.q2 : k == 3 ? b3.q2 : b0.q2,
-                    k == 1 ? b1.q3 : k == 2 ? b2.q3 : k == 3 ? b3.q3 : b0.q3};
-        if (F > 0) pipe_step<OPEN, true, true, MODE, LINES, false, POLY>(pl, st, r, h, pi, bp, prev, have_prev, F, nb, c0, R, keep, wacc, tl);
-        else pipe_step<OPEN, false, true, MODE, LINES, false, POLY>(pl, st, r, h, pi, bp, prev, have_prev, F, nb, c0, R, keep, wacc, tl);
+        Chunk bp = {k == 1 ? b1.q0 : k == 2 ? b2.q0 : b0.q0, k == 1 ? b1.q1 : k == 2 ? b2.q1 : b0.q1,
+                    k == 1 ? b1.q2 : k == 2 ? b2.q2 : b0.q2, k == 1 ? b1.q3 : k == 2 ? b2.q3 : b0.q3};
+        if (F > 0) pipe_step<OPEN, true, true, MODE, LINES>(pl, st, r, h, pi, bp, prev, have_prev, F, nb, c0, R);
+        else pipe_step<OPEN, false, true, MODE, LINES>(pl, st, r, h, pi, bp, prev, have_prev, F, nb, c0, R);
         pending = bl;
     }
-    if constexpr (LINES && PIPE_QUAD) {
-        if (have_prev) { // no partial chunk: block F is prev (+ the tag)
-            tl->p0 = prev;
-            tl->p1 = tl->p2 = tl->p3 = make_uint4(0, 0, 0, 0);
-            tl->n = 1;
-        }
-    } else if constexpr (LINES) {
+    if constexpr (LINES) {
         if (have_prev) frame_store(R, 64 * F, prev); // pl + 4 F - 1
-    } else if (have_prev && MODE != 1) st16<(MODE == 7 ? 4 : MODE >= 4 ? MODE - 3 : 0)>(pl + 4 * F - 1, prev);
-    if constexpr (!(OPEN && (PIPE_OPEN_CUR || !POLY))) absorb_chunk(h, pi, r, pending); // the last chunk's blocks
-    RG_WST(if (wst && (threadIdx.x & 63) == 0) for (int k = 0; k < 6; ++k) atomicAdd((unsigned long long *)&wst[k < 3 ? k : 8ull * gridDim.x * (blockDim.x / 64) + k - 4], (unsigned long long)wacc[k]);)
+    } else if (have_prev && MODE != 1) st16<mode_nt<MODE>()>(pl + 4 * F - 1, prev);
+    if constexpr (!OPEN) absorb_chunk(h, pi, r, pending); // the last chunk's blocks
     return h;
 }
 
@@ -600,7 +383,8 @@ __device__ __forceinline__ void pipe_tag(Acc h, const Mul &r, uint32_t P, const 
 // squarings are general multiplies, the "times r" steps the cheap clamped
 // one) and the group sums by butterfly; every lane of the group then holds
 // the packet's accumulator.  Each lane also computes the one-time-key block
-// itself (no cross-lane dependency before the combine).
+// itself (no cross-lane dependency before the combine).  Segments serve
+// batches too small to give every SIMD a wave at one lane per packet.
 struct Seg {
     uint32_t c0, nb, after; // first chunk, blocks in the segment, blocks after it
 };
@@ -649,22 +433,6 @@ __device__ __forceinline__ Acc combine_segments(Acc h, const Mul &r, uint32_t af
     return h;
 }
 
-#ifdef RG_TILE_MARKS
-// experiment builds only (tools/build_variant.sh): real-time marks inside a
-// seal unit, the data dependence pins each mark after the value it follows
-#define RG_MARK(slot, dep)                                                                  \
-    do {                                                                                    \
-        asm volatile("" ::"v"(dep));                                                        \
-        const uint64_t now_ = __builtin_amdgcn_s_memrealtime();                             \
-        if (a.dbg && (threadIdx.x & 63) == 0)                                               \
-            a.dbg[8ull * (blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64) + (slot)] = now_; \
-    } while (0)
-#else
-#define RG_MARK(slot, dep) \
-    do {                   \
-    } while (0)
-#endif
-
 // ------------------------------------------------------------------ seal
 // Frame: [hdr 16][payload P][tag 16]; desc.len = P.  Checks as seal_packet
 // (rg_kernels.hip): descriptor and force_encrypt's padding assert
@@ -687,23 +455,20 @@ __device__ __forceinline__ void pipe_seal_packet(const SealArgs &a, uint32_t i, 
         return;
     }
     uint8_t *frame = a.buf + d.offset;
-    RG_MARK(1, P);
     const uint32_t nb = P >> 4;
     const Seg sg = make_seg(nb, j, G);
     // an empty segment reads (never writes) the payload start, which is in the frame
     uint4 *pl = reinterpret_cast<uint4 *>(frame + 16) + (sg.nb ? 4 * sg.c0 : 0);
-    Chunk b0, b1, b2 = {}, b3 = {};
+    Chunk b0, b1, b2;
     if constexpr (MODE == 1) {
         b0 = {make_uint4(i, 1, 2, 3), make_uint4(4, i, 6, 7), make_uint4(8, 9, i, 11), make_uint4(12, 13, 14, i)};
         b1 = b0;
         b2 = b0;
-        b3 = b0;
     } else {
-        constexpr int NT = MODE >= 4 && MODE != 7 ? MODE - 3 : 0;
+        constexpr int NT = mode_nt<MODE>() & 1;
         load_chunk<NT>(b0, pl, 0, sg.nb ? sg.nb - 1 : 0);
         load_chunk<NT>(b1, pl, 1, sg.nb ? sg.nb - 1 : 0);
-        if constexpr (kDepth >= 3) load_chunk<NT>(b2, pl, 2, sg.nb ? sg.nb - 1 : 0);
-        if constexpr (kDepth >= 4) load_chunk<NT>(b3, pl, 3, sg.nb ? sg.nb - 1 : 0);
+        load_chunk<NT>(b2, pl, 2, sg.nb ? sg.nb - 1 : 0);
     }
     const Key8 key = load_key(a.keys, d.key_idx);
     const uint64_t ctr = a.counters[i];
@@ -712,72 +477,39 @@ __device__ __forceinline__ void pipe_seal_packet(const SealArgs &a, uint32_t i, 
     uint32_t ks[16];
     stream_block(stm, 0, ks); // RFC 8439 §2.6 one-time key
     const Mul r = make_mul(ks[0], ks[1], ks[2], ks[3]);
-    RG_MARK(2, r.rr3);
     // DataHeader {4, receiver, counter} (rustyguard-core/src/lib.rs:286-290), stored by segment 0
     // together with the first payload blocks
     const bool head = a.receivers != nullptr && j == 0;
     uint4 hdr = make_uint4(4u, head ? a.receivers[d.key_idx] : 0u, n1, n2);
     Acc h;
     Ring R{};
-    QTail tl{};
     if (lines) { // wave-uniform
         if (!head) hdr = *reinterpret_cast<const uint4 *>(frame); // block 0 is stored whole: header unchanged
         R = make_ring(frame, wbase);
-#ifdef RG_PIPE_WSTAMP
-        h = pipe_pass<false, MODE, true>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, b3, hdr, true, R, false, wst_slot(a.dbg), &tl);
-#else
-        h = pipe_pass<false, MODE, true>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, b3, hdr, true, R, false, nullptr, &tl);
-#endif
+        h = pipe_pass<false, MODE, true>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, hdr, true, R);
     } else {
-        h = pipe_pass<false, MODE, false>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, b3, hdr, head, Ring{});
+        h = pipe_pass<false, MODE, false>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, hdr, head, Ring{});
     }
-    RG_MARK(3, h.h4);
     h = combine_segments(h, r, sg.after, G);
-    RG_MARK(5, h.h4);
     if (j != 0) return;
     uint32_t tag[4];
     pipe_tag(h, r, P, ks + 4, tag);
     const uint4 tagv = make_uint4(tag[0], tag[1], tag[2], tag[3]);
-    if (lines && PIPE_QUAD) quad_tail_store(pin_window(R), sg.nb >> 2, tl, tagv); // the frame's last block(s)
-    else if (lines) frame_store(pin_window(R), 16 + P, tagv);
+    if (lines) frame_store(pin_window(R), 16 + P, tagv);
     else *reinterpret_cast<uint4 *>(frame + 16 + P) = tagv;
     if (a.status) a.status[i] = RG_PKT_OK;
 }
 
 // ------------------------------------------------------------------ open
-// RG_PIPE_MAC_FIRST 1: verify, then decrypt -- no unauthenticated plaintext ever in memory, a forged
-// packet costs what a clean one does -- but the Poly1305 pass alone runs latency-bound at one wave per
-// SIMD: config 2's open +12 % (profiles/r3_macfirst_ab.txt).  Default 0: decrypt while MACing and
-// restore forged frames (restore_forged).
-#ifndef RG_PIPE_MAC_FIRST
-#define RG_PIPE_MAC_FIRST 0
-#endif
-
-// Pass 1 of the open: the Horner chain over the segment's nb ciphertext blocks, chunk t absorbed while
-// chunks t+1, t+2 are loading (b0 / b1 / b2 hold chunks 0 / 1 / 2 on entry; chunk c lives in b(c % 3);
-// loads clamped inside the segment, unconditional).
-__device__ __forceinline__ Acc poly_pass(const uint4 *pl, const Mul &r, uint32_t nb, Chunk &b0, Chunk &b1, Chunk &b2) {
-    Acc h = {0, 0, 0, 0, 0};
-    const uint32_t C = (nb + 3) >> 2, last = nb ? nb - 1 : 0;
-    uint32_t t = 0;
-    for (; t + 3 <= C; t += 3) {
-        absorb_chunk(h, b0, r, chunk_blocks(nb, t));
-        load_chunk(b0, pl, t + 3, last);
-        absorb_chunk(h, b1, r, chunk_blocks(nb, t + 1));
-        load_chunk(b1, pl, t + 4, last);
-        absorb_chunk(h, b2, r, chunk_blocks(nb, t + 2));
-        load_chunk(b2, pl, t + 5, last);
-    }
-    if (t < C) absorb_chunk(h, b0, r, chunk_blocks(nb, t));
-    if (t + 1 < C) absorb_chunk(h, b1, r, chunk_blocks(nb, t + 1));
-    return h;
-}
-
 // desc.len = W.  Checks mirror rustyguard-core/src/lib.rs:613-629,
 // rustyguard-types/src/lib.rs:181-196 and rustyguard-crypto/src/prim.rs:
 // 427-429.  Decrypts speculatively while MACing the ciphertext; a failed tag
 // (constant-time compare, identical on every lane of the group) makes each
 // lane re-apply its segment's keystream, so the frame is left unchanged.
+// (Verify-then-decrypt -- a Poly1305 pass, then the keystream pass -- makes a
+// forged packet cost what a clean one does, but that Poly1305 pass runs
+// latency-bound at one wave per SIMD: config 2's open +12 % in round 3,
+// profiles/r3_macfirst_ab.txt.  Dropped.)
 __device__ __forceinline__ void pipe_open_packet(const OpenArgs &a, uint32_t i, const rg_pkt_desc &d, uint32_t j,
                                                  uint32_t G, bool lines_ok) {
     const uint32_t W = d.len;
@@ -802,11 +534,10 @@ __device__ __forceinline__ void pipe_open_packet(const OpenArgs &a, uint32_t i, 
     uint4 *safe = const_cast<uint4 *>(reinterpret_cast<const uint4 *>(a.desc + i));
     uint4 *pl = go ? reinterpret_cast<uint4 *>(frame + 16) + (sg.nb ? 4 * sg.c0 : 0) : safe;
     const uint4 hdr = *(desc_ok ? reinterpret_cast<const uint4 *>(frame) : safe);
-    Chunk b0, b1, b2 = {}, b3 = {};
+    Chunk b0, b1, b2;
     load_chunk(b0, pl, 0, sg.nb ? sg.nb - 1 : 0);
     load_chunk(b1, pl, 1, sg.nb ? sg.nb - 1 : 0);
-    if constexpr (kDepth >= 3) load_chunk(b2, pl, 2, sg.nb ? sg.nb - 1 : 0);
-    if constexpr (kDepth >= 4) load_chunk(b3, pl, 3, sg.nb ? sg.nb - 1 : 0);
+    load_chunk(b2, pl, 2, sg.nb ? sg.nb - 1 : 0);
     const uint4 want = *(go ? reinterpret_cast<const uint4 *>(frame + 16 + P) : safe);
     const Key8 key = load_key(a.keys, go ? d.key_idx : 0);
     uint64_t ctr = 0;
@@ -834,47 +565,11 @@ __device__ __forceinline__ void pipe_open_packet(const OpenArgs &a, uint32_t i, 
     uint32_t ks[16];
     stream_block(stm, 0, ks);
     const Mul r = make_mul(ks[0], ks[1], ks[2], ks[3]);
-#if RG_PIPE_MAC_FIRST
-    // verify, then decrypt (the order of an in-place AEAD open, prim.rs:190-201): pass 1 runs Poly1305
-    // over the ciphertext, pass 2 the keystream; a lane whose tag fails writes its ciphertext back
-    // unchanged in pass 2 (the line stores carry whole lines of eight frames), so a forged packet
-    // costs what a clean one does and no unauthenticated plaintext ever reaches memory
-    const Acc h1 = poly_pass(pl, r, sg.nb, b0, b1, b2);
-    // one instance per store mode, each with chunk buffers of its own (the two passes sharing buffers
-    // across the branch left them in scratch memory)
-    auto verify_decrypt = [&](auto lines_tag) -> uint32_t {
-        constexpr bool L = decltype(lines_tag)::value;
-        Chunk p0, p1, p2, p3 = {}; // pass 2's first chunks, in flight during the tag
-        load_chunk(p0, pl, 0, sg.nb ? sg.nb - 1 : 0);
-        load_chunk(p1, pl, 1, sg.nb ? sg.nb - 1 : 0);
-        load_chunk(p2, pl, 2, sg.nb ? sg.nb - 1 : 0);
-        const Acc h = combine_segments(h1, r, sg.after, G);
-        uint32_t tag[4];
-        pipe_tag(h, r, P, ks + 4, tag);
-        const uint32_t df = (tag[0] ^ want.x) | (tag[1] ^ want.y) | (tag[2] ^ want.z) | (tag[3] ^ want.w);
-        if constexpr (L) {
-            const Ring Rm = make_ring(frame, wbase);
-            QTail tl{};
-            (void)pipe_pass<true, 0, true, false>(pl, stm, r, sg.nb, sg.c0, p0, p1, p2, p3, hdr, true, Rm, df != 0, nullptr, &tl);
-            if constexpr (PIPE_QUAD) quad_tail_store(pin_window(Rm), sg.nb >> 2, tl, want);
-        } else (void)pipe_pass<true, 0, false, false>(pl, stm, r, sg.nb, sg.c0, p0, p1, p2, p3, make_uint4(0, 0, 0, 0), false, Ring{}, df != 0);
-        return df;
-    };
-    const uint32_t diff = lines ? verify_decrypt(std::true_type{}) : verify_decrypt(std::false_type{});
-    (void)key;
-#else
     Acc h;
-    QTail tl{};
     Ring Ro{};
     if (lines) Ro = make_ring(frame, wbase);
-#ifdef RG_PIPE_WSTAMP
-    if (lines) h = pipe_pass<true, 0, true>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, b3, hdr, true, Ro, false, wst_slot(a.dbg), &tl);
-#else
-    if (lines) h = pipe_pass<true, 0, true>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, b3, hdr, true, Ro, false, nullptr, &tl); // header unchanged
-#endif
-    else h = pipe_pass<true, 0, false>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, b3, make_uint4(0, 0, 0, 0), false, Ring{});
-    // the frame's last block(s), the received tag written back unchanged
-    if (lines && PIPE_QUAD) quad_tail_store(pin_window(Ro), sg.nb >> 2, tl, want);
+    if (lines) h = pipe_pass<true, 0, true>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, hdr, true, Ro); // header unchanged
+    else h = pipe_pass<true, 0, false>(pl, stm, r, sg.nb, sg.c0, b0, b1, b2, make_uint4(0, 0, 0, 0), false, Ring{});
     h = combine_segments(h, r, sg.after, G);
     uint32_t tag[4];
     pipe_tag(h, r, P, ks + 4, tag);
@@ -887,40 +582,33 @@ __device__ __forceinline__ void pipe_open_packet(const OpenArgs &a, uint32_t i, 
         wave_sync();
         restore_forged(diff != 0, key, n1, n2, pl, sg.c0, sg.nb);
     }
-#endif
     if (j == 0) {
         a.status[i] = diff == 0 ? RG_PKT_OK : RG_PKT_DECRYPT_ERR;
         if (a.counters_out) a.counters_out[i] = ctr;
     }
 }
 
-// ------------------------------------------------------------- kernels
-// Persistent grid as seal_kernel<1> (rg_kernels.hip): the host launches at most
-// CUs x wg_per_cu workgroups with an LDS reservation that fixes residency.
-// With a diagnostics buffer (debug mode 3) lane 0 of every wave records
-// [s_memtime delta, real-time ticks to the end of the wave's first and second
-// unit, 0, start s_memrealtime, 4, 1, s_memrealtime delta] (tools/stamps.py;
-// s_memrealtime ticks at 100 MHz).
+// ------------------------------------------------------------- stamps
+#if RG_DIAG
+// Diagnostic builds: with a stamp buffer (debug mode 3, or any seal mode) lane 0 of every wave records
+// [s_memtime delta, real-time ticks to the end of the wave's first and second unit, XCC_ID << 32 |
+// HW_ID (wave slot, SIMD, CU, SH, SE), start s_memrealtime, 4, 1, s_memrealtime delta]
+// (tools/stamps.py, tools/coresidency.py; s_memrealtime ticks at 100 MHz).
 __device__ __forceinline__ void pipe_stamp(uint64_t *dbg, uint64_t t0, uint64_t r0, const uint64_t marks[2]) {
     const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
     if ((threadIdx.x & 63) == 0) {
         uint64_t *o = dbg + 8ull * (blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64);
-#if defined(RG_PIPE_WSTAMP)
-        o[0] = t1 - t0; // slots 1-3: the wait-stamp accumulators
-        o[5] = 5;
-        (void)marks;
-#elif !defined(RG_TILE_MARKS)
-        o[0] = t1 - t0; o[1] = marks[0] ? marks[0] - r0 : 0; o[2] = marks[1] ? marks[1] - r0 : 0; o[3] = 0;
-#ifdef RG_PIPE_LB2 // co-residency record: HW_ID (wave, SIMD, CU, SH, SE) and XCC_ID
+        o[0] = t1 - t0;
+        o[1] = marks[0] ? marks[0] - r0 : 0;
+        o[2] = marks[1] ? marks[1] - r0 : 0;
         o[3] = ((uint64_t)(uint32_t)__builtin_amdgcn_s_getreg(0xF814) << 32) | (uint32_t)__builtin_amdgcn_s_getreg(0xF804);
-#endif
+        o[4] = r0;
         o[5] = 4;
-#else
-        o[0] = marks[0];
-#endif
-        o[4] = r0; o[6] = 1; o[7] = r1 - r0;
+        o[6] = 1;
+        o[7] = r1 - r0;
     }
 }
+#endif
 
 // ---------------------------------------------------------------- walk
 // Identity order: lane units u = G * packet + segment, grid-stride (the stride
@@ -1020,30 +708,42 @@ __device__ __forceinline__ void pipe_walk(uint32_t n, uint32_t lg0, const PipePl
     }
 }
 
+// ------------------------------------------------------------- kernels
+// Persistent grid: the host launches at most CUs x wg_per_cu workgroups with
+// an LDS reservation that fixes residency.
 // flags: bits 0-1 log2 lanes per packet (without a plan), kPipeLinesFlag: the LDS ring is reserved
-#ifdef RG_PIPE_LB2
-#define RG_PIPE_LB __launch_bounds__(256, 2)
-#else
-#define RG_PIPE_LB __launch_bounds__(256)
-#endif
-template <int MODE> __global__ RG_PIPE_LB void pipe_seal_kernel(SealArgs a, uint32_t flags, PipePlan pp) {
-    const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+template <int MODE> __global__ __launch_bounds__(256) void pipe_seal_kernel(SealArgs a, uint32_t flags, PipePlan pp) {
     uint64_t marks[2] = {0, 0};
-    const bool lines = RG_PIPE_LINES && (flags & kPipeLinesFlag) != 0;
-    pipe_walk(a.n, flags & 3u, pp, a.desc, a.dbg != nullptr, marks, [=](uint32_t i, const rg_pkt_desc &d, uint32_t j, uint32_t G) {
+    const bool lines = (flags & kPipeLinesFlag) != 0;
+#if RG_DIAG
+    const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+    const bool stamp = a.dbg != nullptr;
+#else
+    constexpr bool stamp = false;
+#endif
+    pipe_walk(a.n, flags & 3u, pp, a.desc, stamp, marks, [=](uint32_t i, const rg_pkt_desc &d, uint32_t j, uint32_t G) {
         pipe_seal_packet<MODE>(a, i, d, j, G, lines);
     });
-    if (a.dbg) pipe_stamp(a.dbg, t0, r0, marks);
+#if RG_DIAG
+    if (stamp) pipe_stamp(a.dbg, t0, r0, marks);
+#endif
 }
 
-__global__ RG_PIPE_LB void pipe_open_kernel(OpenArgs a, uint32_t flags, PipePlan pp) {
-    const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+__global__ __launch_bounds__(256) void pipe_open_kernel(OpenArgs a, uint32_t flags, PipePlan pp) {
     uint64_t marks[2] = {0, 0};
-    const bool lines = RG_PIPE_LINES && (flags & kPipeLinesFlag) != 0;
-    pipe_walk(a.n, flags & 3u, pp, a.desc, a.dbg != nullptr, marks, [=](uint32_t i, const rg_pkt_desc &d, uint32_t j, uint32_t G) {
+    const bool lines = (flags & kPipeLinesFlag) != 0;
+#if RG_DIAG
+    const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+    const bool stamp = a.dbg != nullptr;
+#else
+    constexpr bool stamp = false;
+#endif
+    pipe_walk(a.n, flags & 3u, pp, a.desc, stamp, marks, [=](uint32_t i, const rg_pkt_desc &d, uint32_t j, uint32_t G) {
         pipe_open_packet(a, i, d, j, G, lines);
     });
-    if (a.dbg) pipe_stamp(a.dbg, t0, r0, marks);
+#if RG_DIAG
+    if (stamp) pipe_stamp(a.dbg, t0, r0, marks);
+#endif
 }
 
 static void pipe_grid(uint64_t units, const Launch &L, uint32_t &blocks, uint32_t &lds) {
@@ -1072,33 +772,46 @@ hipError_t launch_pipe(const SealArgs *sa, const OpenArgs *oa, const Launch &L, 
         pipe_grid((uint64_t)n << lg, L, blocks, lds);
     }
     const uint32_t fl = lg | (lds >= 4 * kRingBytes ? kPipeLinesFlag : 0u);
-    if (sa && L.debug_mode == 1) hipLaunchKernelGGL(pipe_seal_kernel<1>, dim3(blocks), dim3(256), lds, s, *sa, fl, pp);
-    else if (sa && L.debug_mode == 2) hipLaunchKernelGGL(pipe_seal_kernel<2>, dim3(blocks), dim3(256), lds, s, *sa, fl, pp);
-    else if (sa && L.debug_mode == 4) hipLaunchKernelGGL(pipe_seal_kernel<4>, dim3(blocks), dim3(256), lds, s, *sa, fl, pp);
-    else if (sa && L.debug_mode == 5) hipLaunchKernelGGL(pipe_seal_kernel<5>, dim3(blocks), dim3(256), lds, s, *sa, fl, pp);
-    else if (sa && L.debug_mode == 6) hipLaunchKernelGGL(pipe_seal_kernel<6>, dim3(blocks), dim3(256), lds, s, *sa, fl, pp);
-    else if (sa && L.debug_mode == 7) hipLaunchKernelGGL(pipe_seal_kernel<7>, dim3(blocks), dim3(256), lds, s, *sa, fl, pp);
-    else if (sa && L.debug_mode == 8) hipLaunchKernelGGL(pipe_seal_kernel<8>, dim3(blocks), dim3(256), lds, s, *sa, fl, pp);
-    else if (sa) hipLaunchKernelGGL(pipe_seal_kernel<0>, dim3(blocks), dim3(256), lds, s, *sa, fl, pp);
-    else hipLaunchKernelGGL(pipe_open_kernel, dim3(blocks), dim3(256), lds, s, *oa, fl, pp);
+    if (oa) {
+        hipLaunchKernelGGL(pipe_open_kernel, dim3(blocks), dim3(256), lds, s, *oa, fl, pp);
+        return hipGetLastError();
+    }
+#if RG_DIAG
+    switch (L.debug_mode) { // debug mode 3 (stamps) runs the normal seal
+    case 1: hipLaunchKernelGGL(pipe_seal_kernel<1>, dim3(blocks), dim3(256), lds, s, *sa, fl, pp); return hipGetLastError();
+    case 2: hipLaunchKernelGGL(pipe_seal_kernel<2>, dim3(blocks), dim3(256), lds, s, *sa, fl, pp); return hipGetLastError();
+    case 4: hipLaunchKernelGGL(pipe_seal_kernel<4>, dim3(blocks), dim3(256), lds, s, *sa, fl, pp); return hipGetLastError();
+    case 5: hipLaunchKernelGGL(pipe_seal_kernel<5>, dim3(blocks), dim3(256), lds, s, *sa, fl, pp); return hipGetLastError();
+    case 6: hipLaunchKernelGGL(pipe_seal_kernel<6>, dim3(blocks), dim3(256), lds, s, *sa, fl, pp); return hipGetLastError();
+    case 7: hipLaunchKernelGGL(pipe_seal_kernel<7>, dim3(blocks), dim3(256), lds, s, *sa, fl, pp); return hipGetLastError();
+    case 8: hipLaunchKernelGGL(pipe_seal_kernel<8>, dim3(blocks), dim3(256), lds, s, *sa, fl, pp); return hipGetLastError();
+    default: break;
+    }
+#endif
+    hipLaunchKernelGGL(pipe_seal_kernel<0>, dim3(blocks), dim3(256), lds, s, *sa, fl, pp);
     return hipGetLastError();
 }
 
 hipError_t prepare_pipe_kernels(int max_wg[2]) {
-    const void *f[9] = {(const void *)pipe_seal_kernel<0>, (const void *)pipe_open_kernel,
-                        (const void *)pipe_seal_kernel<1>, (const void *)pipe_seal_kernel<2>,
-                        (const void *)pipe_seal_kernel<4>, (const void *)pipe_seal_kernel<5>,
-                        (const void *)pipe_seal_kernel<6>, (const void *)pipe_seal_kernel<7>,
-                        (const void *)pipe_seal_kernel<8>};
-    for (int w = 0; w < 9; ++w) {
+    const void *f[2] = {(const void *)pipe_seal_kernel<0>, (const void *)pipe_open_kernel};
+    for (int w = 0; w < 2; ++w) {
         hipError_t e = hipFuncSetAttribute(f[w], hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsPerCu);
         if (e != hipSuccess) return e;
         int nb = 0;
-        if (w >= 2) continue;
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f[w], 256, 0);
         if (e != hipSuccess) return e;
         max_wg[w] = nb;
     }
+#if RG_DIAG
+    const void *d[7] = {(const void *)pipe_seal_kernel<1>, (const void *)pipe_seal_kernel<2>,
+                        (const void *)pipe_seal_kernel<4>, (const void *)pipe_seal_kernel<5>,
+                        (const void *)pipe_seal_kernel<6>, (const void *)pipe_seal_kernel<7>,
+                        (const void *)pipe_seal_kernel<8>};
+    for (const void *k : d) {
+        hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsPerCu);
+        if (e != hipSuccess) return e;
+    }
+#endif
     return hipSuccess;
 }
 

@@ -819,12 +819,18 @@ hipError_t launch_tiles(const SealArgs *sa, const OpenArgs *oa, int G, const Til
     if (G != 1 && G != 2) return hipErrorInvalidValue;
     if (need > kLdsPerCu) return hipErrorInvalidValue;
     const uint32_t lds = kLdsPerCu;
+#if RG_DIAG // stamped variants (debug mode 3): diagnostic builds only
 #define RG_TILES(GG)                                                                                          \
     if (L.debug_mode == 3) {                                                                                  \
         if (sa) hipLaunchKernelGGL((tile_kernel<GG, false, true>), dim3(blocks), dim3(threads), lds, s, a, b, tp); \
         else hipLaunchKernelGGL((tile_kernel<GG, true, true>), dim3(blocks), dim3(threads), lds, s, a, b, tp);     \
     } else if (sa) hipLaunchKernelGGL((tile_kernel<GG, false>), dim3(blocks), dim3(threads), lds, s, a, b, tp);   \
     else hipLaunchKernelGGL((tile_kernel<GG, true>), dim3(blocks), dim3(threads), lds, s, a, b, tp);
+#else
+#define RG_TILES(GG)                                                                                          \
+    if (sa) hipLaunchKernelGGL((tile_kernel<GG, false>), dim3(blocks), dim3(threads), lds, s, a, b, tp);      \
+    else hipLaunchKernelGGL((tile_kernel<GG, true>), dim3(blocks), dim3(threads), lds, s, a, b, tp);
+#endif
     if (G == 1) {
         RG_TILES(1)
     } else {
@@ -835,10 +841,13 @@ hipError_t launch_tiles(const SealArgs *sa, const OpenArgs *oa, int G, const Til
 }
 
 hipError_t prepare_tile_kernels() {
-    void *fs[8] = {(void *)tile_kernel<1, false>,       (void *)tile_kernel<2, false>,
-                   (void *)tile_kernel<1, true>,        (void *)tile_kernel<2, true>,
-                   (void *)tile_kernel<1, false, true>, (void *)tile_kernel<2, false, true>,
-                   (void *)tile_kernel<1, true, true>,  (void *)tile_kernel<2, true, true>};
+    void *fs[] = {(void *)tile_kernel<1, false>,       (void *)tile_kernel<2, false>,
+                  (void *)tile_kernel<1, true>,        (void *)tile_kernel<2, true>,
+#if RG_DIAG
+                  (void *)tile_kernel<1, false, true>, (void *)tile_kernel<2, false, true>,
+                  (void *)tile_kernel<1, true, true>,  (void *)tile_kernel<2, true, true>
+#endif
+    };
     for (void *f : fs) {
         hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsPerCu);
         if (e != hipSuccess) return e;

@@ -19,10 +19,11 @@ from conftest import REPO
 from rustyguard_amd import _lib
 
 HEADER = os.path.join(REPO, "include", "rg_aead.h")
+TEST_HEADER = os.path.join(REPO, "include", "rg_aead_test.h")
 
 
-def header_functions():
-    text = open(HEADER).read()
+def header_functions(path=HEADER):
+    text = open(path).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     return sorted(set(re.findall(r"\b(rg_[a-z0-9_]+)\s*\(", text)))
 
@@ -53,8 +54,52 @@ def test_ctypes_binding_covers_header():
     assert set(header_functions()) == set(_lib.SIGNATURES), set(header_functions()) ^ set(_lib.SIGNATURES)
 
 
+def _built():
+    from rustyguard_amd import build
+
+    build.build()
+    return build
+
+
+def _kernel_symbols(path):
+    out = subprocess.run(["nm", "-C", path], capture_output=True, text=True, check=True).stdout
+    return set(re.findall(r"(rg::(?:pipe_seal_kernel|pipe_open_kernel|tile_kernel|flat_kernel)<[^>]*>)", out))
+
+
+def test_product_library_has_no_diagnostics_or_test_hooks():
+    """the diagnostic seal modes (non-ciphertext output with a success status) and the stamp
+    variants are not compiled into the product library -- only pipe_seal_kernel<0> and the unstamped tile
+    kernels -- and the test hooks (include/rg_aead_test.h) are exported by the test library only."""
+    b = _built()
+    ks = _kernel_symbols(b.LIB)
+    seals = {k for k in ks if k.startswith("rg::pipe_seal_kernel")}
+    assert seals == {"rg::pipe_seal_kernel<0>"}, seals
+    assert not any(k.startswith("rg::tile_kernel") and k.endswith(", true>") and k.count(",") == 2 for k in ks), ks
+    prod = subprocess.run(["nm", "-D", "--defined-only", b.LIB], capture_output=True, text=True, check=True).stdout
+    test = subprocess.run(["nm", "-D", "--defined-only", b.TEST_LIB], capture_output=True, text=True,
+                          check=True).stdout
+    hooks = header_functions(TEST_HEADER)
+    assert hooks == ["rg_debug_fail_reserve", "rg_debug_read_arena"]
+    for h in hooks:
+        assert f" T {h}\n" not in prod and f" T {h}\n" in test, h
+    assert set(hooks) == set(_lib.TEST_SIGNATURES)
+    # the test library carries the same kernels as the product one
+    assert _kernel_symbols(b.TEST_LIB) == ks
+
+
+def test_product_library_refuses_debug_modes(tmp_path):
+    """rg_set_debug_mode(ctx, m != 0) and a stamp buffer are refused by the product library; checked on a
+    context-free path here (a null context is refused first) and on a real context by the GPU tests."""
+    L = _lib.lib()
+    assert L.rg_set_debug_mode(None, 0) == -1  # null context
+    src = open(os.path.join(REPO, "rustyguard_amd", "csrc", "rg_api.cpp")).read()
+    body = src[src.index("int rg_set_debug_mode("):]
+    body = body[:body.index("\n}\n")]
+    assert "#if RG_DIAG" in body and 'mode != 0) return set_err(RG_EINVAL' in body
+
+
 def test_abi_version():
-    assert _lib.lib().rg_abi_version() == 4
+    assert _lib.lib().rg_abi_version() == 5
 
 
 def test_struct_layout_with_gcc(tmp_path):

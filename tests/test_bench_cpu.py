@@ -28,7 +28,7 @@ def test_gpus_n_launches_n_ranks():
     assert sorted(x["local_rank"] for x in lines) == [0, 1]
     # the N > 1 line is self-contained: rank 0 also runs the same workload's 1-GPU base and the CPU baselines
     legs = {x["rank"]: x["legs"] for x in lines}
-    assert legs[0] == ["timed", "base_1gpu", "cpu_baseline"] and legs[1] == ["timed"]
+    assert legs[0] == ["timed", "base_1gpu", "single_process", "cpu_baseline"] and legs[1] == ["timed"]
 
 
 def test_single_gpu_defaults_to_cfg2():

@@ -1,0 +1,252 @@
+"""One thread driving several contexts (rg_group, include/rg_aead.h "several GPUs, one thread") and the
+per-peer endpoint record (rg_sessions_insert_peer).
+
+The reference's host is one thread owning one Sessions (rustyguard-core/src/lib.rs:349-352); a group
+splits each batch into contiguous ranges over its contexts and runs their pipelines from that thread.
+Packets are independent, so every result must equal the one-context / oracle result
+byte for byte.  These tests put N = 2 and 4 contexts on device 0 (one GPU is enough to run every code
+path: streams, splits, the round-robin issue, the gather)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle
+from rustyguard_amd import aead, workloads
+from rustyguard_amd.aead import Engine, Group, Sessions
+from rustyguard_amd.workloads import DESC_DTYPE
+
+pytestmark = pytest.mark.gpu
+S = 1_000_000_000
+
+
+@pytest.fixture(scope="module", params=[2, 4])
+def group(request):
+    g = Group([0] * request.param)
+    yield g
+    g.close()
+
+
+def _ragged(rng, n, keys=5):
+    """A mixed batch: IMIX-like sizes, keepalives (P = 0), several keys, 16-byte gaps between frames."""
+    sizes = rng.choice([0, 16, 64, 576, 1504, 2048], size=n, p=[0.05, 0.15, 0.3, 0.25, 0.2, 0.05])
+    desc = np.zeros(n, DESC_DTYPE)
+    off = 0
+    for i, p in enumerate(sizes):
+        desc[i] = (off, p, rng.integers(0, keys))
+        off += p + 32 + 16 * int(rng.integers(0, 3))
+    buf = rng.integers(0, 256, off + 256, dtype=np.uint8)
+    kt = rng.integers(0, 256, (keys, 32), dtype=np.uint8)
+    rec = rng.integers(0, 2**32, keys, dtype=np.uint64).astype(np.uint32)
+    ctr = rng.integers(0, 2**40, n, dtype=np.uint64)
+    return kt, rec, desc, ctr, buf
+
+
+def test_group_host_seal_open_match_the_oracle(group):
+    rng = np.random.default_rng(len(group))
+    kt, rec, desc, ctr, buf = _ragged(rng, 3000)
+    want = buf.copy()
+    oracle.seal_batch(kt, rec, desc, ctr, want)
+    got = buf.copy()
+    st = group.seal_host(kt, rec, desc, ctr, got)
+    assert (st == 0).all() and np.array_equal(got, want)
+    od = desc.copy()
+    od["len"] += 32
+    ow = want.copy()
+    so_w, co_w = oracle.open_batch(kt, od, ow)
+    so, co = group.open_host(kt, od, got)
+    assert (so_w == 0).all() and np.array_equal(so, so_w) and np.array_equal(got, ow)
+    assert np.array_equal(co, co_w) and np.array_equal(co, ctr)
+    # a forged tag in every part of the split: statuses and bytes as the oracle's (frames left as they came)
+    sealed = want.copy()
+    bnd = aead.split_batch(od, len(group), open_=True)
+    for k in range(len(group)):
+        i = int(bnd[k])
+        if i < len(od):
+            sealed[int(od[i]["offset"]) + int(od[i]["len"]) - 1] ^= 1
+    ow2, got2 = sealed.copy(), sealed.copy()
+    so_w2, _ = oracle.open_batch(kt, od, ow2)
+    so2, _ = group.open_host(kt, od, got2)
+    assert (so_w2 == 1).sum() == len(group) and np.array_equal(so2, so_w2) and np.array_equal(got2, ow2)
+
+
+def test_group_host_large_batch_spans_many_slices(group):
+    """config 2 sized batch: every context runs several 16 MiB pipeline slices, interleaved round-robin."""
+    w = workloads.build("cfg2")
+    buf = np.zeros(w.buf_bytes, np.uint8)
+    oracle.synth_fill(buf, w.desc, w.inner_len, w.data_seed)
+    plain = buf.copy()
+    st = group.seal_host(w.keys, w.receivers, w.desc, w.counters, buf)
+    assert (st == 0).all()
+    ref = plain.copy()
+    sub = slice(0, w.n, 997)  # the oracle on a sample of packets (bit-exact per packet)
+    d = w.desc[sub].copy()
+    oracle.seal_batch(w.keys, w.receivers, d, w.counters[sub], ref)
+    for k in range(0, len(d)):
+        o, p = int(d[k]["offset"]), int(d[k]["len"]) + 32
+        assert np.array_equal(buf[o:o + p], ref[o:o + p]), k
+    so, co = group.open_host(w.keys, w.open_desc(), buf)
+    assert (so == 0).all() and np.array_equal(co, w.counters)
+    pay = np.zeros(len(buf), bool)  # the payload bytes are back to the plaintext (headers and tags stay)
+    for o, p in zip(w.desc["offset"].astype(np.int64), w.desc["len"].astype(np.int64)):
+        pay[o + 16:o + 16 + p] = True
+    assert np.array_equal(buf[pay], plain[pay])
+
+
+def test_group_device_shards(group):
+    """rg_seal_batch_dev_multi / rg_open_batch_dev_multi: one shard per context (here all on device 0,
+    each with its own tensors and stream), enqueued from one thread without waiting."""
+    rng = np.random.default_rng(77)
+    kt, rec, desc, ctr, buf = _ragged(rng, 2000)
+    b = aead.split_batch(desc, len(group))
+    want = buf.copy()
+    oracle.seal_batch(kt, rec, desc, ctr, want)
+    streams = [torch.cuda.Stream() for _ in range(len(group))]
+    shards = []
+    for k in range(len(group)):
+        d = desc[b[k]:b[k + 1]].copy()
+        shards.append({"keys": torch.from_numpy(kt.reshape(-1)).cuda(), "receivers": torch.from_numpy(rec).cuda(),
+                       "desc": torch.from_numpy(d.view(np.uint8)).cuda(), "counters": torch.from_numpy(ctr[b[k]:b[k + 1]].copy()).cuda(),
+                       "buf": torch.from_numpy(buf.copy()).cuda(), "status": torch.zeros(max(len(d), 1), dtype=torch.uint8, device="cuda"),
+                       "stream": streams[k]})
+    torch.cuda.synchronize()
+    group.seal_dev(shards)
+    torch.cuda.synchronize()
+    for k, sh in enumerate(shards):
+        got = sh["buf"].cpu().numpy()
+        assert (sh["status"].cpu().numpy()[: b[k + 1] - b[k]] == 0).all()
+        for i in range(b[k], b[k + 1]):
+            o, p = int(desc[i]["offset"]), int(desc[i]["len"]) + 32
+            assert np.array_equal(got[o:o + p], want[o:o + p]), i
+    for sh in shards:
+        od = sh["desc"].cpu().numpy().view(DESC_DTYPE).copy()
+        od["len"] += 32
+        sh["desc"] = torch.from_numpy(od.view(np.uint8)).cuda()
+        sh["counters_out"] = torch.zeros(len(od), dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    group.open_dev(shards)
+    torch.cuda.synchronize()
+    for k, sh in enumerate(shards):
+        assert (sh["status"].cpu().numpy()[: b[k + 1] - b[k]] == 0).all()
+        assert np.array_equal(sh["counters_out"].cpu().numpy().astype(np.uint64), ctr[b[k]:b[k + 1]])
+        got = sh["buf"].cpu().numpy()
+        for i in range(b[k], b[k + 1]):
+            o, p = int(desc[i]["offset"]), int(desc[i]["len"]) + 32
+            assert np.array_equal(got[o + 16:o + p - 16], buf[o + 16:o + p - 16]), i
+
+
+def _keys(seed):
+    rng = np.random.default_rng(seed)
+    return [rng.integers(0, 256, 32, dtype=np.uint8).tobytes() for _ in range(4)]
+
+
+def _frames(sizes, rng):
+    desc = np.zeros(len(sizes), DESC_DTYPE)
+    off = 0
+    for i, p in enumerate(sizes):
+        desc[i] = (off, p, 0)
+        off += p + 32
+    buf = np.zeros(off + 64, np.uint8)
+    for d in desc:
+        buf[d["offset"] + 16: d["offset"] + 16 + d["len"]] = rng.integers(0, 256, d["len"], dtype=np.uint8)
+    return desc, buf
+
+
+def test_group_sessions_match_one_context(group, engine):
+    """A session table on a group (rg_sessions_create_group) gives the single-context table's results:
+    counters reserved in array order before the split, the anti-replay pass after the gather --
+    duplicates, forgeries and in-batch replays included."""
+    k_ab, k_ba, k_ac, k_ca = _keys(5)
+    rng = np.random.default_rng(9)
+    tabs = []
+    for e in (engine, group):
+        a = Sessions(e, 8)
+        sa = a.insert(0x1111, 0x2222, k_ab, k_ba)
+        sc = a.insert(0x3333, 0x4444, k_ac, k_ca)
+        tabs.append((a, sa, sc))
+    b = Sessions(engine, 8)
+    sb = b.insert(0x2222, 0x1111, k_ba, k_ab)
+    sizes = list(rng.choice([0, 16, 64, 576, 1504], size=700))
+    slots = [tabs[0][1] if x % 3 else tabs[0][2] for x in range(700)]
+    desc, buf = _frames(sizes, rng)
+    outs = []
+    for a, sa, sc in tabs:
+        fr = buf.copy()
+        st, rk = a.send_batch(slots, desc, fr)
+        outs.append((st, fr))
+        assert a.send_counter(sa) == sum(1 for s in slots if s == sa)
+    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
+    # B -> A traffic with replays and a forgery, received by both A tables
+    bdesc, bbuf = _frames([64] * 50 + [1504] * 50, rng)
+    st, _ = b.send_batch([sb] * 100, bdesc, bbuf)
+    od = bdesc.copy()
+    od["len"] += 32
+    idx = np.concatenate([np.arange(100), [5, 17, 5, 99]])  # in-batch replays
+    rd = od[idx].copy()
+    forged = int(rd[40]["offset"]) + int(rd[40]["len"]) - 1
+    res = []
+    for a, sa, sc in tabs:
+        fr = bbuf.copy()
+        fr[forged] ^= 1
+        st, sl, fl = a.recv_batch(rd.copy(), fr, src=np.arange(len(rd), dtype=np.uint64) + 1000, flags=True)
+        res.append((st, sl, fl, fr, a.endpoint(sa)))
+    for x, y in zip(res[0], res[1]):
+        assert np.array_equal(np.asarray(x), np.asarray(y))
+    assert res[0][0][40] == aead.PKT_DECRYPT_ERR and list(res[0][0][100:]) == [aead.PKT_REJECTED] * 4
+
+
+def test_group_sessions_refuse_device_frames(group):
+    a = Sessions(group, 4)
+    s0 = a.insert(1, 2, bytes(32), bytes(32))
+    d = torch.zeros(16, dtype=torch.uint8, device="cuda")
+    with pytest.raises(Exception):
+        a.send_batch_dev([s0], d, torch.zeros(64, dtype=torch.uint8, device="cuda"))
+
+
+def test_peer_endpoint_survives_a_rekey(engine):
+    """peer.endpoint is per peer (rustyguard-core/src/lib.rs:670-671) and the
+    Keepalive timer sends to it (time.rs:135).  After a rekey (a new session slot of the same peer) the
+    new slot reports the endpoint the old one authenticated, and a due keepalive carries that address."""
+    k1, k2, k3, k4 = _keys(11)
+    rng = np.random.default_rng(12)
+    a, b = Sessions(engine, 8), Sessions(engine, 8)
+    PEER = 42
+    s_old = a.insert(0x10, 0x20, k1, k2, peer=PEER)
+    b_old = b.insert(0x20, 0x10, k2, k1)
+    assert a.endpoint(s_old) is None and a.peer_endpoint(PEER) is None
+    desc, buf = _frames([64], rng)
+    assert (b.send_batch([b_old], desc, buf)[0] == 0).all()
+    od = desc.copy()
+    od["len"] += 32
+    st, _ = a.recv_batch(od.copy(), buf.copy(), src=np.array([555], np.uint64))
+    assert st[0] == 0 and a.endpoint(s_old) == 555 and a.peer_endpoint(PEER) == 555
+    # rekey: a new session of the same peer (new ids, new keys); nothing authenticated on it yet
+    s_new = a.insert(0x11, 0x21, k3, k4, peer=PEER)
+    b_new = b.insert(0x21, 0x11, k4, k3)
+    assert a.endpoint(s_new) == 555
+    # a genuine packet on the OLD session from a roamed address moves the peer's endpoint for both
+    desc2, buf2 = _frames([16], rng)
+    assert (b.send_batch([b_old], desc2, buf2)[0] == 0).all()
+    od2 = desc2.copy()
+    od2["len"] += 32
+    st, _ = a.recv_batch(od2.copy(), buf2.copy(), src=np.array([556], np.uint64))
+    assert st[0] == 0 and a.endpoint(s_new) == 556 and a.endpoint(s_old) == 556
+    # the keepalive of the new session goes to the peer's endpoint once the session has been quiet
+    a.set_time(11 * S)
+    assert a.keepalive(s_new) == 556
+    a.set_time(11 * S)
+    desc3, buf3 = _frames([0], rng)
+    assert (a.send_batch([s_new], desc3, buf3)[0] == 0).all()  # the keepalive itself resets `sent`
+    assert a.keepalive(s_new) is None
+    # a session without a peer keeps its own endpoint, as before
+    s_own = a.insert(0x12, 0x22, k1, k3)
+    assert a.endpoint(s_own) is None
+    _ = b_new
+
+
+def test_keepalive_without_endpoint_is_an_error(engine):
+    k1, k2, _, _ = _keys(13)
+    a = Sessions(engine, 4)
+    s = a.insert(0x30, 0x40, k1, k2, peer=7)
+    a.set_time(11 * S)
+    with pytest.raises(Exception):
+        a.keepalive(s)  # due, but the peer never authenticated a packet

@@ -13,7 +13,7 @@ import pytest
 
 from conftest import load_golden
 from oracle import oracle
-from rustyguard_amd import aead, workloads
+from rustyguard_amd import _lib, aead, workloads
 from rustyguard_amd.workloads import DESC_DTYPE
 
 pytestmark = pytest.mark.gpu
@@ -1005,7 +1005,7 @@ def test_flat_first_launch_inside_graph_capture():
     assert np.array_equal(got, ref)
 
 
-def test_per_message_key_wiped_from_device(engine):
+def test_per_message_key_wiped_from_device():
     """The per-message drop-in leaves no key in device memory (the reference zeroizes keys on drop,
     rustyguard-crypto/src/prim.rs:227-231): after enc, dec, a failed dec and the XChaCha pair, the
     device arena read back through the test hook holds none of the key bytes."""
@@ -1013,6 +1013,7 @@ def test_per_message_key_wiped_from_device(engine):
 
     from rustyguard_amd import _lib
 
+    engine = aead.Engine(0, library=_lib.lib_test())  # the hook lives in the test library only
     key = bytes(range(0xA0, 0xC0))
     msg = bytearray(b"\x5a" * 200)
     tag = engine.chacha20poly1305_enc(key, aead.nonce(9), b"aad", msg)
@@ -1022,8 +1023,23 @@ def test_per_message_key_wiped_from_device(engine):
     xt = engine.xchacha20poly1305_enc(key, bytes(24), b"", msg)
     engine.xchacha20poly1305_dec(key, bytes(24), b"", msg, xt)
     out = (ctypes.c_uint8 * (1 << 16))()
-    got = _lib.check(_lib.lib().rg_debug_read_arena(engine.handle, 0, out, len(out)), "rg_debug_read_arena")
+    got = _lib.check(engine.library.rg_debug_read_arena(engine.handle, 0, out, len(out)), "rg_debug_read_arena",
+                     engine.library)
     assert got > 0
     arena = bytes(out[:got])
     for w in range(0, 32, 8):  # no 8-byte run of the key anywhere
         assert key[w:w + 8] not in arena
+
+
+def test_product_library_refuses_diagnostic_modes(engine):
+    """a product context cannot be switched to a diagnostic seal mode (output that is
+    not ciphertext with a success status) or given a stamp buffer; mode 0 stays accepted."""
+    import torch
+
+    for m in (1, 2, 3, 4, 7, 8):
+        with pytest.raises(_lib.RgError):
+            engine.set_debug_mode(m)
+    engine.set_debug_mode(0)
+    with pytest.raises(_lib.RgError):
+        engine.set_debug_buffer(torch.zeros(64, dtype=torch.int64, device="cuda"))
+    engine.set_debug_buffer(None)

@@ -8,7 +8,7 @@ import pytest
 import torch
 
 from rustyguard_amd import _lib, aead
-from rustyguard_amd.aead import Sessions
+from rustyguard_amd.aead import Engine, Sessions
 from rustyguard_amd.workloads import DESC_DTYPE
 
 pytestmark = pytest.mark.gpu
@@ -206,11 +206,12 @@ def test_recv_batch_dev_pending_rules(engine):
     assert list(st) == [0, 0] and list(sl) == [s2, s2]
 
 
-def test_recv_batch_dev_failed_setup_leaves_no_pending_batch(engine):
+def test_recv_batch_dev_failed_setup_leaves_no_pending_batch():
     """An allocation that fails inside rg_recv_batch_dev (forced by rg_debug_fail_reserve: the k-th
     allocation after the hook is armed) leaves no pending batch behind -- finish reports none, and
     neither the window nor the frames moved: the next receive matches the host path on a twin table."""
-    L = _lib.lib()
+    L = _lib.lib_test()  # rg_debug_fail_reserve lives in the test library only
+    engine = Engine(0, library=L)
     failed = 0
     try:
         for k in range(1, 12):
