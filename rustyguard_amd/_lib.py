@@ -87,6 +87,7 @@ SIGNATURES = {
     "rg_seal_batch_dev_multi": (c_int, [c_vp, c_vp]),
     "rg_open_batch_dev_multi": (c_int, [c_vp, c_vp]),
     "rg_sessions_create_group": (c_int, [c_vp, c_u32, ctypes.POINTER(c_vp)]),
+    "rg_set_host_slice": (c_int, [c_vp, c_size]),
 }
 
 # include/rg_aead_test.h: exported by the test library (librg_aead_test.so) only
@@ -104,13 +105,17 @@ def lib_path() -> str:
     return _build.LIB
 
 
-def _load(path: str, sigs: dict, build_if_missing: bool):
+def _load(path: str, sigs: dict, build_if_missing: bool, partial: bool = False):
+    """partial: an experimental build (RG_AEAD_LIB) may predate the newest entry points; those are left
+    unbound instead of failing the load (the in-tree libraries must export every one)."""
     if not os.path.exists(path):
         if not build_if_missing:
             raise RgError(f"{os.path.basename(path)} missing at {path}; run python -m rustyguard_amd.build")
         _build.build()
     L = ctypes.CDLL(path)
     for name, (res, args) in sigs.items():
+        if partial and not hasattr(L, name):
+            continue
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
@@ -122,7 +127,7 @@ def lib(build_if_missing: bool = True):
     global _lib
     if _lib is None:
         path = os.environ.get("RG_AEAD_LIB") or _build.LIB  # override: experimental builds only
-        _lib = _load(path, SIGNATURES, build_if_missing)
+        _lib = _load(path, SIGNATURES, build_if_missing, partial=path != _build.LIB)
     return _lib
 
 

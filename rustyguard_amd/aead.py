@@ -151,6 +151,10 @@ class Engine:
         self._check(self._L.rg_set_debug_buffer(self._h, _vp(tensor) if tensor is not None else None),
               "rg_set_debug_buffer")
 
+    def set_host_slice(self, nbytes: int):
+        """Byte span of one host-pipeline slice (rg_set_host_slice; default 16 MiB)."""
+        self._check(self._L.rg_set_host_slice(self._h, nbytes), "rg_set_host_slice")
+
     def set_wg_per_cu(self, wg: int):
         self._check(self._L.rg_set_wg_per_cu(self._h, wg), "rg_set_wg_per_cu")
 

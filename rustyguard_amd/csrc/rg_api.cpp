@@ -194,6 +194,7 @@ struct rg_ctx {
     int plan = 2;     // size-class planner: 0 off (array order), 1 always, 2 auto (skip for single-class batches)
     int segments = 0; // segments per packet: 0 = automatic, else 1 / 2 / 4
     int last_kernel = -1; // kernel family of the latest batched launch (-1: none yet)
+    size_t host_slice = 16ull << 20; // byte span of one host-pipeline slice (rg_set_host_slice)
     PlanBuf plan_dev; // planner lists of the device API (calls on one ctx are stream-ordered)
     uint64_t *dbg = nullptr; // diagnostics buffer (device), stamp builds only
     int pipe_max_wg[2] = {0, 0}; // [seal, open] resident workgroups per CU of the pipelined kernel
@@ -308,6 +309,13 @@ int rg_set_wg_per_cu(rg_ctx *ctx, int wg) {
     if (!ctx) return set_err(RG_EINVAL, "null context");
     if (wg < -1 || wg > 8) return set_err(RG_EINVAL, "wg_per_cu must be -1..8");
     ctx->wg_per_cu = wg;
+    return RG_OK;
+}
+
+int rg_set_host_slice(rg_ctx *ctx, size_t bytes) {
+    if (!ctx) return set_err(RG_EINVAL, "null context");
+    if (bytes < (64u << 10) || bytes > (1ull << 30)) return set_err(RG_EINVAL, "host slice must be 64 KiB .. 1 GiB");
+    ctx->host_slice = bytes;
     return RG_OK;
 }
 
@@ -650,7 +658,7 @@ void rg_host_free(void *p) {
 // ------------------------------------------------------------ host pipeline
 namespace {
 
-constexpr size_t kSliceBytes = 16ull << 20; // frames per pipeline slice
+constexpr size_t kSliceBytesDefault = 16ull << 20; // frames per pipeline slice (rg_set_host_slice)
 constexpr size_t kSlicePkts = 1u << 16;
 constexpr uint64_t kOutOfRange = (UINT64_MAX / 2) & ~15ull;
 
@@ -713,12 +721,13 @@ int HostRun::step() {
     // slice [i, j): bounded by packet count and by the byte span of its frames
     size_t j = i;
     uint64_t lo = UINT64_MAX, hi = 0;
+    const size_t slice_bytes = ctx->host_slice;
     while (j < end && j - i < kSlicePkts) {
         const rg_pkt_desc &d = desc[j];
         if (in_arena(d, open, buf_len)) {
             const uint64_t e = d.offset + (uint64_t)d.len + (open ? 0 : 32);
             const uint64_t nlo = std::min<uint64_t>(lo, d.offset & ~15ull), nhi = std::max<uint64_t>(hi, e);
-            if (j > i && nhi - nlo > kSliceBytes) break;
+            if (j > i && nhi - nlo > slice_bytes) break;
             lo = nlo;
             hi = nhi;
         }
@@ -807,11 +816,60 @@ int run_host(std::vector<HostRun> &runs) {
     return rc;
 }
 
+// A slice moves the byte span of its frames H2D and back D2H, so slices must cover disjoint spans: with
+// the descriptors in offset order they do (frames do not overlap), in any other order a slice's span
+// would take in other slices' frames and its D2H copy could put back stale bytes over their results.
+// Batches not in offset order therefore run on a sorted copy of the descriptors (and counters), their
+// statuses and counters scattered back to the caller's order afterwards.
+struct HostOrder {
+    bool identity = true;
+    std::vector<rg_pkt_desc> desc;
+    std::vector<uint64_t> ctr, ctr_out;
+    std::vector<uint8_t> status;
+    std::vector<uint32_t> perm; // sorted position k -> caller index
+};
+
+bool in_offset_order(const rg_pkt_desc *desc, size_t n) {
+    for (size_t i = 1; i < n; ++i)
+        if (desc[i].offset < desc[i - 1].offset) return false;
+    return true;
+}
+
+// RunFn(desc, counters, status, counters_out): the pipeline over the (possibly permuted) arrays
+template <class RunFn>
+int run_ordered(const rg_pkt_desc *desc, const uint64_t *counters, size_t n, uint8_t *status, uint64_t *counters_out,
+                RunFn &&run) {
+    if (in_offset_order(desc, n)) return run(desc, counters, status, counters_out);
+    HostOrder o;
+    o.perm.resize(n);
+    for (size_t i = 0; i < n; ++i) o.perm[i] = (uint32_t)i;
+    std::stable_sort(o.perm.begin(), o.perm.end(),
+                     [&](uint32_t a, uint32_t b) { return desc[a].offset < desc[b].offset; });
+    o.desc.resize(n);
+    o.status.resize(n);
+    for (size_t k = 0; k < n; ++k) o.desc[k] = desc[o.perm[k]];
+    if (counters) {
+        o.ctr.resize(n);
+        for (size_t k = 0; k < n; ++k) o.ctr[k] = counters[o.perm[k]];
+    }
+    if (counters_out) o.ctr_out.resize(n);
+    const int rc = run(o.desc.data(), counters ? o.ctr.data() : nullptr, o.status.data(),
+                       counters_out ? o.ctr_out.data() : nullptr);
+    for (size_t k = 0; k < n; ++k) {
+        status[o.perm[k]] = o.status[k];
+        if (counters_out) counters_out[o.perm[k]] = o.ctr_out[k];
+    }
+    return rc;
+}
+
 int host_batch(rg_ctx *ctx, bool open, uint32_t nkeys, const rg_pkt_desc *desc, const uint64_t *counters, size_t n,
                uint8_t *buf, size_t buf_len, uint8_t *status, uint64_t *counters_out, bool with_receivers) {
-    std::vector<HostRun> runs{HostRun{ctx, open, nkeys, desc, counters, 0, n, buf, buf_len, status, counters_out,
-                                      with_receivers}};
-    return run_host(runs);
+    return run_ordered(desc, counters, n, status, counters_out,
+                       [&](const rg_pkt_desc *d, const uint64_t *c, uint8_t *st, uint64_t *co) {
+                           std::vector<HostRun> runs{
+                               HostRun{ctx, open, nkeys, d, c, 0, n, buf, buf_len, st, co, with_receivers}};
+                           return run_host(runs);
+                       });
 }
 
 } // namespace
@@ -908,19 +966,23 @@ int host_multi(rg_group *g, bool open, const uint8_t *keys, const uint32_t *rece
     DeviceGuard dg;
     GroupLock lk(g);
     const int parts = (int)g->ctx.size();
-    std::vector<size_t> b(parts + 1);
-    split_bounds(desc, n, open, parts, b.data());
-    std::vector<HostRun> runs;
     for (int k = 0; k < parts; ++k) {
-        rg_ctx *c = g->ctx[k];
-        if (b[k] == b[k + 1]) continue;
-        RG_HIP(hipSetDevice(c->device), "hipSetDevice");
-        int rc = upload_keys(c, keys, receivers, nkeys);
+        RG_HIP(hipSetDevice(g->ctx[k]->device), "hipSetDevice");
+        int rc = upload_keys(g->ctx[k], keys, receivers, nkeys);
         if (rc) return rc;
-        runs.push_back(HostRun{c, open, nkeys, desc, counters, b[k], b[k + 1], buf, buf_len, status, counters_out,
-                               receivers != nullptr});
     }
-    return run_host(runs);
+    // the split is over the batch in offset order, so the contexts' byte spans are disjoint too
+    return run_ordered(desc, counters, n, status, counters_out,
+                       [&](const rg_pkt_desc *d, const uint64_t *c, uint8_t *st, uint64_t *co) {
+                           std::vector<size_t> b(parts + 1);
+                           split_bounds(d, n, open, parts, b.data());
+                           std::vector<HostRun> runs;
+                           for (int k = 0; k < parts; ++k)
+                               if (b[k] < b[k + 1])
+                                   runs.push_back(HostRun{g->ctx[k], open, nkeys, d, c, b[k], b[k + 1], buf, buf_len,
+                                                          st, co, receivers != nullptr});
+                           return run_host(runs);
+                       });
 }
 
 } // namespace
