@@ -171,12 +171,15 @@ struct PlanBuf {
     }
 };
 
-// one pipeline lane of the host path
+// one slice buffer set of the host path: the slice's frames, descriptors, counters and statuses on
+// both sides, and the events that order it through the three pipeline streams (rg_ctx::hs_*)
 struct Slot {
-    hipStream_t stream = nullptr;
     PlanBuf plan;
     DevBuf d_buf, d_desc, d_ctr, d_status, d_ctr_out;
     HostBuf h_desc, h_ctr, h_status, h_ctr_out;
+    hipEvent_t ev_in = nullptr;  // the slice's inputs are on the device (recorded on hs_in)
+    hipEvent_t ev_run = nullptr; // its kernel is done (recorded on hs_run)
+    hipEvent_t ev_out = nullptr; // its outputs are back in host memory (recorded on hs_out)
     // bookkeeping of the slice in flight
     size_t i0 = 0, i1 = 0;
     bool busy = false;
@@ -194,12 +197,23 @@ struct rg_ctx {
     int plan = 2;     // size-class planner: 0 off (array order), 1 always, 2 auto (skip for single-class batches)
     int segments = 0; // segments per packet: 0 = automatic, else 1 / 2 / 4
     int last_kernel = -1; // kernel family of the latest batched launch (-1: none yet)
-    size_t host_slice = 16ull << 20; // byte span of one host-pipeline slice (rg_set_host_slice)
+    size_t host_slice = 16ull << 20; // byte span of one host-pipeline slice (rg_set_host_slice; 16 MiB default)
     PlanBuf plan_dev; // planner lists of the device API (calls on one ctx are stream-ordered)
     uint64_t *dbg = nullptr; // diagnostics buffer (device), stamp builds only
     int pipe_max_wg[2] = {0, 0}; // [seal, open] resident workgroups per CU of the pipelined kernel
     std::mutex mu;
-    Slot slots[3]; // host pipeline: up to three slices in flight (H2D of one beside D2H of another)
+    // Host pipeline: up to kHostSlots slices in flight.  All uploads go through hs_in, all kernels through
+    // hs_run and all downloads through hs_out, so that copies of one direction run one after another at
+    // the link's full rate while the other direction's copy of a neighbouring slice runs beside them
+    // (round 4: with one stream per slice the three slices' H2D copies ran at once and shared the
+    // link, then their D2H copies -- half duplex, 27 GB/s per direction against a 48 GB/s duplex
+    // ceiling; profiles/r4_e2e.txt).  Four slots: the host reuses a slot once its slice is back, and with
+    // three the upload of slice k + 1 waited for the download of slice k - 2, which ends with slice k's
+    // upload, plus the host's wake-up (~46 us per 16 MiB slice).
+    static constexpr int kHostSlots = 4;
+    Slot slots[kHostSlots];
+    hipStream_t hs_in = nullptr, hs_run = nullptr, hs_out = nullptr;
+    hipStream_t gen_stream = nullptr; // the per-message drop-in
     DevBuf d_keys, d_recv;
     DevBuf d_general;  // per-message drop-in arena: [job][aad][payload][tag]
     HostBuf h_general; // its pinned host image (one H2D and one D2H per call)
@@ -252,8 +266,13 @@ int rg_create(int device, rg_ctx **out) {
             return set_err(RG_EDEVICE, "kernel setup", e);
         }
     }
-    for (auto &s : c->slots) {
-        hipError_t e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
+    {
+        hipError_t e = hipSuccess;
+        for (hipStream_t *sp : {&c->hs_in, &c->hs_run, &c->hs_out, &c->gen_stream})
+            if (e == hipSuccess) e = hipStreamCreateWithFlags(sp, hipStreamNonBlocking);
+        for (auto &s : c->slots)
+            for (hipEvent_t *ep : {&s.ev_in, &s.ev_run, &s.ev_out})
+                if (e == hipSuccess) e = hipEventCreateWithFlags(ep, hipEventDisableTiming);
         if (e != hipSuccess) {
             rg_destroy(c);
             return set_err(RG_EDEVICE, "hipStreamCreate", e);
@@ -266,11 +285,14 @@ int rg_create(int device, rg_ctx **out) {
 void rg_destroy(rg_ctx *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
-    for (auto &s : ctx->slots) {
-        if (s.stream) {
-            (void)hipStreamSynchronize(s.stream);
-            (void)hipStreamDestroy(s.stream);
+    for (hipStream_t sp : {ctx->hs_in, ctx->hs_run, ctx->hs_out, ctx->gen_stream})
+        if (sp) {
+            (void)hipStreamSynchronize(sp);
+            (void)hipStreamDestroy(sp);
         }
+    for (auto &s : ctx->slots) {
+        for (hipEvent_t ep : {s.ev_in, s.ev_run, s.ev_out})
+            if (ep) (void)hipEventDestroy(ep);
         s.plan.release();
         s.d_buf.release(); s.d_desc.release(); s.d_ctr.release(); s.d_status.release(); s.d_ctr_out.release();
         s.h_desc.release(); s.h_ctr.release(); s.h_status.release(); s.h_ctr_out.release();
@@ -658,7 +680,6 @@ void rg_host_free(void *p) {
 // ------------------------------------------------------------ host pipeline
 namespace {
 
-constexpr size_t kSliceBytesDefault = 16ull << 20; // frames per pipeline slice (rg_set_host_slice)
 constexpr size_t kSlicePkts = 1u << 16;
 constexpr uint64_t kOutOfRange = (UINT64_MAX / 2) & ~15ull;
 
@@ -680,7 +701,7 @@ int upload_keys(rg_ctx *ctx, const uint8_t *keys, const uint32_t *receivers, uin
 // Drain a finished slice: copy statuses / counters back to the caller.
 int finish_slot(Slot &s, uint8_t *status, uint64_t *counters_out) {
     if (!s.busy) return RG_OK;
-    RG_HIP(hipStreamSynchronize(s.stream), "slice sync");
+    RG_HIP(hipEventSynchronize(s.ev_out), "slice sync");
     const size_t m = s.i1 - s.i0;
     if (status) memcpy(status + s.i0, s.h_status.p, m);
     if (counters_out) memcpy(counters_out + s.i0, s.h_ctr_out.p, m * 8);
@@ -750,15 +771,25 @@ int HostRun::step() {
         // frames outside the arena get an aligned out-of-range offset: the kernel flags them INVALID
         hd[k].offset = in_arena(desc[i + k], open, buf_len) ? desc[i + k].offset - lo : kOutOfRange;
     }
-    hipStream_t st = s.stream;
-    RG_HIP(hipMemcpyAsync(s.d_desc.p, hd, m * sizeof(rg_pkt_desc), hipMemcpyHostToDevice, st), "H2D desc");
-    if (span) RG_HIP(hipMemcpyAsync(s.d_buf.p, buf + lo, span, hipMemcpyHostToDevice, st), "H2D frames");
+    // uploads on hs_in (after the previous use of this slot's device buffers has been downloaded: the
+    // host waited for ev_out above, so nothing of it is still in flight)
+    hipStream_t sin = ctx->hs_in, srun = ctx->hs_run, sout = ctx->hs_out;
+    RG_HIP(hipMemcpyAsync(s.d_desc.p, hd, m * sizeof(rg_pkt_desc), hipMemcpyHostToDevice, sin), "H2D desc");
+    if (span) RG_HIP(hipMemcpyAsync(s.d_buf.p, buf + lo, span, hipMemcpyHostToDevice, sin), "H2D frames");
     uint8_t *dbuf = static_cast<uint8_t *>(s.d_buf.p);
     if (!open) {
         RG_HIP(s.d_ctr.reserve(m * 8), "alloc ctr");
         RG_HIP(s.h_ctr.reserve(m * 8), "alloc h_ctr");
         memcpy(s.h_ctr.p, counters + i, m * 8);
-        RG_HIP(hipMemcpyAsync(s.d_ctr.p, s.h_ctr.p, m * 8, hipMemcpyHostToDevice, st), "H2D ctr");
+        RG_HIP(hipMemcpyAsync(s.d_ctr.p, s.h_ctr.p, m * 8, hipMemcpyHostToDevice, sin), "H2D ctr");
+    } else {
+        RG_HIP(s.d_ctr_out.reserve(m * 8), "alloc ctr_out");
+        RG_HIP(s.h_ctr_out.reserve(m * 8), "alloc h_ctr_out");
+    }
+    RG_HIP(hipEventRecord(s.ev_in, sin), "slice event");
+    // the kernel on hs_run, once the inputs are in
+    RG_HIP(hipStreamWaitEvent(srun, s.ev_in, 0), "slice wait");
+    if (!open) {
         rg::SealArgs a{};
         a.keys = static_cast<const uint32_t *>(ctx->d_keys.p);
         a.receivers = with_receivers ? static_cast<const uint32_t *>(ctx->d_recv.p) : nullptr;
@@ -769,10 +800,8 @@ int HostRun::step() {
         a.status = static_cast<uint8_t *>(s.d_status.p);
         a.nkeys = nkeys;
         a.n = (uint32_t)m;
-        RG_HIP(launch_seal_any(ctx, a, s.plan, st), "seal launch");
+        RG_HIP(launch_seal_any(ctx, a, s.plan, srun), "seal launch");
     } else {
-        RG_HIP(s.d_ctr_out.reserve(m * 8), "alloc ctr_out");
-        RG_HIP(s.h_ctr_out.reserve(m * 8), "alloc h_ctr_out");
         rg::OpenArgs a{};
         a.keys = static_cast<const uint32_t *>(ctx->d_keys.p);
         a.desc = static_cast<const rg_pkt_desc *>(s.d_desc.p);
@@ -782,16 +811,20 @@ int HostRun::step() {
         a.counters_out = static_cast<uint64_t *>(s.d_ctr_out.p);
         a.nkeys = nkeys;
         a.n = (uint32_t)m;
-        RG_HIP(launch_open_any(ctx, a, s.plan, st), "open launch");
-        RG_HIP(hipMemcpyAsync(s.h_ctr_out.p, s.d_ctr_out.p, m * 8, hipMemcpyDeviceToHost, st), "D2H ctr");
+        RG_HIP(launch_open_any(ctx, a, s.plan, srun), "open launch");
     }
-    if (span) RG_HIP(hipMemcpyAsync(buf + lo, s.d_buf.p, span, hipMemcpyDeviceToHost, st), "D2H frames");
-    RG_HIP(hipMemcpyAsync(s.h_status.p, s.d_status.p, m, hipMemcpyDeviceToHost, st), "D2H status");
+    RG_HIP(hipEventRecord(s.ev_run, srun), "slice event");
+    // downloads on hs_out, once the kernel is done
+    RG_HIP(hipStreamWaitEvent(sout, s.ev_run, 0), "slice wait");
+    if (span) RG_HIP(hipMemcpyAsync(buf + lo, s.d_buf.p, span, hipMemcpyDeviceToHost, sout), "D2H frames");
+    if (open) RG_HIP(hipMemcpyAsync(s.h_ctr_out.p, s.d_ctr_out.p, m * 8, hipMemcpyDeviceToHost, sout), "D2H ctr");
+    RG_HIP(hipMemcpyAsync(s.h_status.p, s.d_status.p, m, hipMemcpyDeviceToHost, sout), "D2H status");
+    RG_HIP(hipEventRecord(s.ev_out, sout), "slice event");
     s.i0 = i;
     s.i1 = j;
     s.busy = true;
     i = j;
-    which = (which + 1) % 3;
+    which = (which + 1) % rg_ctx::kHostSlots;
     return RG_OK;
 }
 
@@ -1129,14 +1162,14 @@ static int general_one(rg_ctx *ctx, bool dec, const uint8_t key[32], const uint8
             (void)hipStreamSynchronize(st);
             memset(h, 0, n);
         }
-    } wipe{h, d, job_bytes, ctx->slots[0].stream};
+    } wipe{h, d, job_bytes, ctx->gen_stream};
     memset(&job.key, 0, sizeof job.key); // the stack copy
     uint8_t *hb = h + job_bytes; // arena base as the kernel sees it; padding zeroed (pad16)
     memset(hb, 0, tag_off + 16);
     if (aad_len) memcpy(hb + aad_off, aad, aad_len);
     if (len) memcpy(hb + pay_off, payload, len);
     if (dec) memcpy(hb + tag_off, tag, 16);
-    hipStream_t st = ctx->slots[0].stream;
+    hipStream_t st = ctx->gen_stream;
     RG_HIP(hipMemcpyAsync(d, h, arena, hipMemcpyHostToDevice, st), "H2D arena");
     RG_HIP(rg::launch_general(reinterpret_cast<rg::GeneralJob *>(d), 1, d + job_bytes, st), "general launch");
     RG_HIP(hipMemcpyAsync(h, d, arena, hipMemcpyDeviceToHost, st), "D2H arena");

@@ -566,33 +566,23 @@ __device__ __forceinline__ void dma16(const v4i &rsrc, uint32_t voff, uint32_t l
                  : "memory");
 }
 
-// Write-through (sc1) frame stores, off: a plain store leaves its line dirty in the XCD's L2 and the
+// Frame stores stay plain (write-back): a plain store leaves its line dirty in the XCD's L2 and the
 // end-of-kernel release writes the dirty lines back after the last wave (tools/tailbench.hip,
 // profiles/r3_tailbench.json: +2.2 us of tail at ~100 MB of coalesced stores per launch, none with sc1),
-// but in the AEAD kernels sc1 measured no faster on configs 2, 4 and 5 and 4 % slower on config 3, whose
-// 16-byte stores at a 16-byte phase then reach memory piece by piece (profiles/r3_sc1_ab.txt).
-#ifndef RG_STORE_SC1
-#define RG_STORE_SC1 0
-#endif
+// but in the AEAD kernels write-through (sc1) stores measured no faster on configs 2, 4 and 5 and 4 %
+// slower on config 3, whose 16-byte stores at a 16-byte phase then reach memory piece by piece
+// (round 3, profiles/r3_sc1_ab.txt).
 __device__ __forceinline__ void store16(const v4i &rsrc, uint32_t voff, const uint4 &v) {
     v4u d;
     d.x = v.x;
     d.y = v.y;
     d.z = v.z;
     d.w = v.w;
-#if RG_STORE_SC1
-    asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen sc1\n\t"
-                 "s_nop 1"
-                 :
-                 : "v"(d), "v"(voff), "s"(rsrc)
-                 : "memory");
-#else
     asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen\n\t"
                  "s_nop 1"
                  :
                  : "v"(d), "v"(voff), "s"(rsrc)
                  : "memory");
-#endif
 }
 
 template <int N> __device__ __forceinline__ void wait_vm() {

@@ -53,7 +53,6 @@ __device__ __forceinline__ uint64_t fdiv(uint64_t a, uint64_t b) {
 // hardware drops (no sink traffic; config 3 +1 %, profiles/r3_sc1_ab.txt).  Larger arenas store
 // through 64-bit pointers, the non-payload stores into a per-lane sink.
 constexpr uint32_t kDrop = 0x80000000u;    // past num_records: dropped by the range check
-constexpr int kFlatAux = RG_STORE_SC1 ? 16 : 0;
 struct FStore {
     uint8_t *buf;
     __amdgpu_buffer_rsrc_t rs;
@@ -63,7 +62,7 @@ template <bool WIN> __device__ __forceinline__ void fstore(const FStore &S, cons
                                                           const uint4 &v) {
     if constexpr (WIN) {
         const uint32_t off = keep ? (uint32_t)(reinterpret_cast<const uint8_t *>(p) - S.buf) : kDrop;
-        __builtin_amdgcn_raw_buffer_store_b128(v4u{v.x, v.y, v.z, v.w}, S.rs, (int)off, 0, kFlatAux);
+        __builtin_amdgcn_raw_buffer_store_b128(v4u{v.x, v.y, v.z, v.w}, S.rs, (int)off, 0, 0);
     } else {
         *const_cast<uint4 *>(keep ? p : S.junk + j) = v;
     }
@@ -81,78 +80,45 @@ __device__ __forceinline__ uint32_t flat_work(const rg_pkt_desc &d, bool open) {
 // -------------------------------------------------------------- LDS image
 // One per wave, one record set per packet of the sub-unit, laid out so that a
 // lane moving on to the next packet issues all its LDS reads at once.
-#ifndef RG_FLAT_MAX_PK
-#define RG_FLAT_MAX_PK 128 // packets per sub-unit (phase A holds their key loads in registers)
-#endif
-constexpr uint32_t kFlatMaxPk = RG_FLAT_MAX_PK;
-#ifndef RG_FLAT_KR
-#define RG_FLAT_KR 16 // key-record stride in dwords (20: lanes reading consecutive packets' rows hit distinct banks)
-#endif
+constexpr uint32_t kFlatMaxPk = 128; // packets per sub-unit (phase A holds their key loads in registers; 64 measured 15 % slower)
 struct FlatLds {
     uint4 rec[kFlatMaxPk + 1];    // {offset lo, offset hi, nb | kLiveBit, cs}; rec[m].w = D
-    uint32_t kr[kFlatMaxPk][RG_FLAT_KR]; // key[8], counter lo/hi, r[4] (unclamped), desc len, desc key_idx
+    // key[8], counter lo/hi, r[4] (unclamped), desc len, desc key_idx (a 20-dword stride halves the LDS bank
+    // conflicts of phase C's key reads and changes no time: round 3, profiles/r3_lds_counters.txt)
+    uint32_t kr[kFlatMaxPk][16];
     uint32_t sw[kFlatMaxPk][4];   // seal: s; open: tag - s (mod 2^128)
-    uint32_t hs[kFlatMaxPk][8];   // [6] kFail (open: the tag did not verify)
+    uint32_t fail[kFlatMaxPk];    // kFail: the tag did not verify (open)
     unsigned long long ps[kFlatMaxPk][5]; // sum of the packet's Horner pieces, radix 2^32 limbs (LDS atomics)
     uint32_t ck[64];              // scratch: the lanes' first-packet markers
     uint32_t ch[64][5];           // scratch: the lanes' last-packet markers (stride 5)
 };
 constexpr uint32_t kLiveBit = 0x80000000u, kFail = 2u;
 // workgroup-cooperative unit search (round 3): groups of kCoopGroup packets, work of a packet
-// RG_FLAT_WPKT + RG_FLAT_WCHK x chunks (a key block costs less than its share of the lanes' chunk steps:
+// kCoopWPkt + kCoopWChk x chunks (a key block costs less than its share of the lanes' chunk steps:
 // see flat_coop_ok and DESIGN.md §4.6)
-#ifndef RG_FLAT_COOP
-#define RG_FLAT_COOP 1
-#endif
-#ifndef RG_FLAT_WPKT
-#define RG_FLAT_WPKT 1
-#endif
-#ifndef RG_FLAT_WCHK
-#define RG_FLAT_WCHK 8
-#endif
 constexpr uint32_t kCoopGroup = 4096;
+constexpr uint32_t kCoopWPkt = 1, kCoopWChk = 8;
+// the coop search sums work in 32 bits and doubles it for the midpoint targets
+static_assert(kCoopGroup * (kCoopWPkt + kCoopWChk * (kMaxPayload / 64ull + 1)) * 2 < (1ull << 32),
+              "coop work sums overflow 32 bits");
 constexpr uint32_t kCoopLds = 256; // shared slots: wave totals, cut counts
-#ifndef RG_FLAT_WAVES
-#define RG_FLAT_WAVES 4 // waves per workgroup, one workgroup per CU: one wave per SIMD
-#endif
-constexpr uint32_t kFlatWaves = RG_FLAT_WAVES;
-#ifndef RG_FLAT_WG_PER_CU
-#define RG_FLAT_WG_PER_CU 1 // resident workgroups per CU (2: two waves per SIMD)
-#endif
-constexpr uint32_t kFlatWgPerCu = RG_FLAT_WG_PER_CU;
-static_assert(kFlatWgPerCu * (kFlatWaves * sizeof(FlatLds) + 256) <= kLdsPerCu, "flat LDS images per CU");
+constexpr uint32_t kFlatWaves = 4; // waves per workgroup (the coop search's four quarters), one per SIMD
 static_assert(kFlatWaves * sizeof(FlatLds) + 256 <= kLdsPerCu, "flat LDS image");
 
-#ifndef RG_FLAT_NTLOAD
-#define RG_FLAT_NTLOAD 0
-#endif
-#ifndef RG_FLAT_ALIGN
-#define RG_FLAT_ALIGN 0
-#endif
 
 struct FChunk {
     uint4 q0, q1, q2, q3;
 };
 
 // chunk t of a packet whose last 16-byte block is `last`: four loads, indices
-// clamped inside the payload (always readable)
+// clamped inside the payload (always readable).  (Streaming `nt` loads cut the
+// written bytes 23 % but re-read 19 % more and ran 10 % slower: round 3.)
 __device__ __forceinline__ void fload(FChunk &c, const uint4 *pl, uint32_t t, uint32_t last) {
     const uint32_t b = 4 * t;
-#ifdef RG_FLAT_ABL_NOLOAD // diagnostics only: no payload loads (output invalid)
-    c.q0.x ^= b; c.q1.y ^= b; c.q2.z ^= b; c.q3.w ^= last; return;
-#endif
-#if RG_FLAT_NTLOAD // streaming loads: the payload is read once, so its lines go first in L2
-    auto nt = [&](uint32_t i) {
-        const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(pl + min(i, last)));
-        return make_uint4(v.x, v.y, v.z, v.w);
-    };
-    c.q0 = nt(b + 0); c.q1 = nt(b + 1); c.q2 = nt(b + 2); c.q3 = nt(b + 3);
-#else
     c.q0 = pl[min(b + 0, last)];
     c.q1 = pl[min(b + 1, last)];
     c.q2 = pl[min(b + 2, last)];
     c.q3 = pl[min(b + 3, last)];
-#endif
 }
 
 // a lane's position in the sub-unit's chunk stream
@@ -223,11 +189,6 @@ struct FLane {
     uint32_t pe;
     int pb;
     uint32_t rn[4]; // seal: r of the compute cursor's packet, kept from its key read for the pk switch
-#if RG_FLAT_ALIGN
-    uint4 d1, d2, d3;  // pieces 1..3 of the previous chunk waiting for their segment's other part
-    const uint4 *dd;   // where that chunk goes
-    uint32_t dm;       // which of them wait (bits 1..3)
-#endif
 };
 
 // one square-and-multiply step of the carry power (pb is wave-uniform)
@@ -266,9 +227,6 @@ __device__ __forceinline__ void flat_step(FLane &s, FChunk &b, uint32_t j, FlatL
     if (active && s.cur.live) cnt = min(4u, s.cur.nb - 4 * s.cur.t);
     uint32_t ks[16];
     stream_block_hooked(s.st, s.cur.t + 1, ks, [&](int dr) {
-#ifdef RG_FLAT_ABL_NOPOLY // diagnostics only: no Poly1305 absorption (output invalid)
-        if (dr < 100) return;
-#endif
         if constexpr (OPEN) {
             if (dr == 1) acc_block_pred(s.h, b.q0, s.r, cnt > 0);
             if (dr == 3) acc_block_pred(s.h, b.q1, s.r, cnt > 1);
@@ -281,45 +239,15 @@ __device__ __forceinline__ void flat_step(FLane &s, FChunk &b, uint32_t j, FlatL
             if (dr == 7) acc_block_pred(s.h, s.pi.q3, s.r, s.pi_cnt > 3);
         }
         if (dr % 2 == 1) pin_acc(s.h);
-#ifdef RG_FLAT_POW_HOOK
-        if (dr == 2 || dr == 6) {
-            pow_step(s);
-            pin_acc(s.px);
-        }
-#endif
     });
     const FChunk x = {xor4(b.q0, ks + 0), xor4(b.q1, ks + 4), xor4(b.q2, ks + 8), xor4(b.q3, ks + 12)};
     uint4 *dst = const_cast<uint4 *>(s.cur.pl) + 4 * s.cur.t;
-#ifdef RG_FLAT_ABL_NOSTORE // diagnostics only: ciphertext not stored (output invalid)
-    if (s.cur.k == 0xFFFFFFFFu)
-#endif
-    {
-#if RG_FLAT_ALIGN
-        // 64-byte segments whole within one step: a chunk at 16-byte phase ph straddles two segments, so
-        // its pieces 4 - ph .. 3 wait for the next chunk's step and are stored just before its first
-        // pieces (a packet's last chunk and the lane's last step store everything).  Stores one step
-        // apart into the same segment leave it partially written in L2, where the payload reads evict it
-        // (written back twice: profiles/r3_cfg3_traffic_attribution.txt).
-        const uint32_t ph = (uint32_t)(reinterpret_cast<uintptr_t>(dst) >> 4) & 3u;
-        const bool fin = s.cur.t + 1 == s.cur.c || j + 1 == s.nsteps;
-        const uint32_t head = fin ? 4u : 4u - ph; // pieces stored now (ph = 0: all)
-        fstore<WIN>(FS, s.dd + 1, (s.dm & 2u) != 0, 1, s.d1);
-        fstore<WIN>(FS, s.dd + 2, (s.dm & 4u) != 0, 2, s.d2);
-        fstore<WIN>(FS, s.dd + 3, (s.dm & 8u) != 0, 3, s.d3);
-        fstore<WIN>(FS, dst + 0, cnt > 0, 0, x.q0);
-        fstore<WIN>(FS, dst + 1, cnt > 1 && head > 1, 1, x.q1);
-        fstore<WIN>(FS, dst + 2, cnt > 2 && head > 2, 2, x.q2);
-        fstore<WIN>(FS, dst + 3, cnt > 3 && head > 3, 3, x.q3);
-        s.dm = (cnt > 1 && head <= 1 ? 2u : 0u) | (cnt > 2 && head <= 2 ? 4u : 0u) | (cnt > 3 && head <= 3 ? 8u : 0u);
-        s.dd = dst;
-        s.d1 = x.q1; s.d2 = x.q2; s.d3 = x.q3;
-#else
-        fstore<WIN>(FS, dst + 0, cnt > 0, 0, x.q0);
-        fstore<WIN>(FS, dst + 1, cnt > 1, 1, x.q1);
-        fstore<WIN>(FS, dst + 2, cnt > 2, 2, x.q2);
-        fstore<WIN>(FS, dst + 3, cnt > 3, 3, x.q3);
-#endif
-    }
+    // (segment-whole stores -- a chunk's pieces past its 64-byte seam held one step -- cut the written bytes
+    // 16 % and ran 1.3 % slower: round 3, profiles/r3_cfg3_traffic_attribution.txt)
+    fstore<WIN>(FS, dst + 0, cnt > 0, 0, x.q0);
+    fstore<WIN>(FS, dst + 1, cnt > 1, 1, x.q1);
+    fstore<WIN>(FS, dst + 2, cnt > 2, 2, x.q2);
+    fstore<WIN>(FS, dst + 3, cnt > 3, 3, x.q3);
     if constexpr (OPEN) {
         if (active && s.cur.t + 1 == s.cur.c) { // the packet's last chunk: its final piece
             if (s.cur.live) add_h(L, s.cur.k, s.h);
@@ -342,9 +270,6 @@ __device__ __forceinline__ void flat_step(FLane &s, FChunk &b, uint32_t j, FlatL
     }
     fload(b, s.f.pl, s.f.t, s.f.nb ? s.f.nb - 1 : 0);
     if (active && fcur_next(s.cur, L, buf, m) && s.cur.k < m) {
-#ifdef RG_FLAT_ABL_NOSWITCH // diagnostics only: the stream is not re-keyed at a packet switch (output invalid)
-        if (s.cur.k != 0xFFFFFFFFu) return;
-#endif
         const FKey q = fkey(L, s.cur.k);
         s.st = make_stream(q.key, 0u, q.n1, q.n2);
         if constexpr (OPEN) s.r = make_mul(q.r[0], q.r[1], q.r[2], q.r[3]);
@@ -381,9 +306,6 @@ __device__ __forceinline__ Acc flat_pow_mul(Acc h, const Mul &r, uint32_t e) {
 // One ChaCha20 block on a lane quad: lane j holds column j (rows a, b, c, d = state words j, 4 + j,
 // 8 + j, 12 + j); the diagonal rounds rotate rows b, c, d across the quad with DPP quad_perm.  Only
 // the one-time key is wanted: r_j = keystream word j, s_j = word 4 + j (RFC 8439 §2.6).
-#ifndef RG_FLAT_QUAD
-#define RG_FLAT_QUAD 1
-#endif
 template <int CTRL> __device__ __forceinline__ uint32_t quad_perm(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
 }
@@ -477,7 +399,8 @@ template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) voi
     FS.buf = buf;
     FS.rs = __builtin_amdgcn_make_buffer_rsrc(buf, (short)0, 0x7FFFFFFF, 0x00020000);
     FS.junk = WIN ? nullptr : A.junk + ((uint64_t)wid * 64 + lane) * 4;
-    // diagnostics (debug mode 3): per wave, s_memtime at the end of each phase of its first sub-unit
+#if RG_DIAG
+    // diagnostic builds (debug mode 3): per wave, s_memtime at the end of each phase of its first sub-unit
     uint64_t *const dbg = OPEN ? A.oa.dbg : A.sa.dbg;
     uint64_t mk[8] = {__builtin_amdgcn_s_memtime(), 0, 0, 0, 0, 0, 0, 0};
     const uint64_t rt0 = dbg ? __builtin_amdgcn_s_memrealtime() : 0; // 100 MHz wall clock (wave start / end)
@@ -485,13 +408,12 @@ template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) voi
     do {                                                                    \
         if (dbg && mk[slot] == 0) mk[slot] = __builtin_amdgcn_s_memtime(); \
     } while (0)
-#ifdef RG_FLAT_START_MARK
-    if (dbg && lane == 0) dbg[8ull * wid + 6] = 0xABCD0000ull + wv;
+#else
+#define RG_FLAT_MARK(slot) \
+    do {                   \
+    } while (0)
 #endif
     const uint32_t NU = A.units;
-#ifdef RG_FLAT_PRO_STAMPS2
-    if (dbg && mk[6] == 0) mk[6] = __builtin_amdgcn_s_memtime() + (NU == 0xFFFFFFFFu) + (n == 0xFFFFFFFFu);
-#endif
     for (uint32_t u = wid; u < NU; u += nw) {
         // ---- this unit's packets [s, e) and, when it is read from a group, its first sub-unit staged
         uint32_t s0, e0, staged = 0;
@@ -608,9 +530,6 @@ template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) voi
             }
             const uint32_t kg = f1 - f0, j = u - f0;
             const uint32_t gb = g * kFlatGroup, gn = min(kFlatGroup, n - gb);
-#ifdef RG_FLAT_PRO_STAMPS2
-            if (dbg && mk[4] == 0) mk[4] = __builtin_amdgcn_s_memtime();
-#endif
             // coalesced: lane l holds packets l + 64 q of the group (q = 0..15)
             rg_pkt_desc d[16];
 #pragma unroll
@@ -618,14 +537,6 @@ template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) voi
                 const uint32_t i = lane + 64 * q;
                 d[q] = desc[gb + (i < gn ? i : 0)];
             }
-#ifdef RG_FLAT_PRO_STAMPS2
-            {
-                uint32_t acc = 0;
-#pragma unroll
-                for (int q = 0; q < 16; ++q) acc ^= d[q].len; // forces every load to land
-                if (dbg && mk[5] == 0) mk[5] = __builtin_amdgcn_s_memtime() + (acc == 0x7FFFFFFFu);
-            }
-#endif
             // The work prefix in packet order, lane-contiguous: the per-packet work goes through LDS
             // (the key-record area, written only later) from the coalesced order (lane + 64 q) to
             // lane l holding packets 16 l .. 16 l + 15; each lane sums its 16 serially and one DPP
@@ -655,9 +566,6 @@ template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) voi
 #pragma unroll
             for (int q = 0; q < 16; ++q) e[q] += lx; // E_i, inclusive, of packet 16 lane + q
             const uint32_t total = lane63(lx + lsum);
-#ifdef RG_FLAT_PRO_STAMPS
-            if (dbg && mk[2] == 0) mk[2] = __builtin_amdgcn_s_memtime();
-#endif
             // targets j total / kg and (j + 1) total / kg without a 64-bit division
             const uint32_t t2[2] = {uniform_u32(2 * (uint32_t)fdiv((uint64_t)total * j, kg)),
                                     uniform_u32(2 * (uint32_t)fdiv((uint64_t)total * (j + 1), kg))};
@@ -679,9 +587,6 @@ template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) voi
             uint32_t cut[2] = {lane63(wave_scan_incl(c0)), lane63(wave_scan_incl(c1))};
             if (j == 0) cut[0] = 0;
             if (j + 1 == kg) cut[1] = gn;
-#ifdef RG_FLAT_PRO_STAMPS
-            if (dbg && mk[3] == 0) mk[3] = __builtin_amdgcn_s_memtime();
-#endif
             s0 = gb + cut[0];
             e0 = gb + cut[1];
             // stage the first sub-unit straight from the registers
@@ -828,7 +733,7 @@ template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) voi
             // ---- phase A: checks, one-time-key blocks, header (seal), counters_out (open)
             // Packets 64.. of a sub-unit of 65-96 get their key blocks from lane quads (16 blocks per
             // pass at ~0.36 of a full pass) instead of a second one-lane-per-packet pass.
-            const bool quad = RG_FLAT_QUAD && m > 64 && m <= 96; // wave-uniform
+            const bool quad = m > 64 && m <= 96; // wave-uniform
 #pragma unroll
             for (uint32_t q = 0; q < kFlatMaxPk / 64; ++q) {
                 const uint32_t k = lane + 64 * q;
@@ -882,7 +787,7 @@ template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) voi
                 {
                     unsigned long long *z = L.ps[k];
                     z[0] = z[1] = z[2] = z[3] = z[4] = 0ull;
-                    L.hs[k][6] = 0u;
+                    L.fail[k] = 0u;
                 }
                 if (st == 0xFF) {
                     L.rec[k].z |= kLiveBit;
@@ -941,11 +846,6 @@ template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) voi
             s.pi = FChunk{};
             s.pi_cnt = 0;
             s.pk = s.cur.k;
-#if RG_FLAT_ALIGN
-            s.d1 = s.d2 = s.d3 = make_uint4(0, 0, 0, 0);
-            s.dd = s.cur.pl;
-            s.dm = 0;
-#endif
             // the carry's power: the packet of the lane's last chunk, when it goes on past the lane
             {
                 s.pe = 0;
@@ -1044,7 +944,7 @@ template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) voi
                     const uint32_t diff = (tag[0] ^ swk.x) | (tag[1] ^ swk.y) | (tag[2] ^ swk.z) | (tag[3] ^ swk.w);
                     status[i] = diff == 0 ? RG_PKT_OK : RG_PKT_DECRYPT_ERR;
                     if (diff != 0) {
-                        L.hs[k][6] = kFail;
+                        L.fail[k] = kFail;
                         any_fail = true;
                     }
                 }
@@ -1062,7 +962,7 @@ template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) voi
 #pragma unroll
                     for (uint32_t q = 0; q < kFlatMaxPk / 64; ++q) {
                         const uint32_t k = lane + 64 * q;
-                        const bool f = k < m && L.hs[k][6] == kFail;
+                        const bool f = k < m && L.fail[k] == kFail;
                         cn[q] = f ? ((L.rec[k].z & ~kLiveBit) + 3) >> 2 : 0u;
                         fmask[q] = __ballot(f && cn[q] > 0);
                     }
@@ -1114,6 +1014,7 @@ template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) voi
             wave_sync(); // the next sub-unit overwrites the LDS image
         }
     }
+#if RG_DIAG
     if (dbg) {
         mk[7] = __builtin_amdgcn_s_memtime();
         const uint64_t rt1 = __builtin_amdgcn_s_memrealtime();
@@ -1123,6 +1024,7 @@ template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) voi
             dbg[8ull * (nw + wid) + 1] = rt1;
         }
     }
+#endif
 #undef RG_FLAT_MARK
 }
 
@@ -1130,7 +1032,7 @@ template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) voi
 // kCoopGroup packets: n a multiple of kCoopGroup and units x kCoopGroup / n a multiple of four.
 // Returns the units per group (0: the one-wave search).
 static uint32_t flat_coop_ok(uint32_t n, uint32_t units, bool balance) {
-    if (!RG_FLAT_COOP || !balance || kFlatWaves != 4 || n < kCoopGroup || n % kCoopGroup != 0) return 0;
+    if (!balance || n < kCoopGroup || n % kCoopGroup != 0) return 0;
     const uint64_t x = (uint64_t)units * kCoopGroup;
     if (x % n != 0) return 0;
     const uint64_t kgc = x / n;
@@ -1143,13 +1045,14 @@ hipError_t launch_flat(const SealArgs *sa, const OpenArgs *oa, bool balance, uin
     FlatArgs A{};
     if (sa) A.sa = *sa;
     if (oa) A.oa = *oa;
-    const uint32_t blocks = (uint32_t)(cus > 0 ? cus : 1) * kFlatWgPerCu;
+    // one workgroup per CU (two, at two waves per SIMD, measured 5-8 % slower: profiles/r4_cfg3_twowave_ab.txt)
+    const uint32_t blocks = (uint32_t)(cus > 0 ? cus : 1);
     A.units = blocks * kFlatWaves;
     A.junk = junk;
     A.balance = balance ? 1u : 0u;
     A.coop = flat_coop_ok(n, A.units, balance);
-    A.wpkt = RG_FLAT_WPKT;
-    A.wchk = RG_FLAT_WCHK;
+    A.wpkt = kCoopWPkt;
+    A.wchk = kCoopWChk;
     const uint32_t lds = kFlatWaves * (uint32_t)sizeof(FlatLds) + kCoopLds;
     const bool win = (sa ? sa->buf_len : oa->buf_len) < 0x7FFFFFF0ull; // frame offsets below 2 GiB
     if (sa && win) hipLaunchKernelGGL((flat_kernel<false, true>), dim3(blocks), dim3(64 * kFlatWaves), lds, s, A);
@@ -1159,7 +1062,7 @@ hipError_t launch_flat(const SealArgs *sa, const OpenArgs *oa, bool balance, uin
     return hipGetLastError();
 }
 
-uint32_t flat_junk_bytes(int cus) { return (uint32_t)(cus > 0 ? cus : 1) * kFlatWgPerCu * kFlatWaves * 64 * 64; }
+uint32_t flat_junk_bytes(int cus) { return (uint32_t)(cus > 0 ? cus : 1) * kFlatWaves * 64 * 64; }
 
 hipError_t prepare_flat_kernels() {
     const int lds = (int)(kFlatWaves * sizeof(FlatLds) + kCoopLds);

@@ -46,10 +46,7 @@ __device__ __forceinline__ uint32_t class_of(uint32_t chunks) {
 // class one ballot -> one LDS atomic (runs of consecutive packets stay
 // together), then one global atomic per class and workgroup.  Uniform batches
 // therefore keep tiles of 64 consecutive frames.
-#ifndef RG_PLAN_PER
-#define RG_PLAN_PER 2 // 1, 8 and 16 measured slower at config 3 (round r1e)
-#endif
-constexpr uint32_t kPlanPer = RG_PLAN_PER;
+constexpr uint32_t kPlanPer = 2; // 1, 8 and 16 measured slower at config 3 (round r1e)
 
 __global__ __launch_bounds__(256) void plan_kernel(const rg_pkt_desc *desc, uint32_t n, uint32_t open,
                                                    uint32_t *counts, uint32_t *lists, uint32_t cap, uint32_t *sched,
@@ -161,18 +158,7 @@ __device__ __forceinline__ uint64_t realtime() { // 100 MHz constant clock
 }
 
 constexpr uint32_t kMinSegment = 4;
-#ifndef RG_TILE_DYN
-#define RG_TILE_DYN 1
-#endif
-#ifndef RG_TILE_POOL
-#define RG_TILE_POOL 1
-#endif
-#ifndef RG_TILE_POOL_MIN
-#define RG_TILE_POOL_MIN 8 // deal rounds from which the grid-wide pool is used (the measured regime)
-#endif
-#ifndef RG_TILE_POOL_AHEAD
-#define RG_TILE_POOL_AHEAD 1 // pool items requested one tile ahead
-#endif
+constexpr uint32_t kPoolMinRounds = 8; // deal rounds from which the grid-wide pool is used (the measured regime)
 
 __device__ __forceinline__ uint32_t pow2ceil(uint32_t x) { return x <= 1 ? 1u : 1u << (32 - __clz(x - 1)); }
 
@@ -281,14 +267,14 @@ __global__ __launch_bounds__(512) void tile_kernel(SealArgs sa, OpenArgs oa, Til
     const uint32_t S = halves * gridDim.x;
     const uint32_t my_slot = half == 0 ? blockIdx.x : S - 1 - blockIdx.x;
     const uint32_t rounds = (sc.total_groups + S - 1) / S;
-    const bool dyn = RG_TILE_DYN && halves == 2 && __ballot(sc.K > 1) == 0; // same in every wave
+    const bool dyn = halves == 2 && __ballot(sc.K > 1) == 0; // same in every wave
     // From eight deal rounds on, the last eighth of them goes to a pool shared by the whole
     // grid: the XCDs do not run at one rate (per-CU finish times at config 4 spread by 8 %, by XCD), so
     // the workgroups that run out of their own tiles first take these, one tile per device-scope atomic
     // on tp.gq[0], requested one tile ahead.  Measured: config 5 on one GPU (64 rounds) +1.5 %, config 4
     // (8 rounds) +0.7 % (with each draw waited for on the spot, config 4 lost 1 %).  Below eight rounds
     // (unmeasured: one pooled round would be half or a third of the tiles) every tile stays local.
-    const uint32_t R = (RG_TILE_POOL && dyn && tp.gq && rounds >= RG_TILE_POOL_MIN) ? max(1u, rounds / 8) : 0u;
+    const uint32_t R = (dyn && tp.gq && rounds >= kPoolMinRounds) ? max(1u, rounds / 8) : 0u;
     const uint32_t rounds_local = rounds - R;
     const uint32_t pool = R ? (sc.total_groups - rounds_local * S) * 4u : 0u; // tiles in the global pool
     bool pooled = false, gq_pending = false;
@@ -318,10 +304,10 @@ __global__ __launch_bounds__(512) void tile_kernel(SealArgs sa, OpenArgs oa, Til
             const uint32_t item = uniform_u32(__shfl((int)gq_next, 0));
             gq_pending = false;
             if (item >= pool) break;
-            if (RG_TILE_POOL_AHEAD && lane == 0) {
+            if (lane == 0) { // requested one tile ahead (waiting for each draw on the spot: config 4 -1 %)
                 gq_next = __hip_atomic_fetch_add(tp.gq, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
-            gq_pending = RG_TILE_POOL_AHEAD != 0;
+            gq_pending = true;
             g = rounds_local * S + (item >> 2);
             thw = item & 3u;
         } else {
