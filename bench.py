@@ -899,7 +899,13 @@ def main():
         # the same split driven by ONE process and ONE thread over every GPU (rg_group), beside the
         # one-process-per-GPU value above; the other ranks wait on a CPU barrier meanwhile
         devs = [0] * world if share else list(range(world))
-        out["single_process"] = single_process_run(devs, max(3, min(args.steps, 10)), 2, args.verify)
+        if not share and torch.cuda.device_count() < world:
+            out["single_process"] = {"skipped": f"rank 0 sees {torch.cuda.device_count()} GPU(s), not {world}"}
+        else:
+            try:
+                out["single_process"] = single_process_run(devs, max(3, min(args.steps, 10)), 2, args.verify)
+            except Exception as e:  # an extra leg: never lose the timed line for it
+                out["single_process"] = {"error": f"{type(e).__name__}: {e}"}
     if "cpu_baseline" in legs:
         port, ossl = cpu_baselines(w, args.cpu_seconds, all_core_threads(args.cpu_threads))
         out["cpu_baseline"] = port
@@ -917,31 +923,45 @@ def main():
 
 def pcie_ceiling(nbytes: int):
     """Pinned-host <-> device copy rates (torch pinned memory is hipHostMalloc): H2D alone, D2H alone and
-    both directions at once on two streams -- the ceiling the end-to-end path is measured against."""
+    both directions at once -- the ceiling the end-to-end path is measured against.  The copies are
+    hipMemcpyAsync calls on two of torch's (non-blocking) streams, as rg_{seal,open}_batch_host issue them
+    and as tools/pcie.hip measures (round 4: torch's own pinned copy_ on two streams ran the two
+    directions one after the other, 28 GB/s per direction, which round 3 took for the duplex ceiling)."""
+    import ctypes
+
     import torch
 
+    hip = ctypes.CDLL("libamdhip64.so.7")  # torch's HIP runtime (same soname: the loaded copy)
+    hip.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
+    hip.hipMemcpyAsync.restype = ctypes.c_int
     h_src = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
     h_dst = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
     d_a = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
     d_b = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
     s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
 
+    def copy(dst, src, kind, s):  # kind 1: host -> device, 2: device -> host
+        rc = hip.hipMemcpyAsync(ctypes.c_void_p(dst.data_ptr()), ctypes.c_void_p(src.data_ptr()), nbytes, kind,
+                                ctypes.c_void_p(s.cuda_stream))
+        if rc != 0:
+            raise RuntimeError(f"hipMemcpyAsync failed: {rc}")
+
     def timed(fn, reps=5):
         fn()
         torch.cuda.synchronize()
-        t0 = time.perf_counter()
+        t = []
         for _ in range(reps):
+            t0 = time.perf_counter()
             fn()
-        torch.cuda.synchronize()
-        return (time.perf_counter() - t0) / reps
+            torch.cuda.synchronize()
+            t.append(time.perf_counter() - t0)
+        return sorted(t)[reps // 2]
 
     def h2d():
-        with torch.cuda.stream(s1):
-            d_a.copy_(h_src, non_blocking=True)
+        copy(d_a, h_src, 1, s1)
 
     def d2h():
-        with torch.cuda.stream(s2):
-            h_dst.copy_(d_b, non_blocking=True)
+        copy(h_dst, d_b, 2, s2)
 
     def both():
         h2d()
@@ -949,7 +969,9 @@ def pcie_ceiling(nbytes: int):
 
     t_h2d, t_d2h, t_both = timed(h2d), timed(d2h), timed(both)
     return {"h2d_gb_s": round(nbytes / t_h2d / 1e9, 2), "d2h_gb_s": round(nbytes / t_d2h / 1e9, 2),
-            "bidir_gb_s_per_dir": round(nbytes / t_both / 1e9, 2), "bytes": nbytes}
+            "bidir_gb_s_per_dir": round(nbytes / t_both / 1e9, 2), "bytes": nbytes,
+            "how": "hipMemcpyAsync on two non-blocking streams, pinned buffers, median of 5 (tools/pcie.hip: "
+                   "profiles/r4_pcie.json)"}
 
 
 def e2e_host(eng, w, b):

@@ -207,10 +207,9 @@ struct rg_ctx {
     // the link's full rate while the other direction's copy of a neighbouring slice runs beside them
     // (round 4: with one stream per slice the three slices' H2D copies ran at once and shared the
     // link, then their D2H copies -- half duplex, 27 GB/s per direction against a 48 GB/s duplex
-    // ceiling; profiles/r4_e2e.txt).  Four slots: the host reuses a slot once its slice is back, and with
-    // three the upload of slice k + 1 waited for the download of slice k - 2, which ends with slice k's
-    // upload, plus the host's wake-up (~46 us per 16 MiB slice).
-    static constexpr int kHostSlots = 4;
+    // ceiling; profiles/r4_e2e_probe.txt).  Three slots: a fourth (so that the upload of slice k + 1 need
+    // not wait for the download of slice k - 2) measured the same at 16 MiB slices and slower at 8 MiB.
+    static constexpr int kHostSlots = 3;
     Slot slots[kHostSlots];
     hipStream_t hs_in = nullptr, hs_run = nullptr, hs_out = nullptr;
     hipStream_t gen_stream = nullptr; // the per-message drop-in

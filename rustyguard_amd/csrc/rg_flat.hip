@@ -86,6 +86,9 @@ struct FlatLds {
     // key[8], counter lo/hi, r[4] (unclamped), desc len, desc key_idx (a 20-dword stride halves the LDS bank
     // conflicts of phase C's key reads and changes no time: round 3, profiles/r3_lds_counters.txt)
     uint32_t kr[kFlatMaxPk][16];
+    // the stream's counter-independent first column round (Stream::c1..c3), made with the one-time key in
+    // phase A, so that a packet switch in phase C reads it instead of recomputing three quarter-rounds
+    uint32_t hq[kFlatMaxPk][12];
     uint32_t sw[kFlatMaxPk][4];   // seal: s; open: tag - s (mod 2^128)
     uint32_t fail[kFlatMaxPk];    // kFail: the tag did not verify (open)
     unsigned long long ps[kFlatMaxPk][5]; // sum of the packet's Horner pieces, radix 2^32 limbs (LDS atomics)
@@ -128,30 +131,27 @@ struct FCur {
     const uint4 *pl;
 };
 
-__device__ __forceinline__ void fcur_from(FCur &p, const uint4 &rc, uint8_t *buf, uint32_t k, uint32_t t) {
+// Every packet of the stream has at least one chunk: a packet without payload blocks (P = 0, or a
+// descriptor that failed its checks) holds one chunk step whose four blocks are not payload (no Horner
+// block, stores dropped) and whose loads read `safe`, so that the cursors never skip packets.
+__device__ __forceinline__ uint32_t flat_chunks(uint32_t nb) { return nb ? (nb + 3) >> 2 : 1u; }
+
+__device__ __forceinline__ void fcur_from(FCur &p, const uint4 &rc, uint8_t *buf, const uint4 *safe, uint32_t k,
+                                          uint32_t t) {
     p.k = k;
     p.t = t;
     p.nb = rc.z & ~kLiveBit;
     p.live = (rc.z & kLiveBit) != 0;
-    p.c = (p.nb + 3) >> 2;
-    p.pl = reinterpret_cast<const uint4 *>(buf + (((uint64_t)rc.y << 32) | rc.x) + 16);
+    p.c = flat_chunks(p.nb);
+    p.pl = p.nb ? reinterpret_cast<const uint4 *>(buf + (((uint64_t)rc.y << 32) | rc.x) + 16) : safe;
 }
 
-// next chunk; returns true when it starts a new packet (packets without chunks skipped)
-__device__ __forceinline__ bool fcur_next(FCur &p, const FlatLds &L, uint8_t *buf, uint32_t m) {
+// next chunk; returns true when it starts a new packet (one 16-byte LDS read)
+__device__ __forceinline__ bool fcur_next(FCur &p, const FlatLds &L, uint8_t *buf, const uint4 *safe, uint32_t m) {
     if (++p.t < p.c) return false;
-    uint32_t k = p.k + 1;
-    // one 16-byte LDS read on the common path (the next packet has chunks); packets without
-    // chunks (P = 0) are skipped by the rare loop
-    uint4 rc = L.rec[k < m ? k : m];
-    asm volatile("" ::"v"(rc.x), "v"(rc.y), "v"(rc.z)); // all fields now: one ds_read_b128
-    if (k < m && (rc.z & ~kLiveBit) == 0) {
-        do {
-            ++k;
-            rc = L.rec[k < m ? k : m];
-        } while (k < m && (rc.z & ~kLiveBit) == 0);
-    }
-    if (k < m) fcur_from(p, rc, buf, k, 0);
+    const uint32_t k = p.k + 1;
+    const uint4 rc = L.rec[k < m ? k : m];
+    if (k < m) fcur_from(p, rc, buf, safe, k, 0);
     else p.k = m; // past the sub-unit (keeps pl: loads stay readable)
     return true;
 }
@@ -171,6 +171,22 @@ __device__ __forceinline__ FKey fkey(const FlatLds &L, uint32_t k) {
     o.n2 = c.y;
     o.r[0] = c.z; o.r[1] = c.w; o.r[2] = d.x; o.r[3] = d.y;
     return o;
+}
+
+// packet k's stream (nonce 0 || counter) from its key row and the first column round phase A left in hq
+__device__ __forceinline__ Stream fstream(const FlatLds &L, uint32_t k, const FKey &q) {
+    const uint4 *p = reinterpret_cast<const uint4 *>(L.hq[k]);
+    const uint4 a = p[0], b = p[1], c = p[2];
+    Stream st;
+    st.key = q.key;
+    st.n0 = 0u;
+    st.n1 = q.n1;
+    st.n2 = q.n2;
+    st.x0p = 0x61707865u + q.key.k[0];
+    st.c1[0] = a.x; st.c1[1] = a.y; st.c1[2] = a.z; st.c1[3] = a.w;
+    st.c2[0] = b.x; st.c2[1] = b.y; st.c2[2] = b.z; st.c2[3] = b.w;
+    st.c3[0] = c.x; st.c3[1] = c.y; st.c3[2] = c.z; st.c3[3] = c.w;
+    return st;
 }
 
 // per-lane state of phase C
@@ -221,7 +237,7 @@ __device__ __forceinline__ void add_h(FlatLds &L, uint32_t k, const Acc &h) {
 // packet changes.  Afterwards chunk j + 3 is requested into b.
 template <bool OPEN, bool WIN>
 __device__ __forceinline__ void flat_step(FLane &s, FChunk &b, uint32_t j, FlatLds &L, uint8_t *buf, const FStore &FS,
-                                          uint32_t m, uint32_t lane) {
+                                          const uint4 *safe, uint32_t m) {
     const bool active = j < s.nsteps;
     uint32_t cnt = 0;
     if (active && s.cur.live) cnt = min(4u, s.cur.nb - 4 * s.cur.t);
@@ -266,12 +282,12 @@ __device__ __forceinline__ void flat_step(FLane &s, FChunk &b, uint32_t j, FlatL
     // request chunk j + 3 of the lane into b (the same chunk again past the range)
     if (s.fj + 1 < s.nsteps) {
         ++s.fj;
-        fcur_next(s.f, L, buf, m);
+        fcur_next(s.f, L, buf, safe, m);
     }
     fload(b, s.f.pl, s.f.t, s.f.nb ? s.f.nb - 1 : 0);
-    if (active && fcur_next(s.cur, L, buf, m) && s.cur.k < m) {
+    if (active && fcur_next(s.cur, L, buf, safe, m) && s.cur.k < m) {
         const FKey q = fkey(L, s.cur.k);
-        s.st = make_stream(q.key, 0u, q.n1, q.n2);
+        s.st = fstream(L, s.cur.k, q);
         if constexpr (OPEN) s.r = make_mul(q.r[0], q.r[1], q.r[2], q.r[3]);
         else {
             s.rn[0] = q.r[0]; s.rn[1] = q.r[1]; s.rn[2] = q.r[2]; s.rn[3] = q.r[3];
@@ -316,14 +332,16 @@ __device__ __forceinline__ void quad_qr(uint32_t &a, uint32_t &b, uint32_t &c, u
     a += b; d ^= a; d = rotl(d, 8);
     c += d; b ^= c; b = rotl(b, 7);
 }
-// kw: the packet's key-record row (key[8], counter lo, hi); block 0, nonce 0 || le64(counter)
-__device__ __forceinline__ void quad_otk(const uint32_t *kw, uint32_t j, uint32_t &r_j, uint32_t &s_j) {
+// kw: the packet's key-record row (key[8], counter lo, hi); block 0, nonce 0 || le64(counter).  col: column j
+// after the first column round (for j >= 1 the stream's counter-independent Stream::c_j)
+__device__ __forceinline__ void quad_otk(const uint32_t *kw, uint32_t j, uint32_t &r_j, uint32_t &s_j, uint4 &col) {
     const uint32_t a0 = j == 0 ? 0x61707865u : j == 1 ? 0x3320646eu : j == 2 ? 0x79622d32u : 0x6b206574u;
     const uint32_t b0 = kw[j];
     uint32_t a = a0, b = b0, c = kw[4 + j], d = j < 2 ? 0u : kw[6 + j]; // words 12, 13 = 0; 14, 15 = counter
 #pragma unroll
     for (int i = 0; i < 10; ++i) {
         quad_qr(a, b, c, d); // columns
+        if (i == 0) col = make_uint4(a, b, c, d);
         b = quad_perm<0x39>(b); // lane j <- j + 1
         c = quad_perm<0x4E>(c); // lane j <- j + 2
         d = quad_perm<0x93>(d); // lane j <- j + 3
@@ -380,7 +398,7 @@ __device__ __forceinline__ uint32_t flat_stage(FlatLds &L, uint32_t k, const rg_
     L.rec[k] = make_uint4((uint32_t)d.offset, (uint32_t)(d.offset >> 32), nb, 0u);
     L.kr[k][14] = d.len;
     L.kr[k][15] = d.key_idx;
-    return (nb + 3) >> 2;
+    return flat_chunks(nb);
 }
 
 template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) void flat_kernel(FlatArgs A) {
@@ -605,31 +623,42 @@ template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) voi
         RG_FLAT_MARK(1);
         for (uint32_t sb = s0; sb < e0; sb += kFlatMaxPk) {
             const uint32_t m = min(kFlatMaxPk, e0 - sb);
-            // ---- stage (unless done above) and scan the chunk counts in k order (k = lane + 64 q)
-            if (!staged) {
-#pragma unroll
-                for (uint32_t q = 0; q < kFlatMaxPk / 64; ++q) {
-                    const uint32_t k = lane + 64 * q;
-                    if (k < m) flat_stage<OPEN>(L, k, desc[sb + k], nkeys, buf_len);
-                }
-            }
-            staged = 0;
-            wave_sync();
             // ---- phase A loads, issued first so that their latency hides behind the chunk-count scan
             // and the range search (and ahead of the chunk prefetch, so that their waits stay exact)
             uint8_t dst[kFlatMaxPk / 64]; // statuses of the descriptor checks, kept for phase A
             uint4 ka[kFlatMaxPk / 64], kb[kFlatMaxPk / 64], hx[kFlatMaxPk / 64], tg[kFlatMaxPk / 64];
             uint32_t rcv[kFlatMaxPk / 64], dlen[kFlatMaxPk / 64], dkey[kFlatMaxPk / 64];
-            uint64_t doff[kFlatMaxPk / 64];
+            uint64_t doff[kFlatMaxPk / 64], ctr[kFlatMaxPk / 64];
+            // ---- stage (unless done above): packet k = lane + 64 q is read by the lane that works on it in
+            // phase A, so its fields stay in registers (no LDS round trip before the key loads), and a
+            // seal's counters are requested together with the descriptors
+            if (!staged) {
 #pragma unroll
-            for (uint32_t q = 0; q < kFlatMaxPk / 64; ++q) {
-                const uint32_t k = lane + 64 * q;
-                if (64 * q >= m) break; // wave-uniform
-                const uint4 rc = L.rec[k < m ? k : 0];
-                dlen[q] = L.kr[k < m ? k : 0][14];
-                dkey[q] = L.kr[k < m ? k : 0][15];
-                doff[q] = ((uint64_t)rc.y << 32) | rc.x;
+                for (uint32_t q = 0; q < kFlatMaxPk / 64; ++q) {
+                    const uint32_t k = lane + 64 * q;
+                    if (64 * q >= m) break; // wave-uniform
+                    const uint32_t i = sb + (k < m ? k : 0u);
+                    const rg_pkt_desc d = desc[i];
+                    if constexpr (!OPEN) ctr[q] = A.sa.counters[i];
+                    if (k < m) flat_stage<OPEN>(L, k, d, nkeys, buf_len);
+                    dlen[q] = d.len;
+                    dkey[q] = d.key_idx;
+                    doff[q] = d.offset;
+                }
+            } else {
+                wave_sync(); // staged by the one-wave search (another lane mapping): read back
+#pragma unroll
+                for (uint32_t q = 0; q < kFlatMaxPk / 64; ++q) {
+                    const uint32_t k = lane + 64 * q;
+                    if (64 * q >= m) break; // wave-uniform
+                    const uint4 rc = L.rec[k < m ? k : 0];
+                    dlen[q] = L.kr[k < m ? k : 0][14];
+                    dkey[q] = L.kr[k < m ? k : 0][15];
+                    doff[q] = ((uint64_t)rc.y << 32) | rc.x;
+                    if constexpr (!OPEN) ctr[q] = A.sa.counters[sb + (k < m ? k : 0u)];
+                }
             }
+            staged = 0;
             // the descriptor checks again, from the staged fields (VALU only)
 #pragma unroll
             for (uint32_t q = 0; q < kFlatMaxPk / 64; ++q) {
@@ -648,7 +677,7 @@ template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) voi
                 kb[q] = kp[1];
                 const uint4 *safe = reinterpret_cast<const uint4 *>(desc + sb);
                 if constexpr (!OPEN) {
-                    const uint64_t c = A.sa.counters[sb + (k < m ? k : 0)];
+                    const uint64_t c = ctr[q];
                     hx[q] = make_uint4((uint32_t)c, (uint32_t)(c >> 32), 0, 0);
                     rcv[q] = A.sa.receivers ? A.sa.receivers[ok ? dkey[q] : 0u] : 0u;
                     tg[q] = make_uint4(0, 0, 0, 0);
@@ -670,7 +699,7 @@ template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) voi
                 csr[q] = 0xFFFFFFFFu;
                 if (64 * q >= m) break; // wave-uniform
                 const uint32_t k = lane + 64 * q;
-                const uint32_t c = k < m ? (L.rec[k].z + 3) >> 2 : 0u;
+                const uint32_t c = k < m ? flat_chunks(L.rec[k].z) : 0u;
                 const uint32_t x = wave_scan_incl(c);
                 if (k < m) L.rec[k].w = csr[q] = run + x - c;
                 run += lane63(x);
@@ -717,18 +746,19 @@ template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) voi
             const uint32_t kstart = D ? kstart_scan : m - 1;
             // ---- the lane's first three chunks
             FChunk b0, b1, b2;
+            const uint4 *const safe = reinterpret_cast<const uint4 *>(desc + sb); // 16 readable bytes
             if (s.nsteps) {
-                fcur_from(s.cur, L.rec[kstart], buf, kstart, c_lo - L.rec[kstart].w);
+                fcur_from(s.cur, L.rec[kstart], buf, safe, kstart, c_lo - L.rec[kstart].w);
             } else { // no chunks: a readable dummy position
                 s.cur.k = m; s.cur.t = 0; s.cur.c = 0; s.cur.nb = 1; s.cur.live = false;
-                s.cur.pl = reinterpret_cast<const uint4 *>(desc + sb);
+                s.cur.pl = safe;
             }
             s.f = s.cur;
             s.fj = 0;
             fload(b0, s.f.pl, s.f.t, s.f.nb ? s.f.nb - 1 : 0);
-            if (s.fj + 1 < s.nsteps) { ++s.fj; fcur_next(s.f, L, buf, m); }
+            if (s.fj + 1 < s.nsteps) { ++s.fj; fcur_next(s.f, L, buf, safe, m); }
             fload(b1, s.f.pl, s.f.t, s.f.nb ? s.f.nb - 1 : 0);
-            if (s.fj + 1 < s.nsteps) { ++s.fj; fcur_next(s.f, L, buf, m); }
+            if (s.fj + 1 < s.nsteps) { ++s.fj; fcur_next(s.f, L, buf, safe, m); }
             fload(b2, s.f.pl, s.f.t, s.f.nb ? s.f.nb - 1 : 0);
             // ---- phase A: checks, one-time-key blocks, header (seal), counters_out (open)
             // Packets 64.. of a sub-unit of 65-96 get their key blocks from lane quads (16 blocks per
@@ -770,6 +800,10 @@ template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) voi
                 const Stream stm = make_stream(key, 0u, n1, n2); // nonce 0 || le64(counter), prim.rs:32-36
                 uint32_t ks[16];
                 stream_block(stm, 0, ks); // RFC 8439 §2.6 one-time key
+                uint4 *hq = reinterpret_cast<uint4 *>(L.hq[k]);
+                hq[0] = make_uint4(stm.c1[0], stm.c1[1], stm.c1[2], stm.c1[3]);
+                hq[1] = make_uint4(stm.c2[0], stm.c2[1], stm.c2[2], stm.c2[3]);
+                hq[2] = make_uint4(stm.c3[0], stm.c3[1], stm.c3[2], stm.c3[3]);
                 kr[2] = make_uint4(n1, n2, ks[0], ks[1]);
                 L.kr[k][12] = ks[2];
                 L.kr[k][13] = ks[3];
@@ -806,7 +840,8 @@ template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) voi
                     const uint32_t k = p0 + (lane >> 2), j = lane & 3u;
                     const uint32_t kk = k < m ? k : p0;
                     uint32_t r_j, s_j;
-                    quad_otk(L.kr[kk], j, r_j, s_j);
+                    uint4 col;
+                    quad_otk(L.kr[kk], j, r_j, s_j, col);
                     if constexpr (OPEN) {
                         // tag - s (mod 2^128) needs all four words of s in every lane of the quad
                         const uint32_t s0 = quad_bcast<0x00>(s_j), s1 = quad_bcast<0x55>(s_j);
@@ -823,6 +858,7 @@ template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) voi
                     if (k < m) {
                         L.kr[k][10 + j] = r_j;
                         L.sw[k][j] = s_j;
+                        if (j) reinterpret_cast<uint4 *>(L.hq[k])[j - 1] = col;
                     }
                 }
                 wave_sync();
@@ -834,7 +870,7 @@ template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) voi
                 s.cur.live = (L.rec[s.cur.k].z & kLiveBit) != 0;
                 s.f.live = s.cur.live;
                 const FKey q = fkey(L, s.cur.k);
-                s.st = make_stream(q.key, 0u, q.n1, q.n2);
+                s.st = fstream(L, s.cur.k, q);
                 s.r = make_mul(q.r[0], q.r[1], q.r[2], q.r[3]);
                 s.rn[0] = q.r[0]; s.rn[1] = q.r[1]; s.rn[2] = q.r[2]; s.rn[3] = q.r[3];
             } else {
@@ -868,16 +904,18 @@ template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) voi
             {
                 uint32_t j = 0;
                 for (; j + 3 <= S; j += 3) {
-                    flat_step<OPEN, WIN>(s, b0, j, L, buf, FS, m, lane);
-                    flat_step<OPEN, WIN>(s, b1, j + 1, L, buf, FS, m, lane);
-                    flat_step<OPEN, WIN>(s, b2, j + 2, L, buf, FS, m, lane);
+                    flat_step<OPEN, WIN>(s, b0, j, L, buf, FS, safe, m);
+                    flat_step<OPEN, WIN>(s, b1, j + 1, L, buf, FS, safe, m);
+                    flat_step<OPEN, WIN>(s, b2, j + 2, L, buf, FS, safe, m);
                 }
-                if (j < S) flat_step<OPEN, WIN>(s, b0, j, L, buf, FS, m, lane);
-                if (j + 1 < S) flat_step<OPEN, WIN>(s, b1, j + 1, L, buf, FS, m, lane);
+                if (j < S) flat_step<OPEN, WIN>(s, b0, j, L, buf, FS, safe, m);
+                if (j + 1 < S) flat_step<OPEN, WIN>(s, b1, j + 1, L, buf, FS, safe, m);
             }
             RG_FLAT_MARK(4);
             uint32_t ck = ~0u, after = 0;
             if constexpr (!OPEN) { // the last ciphertext chunk
+                // (interleaving these four blocks with the first carry-power steps, independent chains in one
+                // basic block, measured no faster: round 4)
                 acc_block_pred(s.h, s.pi.q0, s.r, s.pi_cnt > 0);
                 acc_block_pred(s.h, s.pi.q1, s.r, s.pi_cnt > 1);
                 acc_block_pred(s.h, s.pi.q2, s.r, s.pi_cnt > 2);

@@ -425,6 +425,46 @@ def test_flat_subunits_vs_oracle(engine, plan, per_unit):
     _reset(engine)
 
 
+@pytest.mark.parametrize("plan", [0, 1])
+def test_flat_far_and_empty_descriptors_vs_oracle(engine, plan):
+    """Round 4: in the flattened chunk stream every packet holds at least one chunk step; a packet with no
+    payload block (P = 0 keepalive, a descriptor that failed its checks) gets one step whose loads read a
+    safe address and whose stores are dropped.  Descriptors far past the arena (offset 2^40, 2^63), short
+    and unaligned ones sit between valid frames of 0..1504 bytes: statuses and every byte against the
+    oracle, open of the sealed batch, forged tags restored."""
+    engine.set_staged(3)
+    engine.set_plan(plan)
+    rng = np.random.default_rng(404)
+    n = 3000
+    sizes = rng.choice(np.array([0, 16, 64, 576, 1504]), n, p=[0.2, 0.2, 0.3, 0.2, 0.1])
+    keys, rec, desc, ctr, buf = _random_batch(rng, n, nkeys=3, sizes=sizes)
+    bad = rng.choice(n, 60, replace=False)
+    kinds = [(1 << 40, 64), (1 << 63, 16), (8, 16), (0, 17)]
+    for j, i in enumerate(bad):
+        o, p = kinds[j % len(kinds)]
+        desc[i]["offset"], desc[i]["len"] = o if o else int(desc[i]["offset"]), p
+    good = np.ones(n, bool)
+    good[bad] = False
+    want = buf.copy()
+    oracle.seal_batch(keys, rec, desc[good], ctr[good], want, nthreads=8)
+    got, st = _gpu_seal(engine, keys, rec, desc, ctr, buf)
+    assert (st[good] == aead.PKT_OK).all() and (st[bad] == aead.PKT_INVALID).all()
+    assert np.array_equal(got, want)
+    od = desc.copy()
+    od["len"][good] += 32
+    forged = rng.choice(np.nonzero(good)[0], 30, replace=False)
+    tampered = got.copy()
+    for i in forged:
+        tampered[int(od[i]["offset"]) + int(od[i]["len"]) - 1] ^= 1
+    back, st, co = _gpu_open(engine, keys, od, tampered)
+    want_back = tampered.copy()
+    wst, wctr = oracle.open_batch(keys, od[good], want_back, nthreads=8)
+    assert np.array_equal(st[good], wst) and (st[bad] != aead.PKT_OK).all()
+    assert (wst[np.searchsorted(np.nonzero(good)[0], forged)] == oracle.DECRYPT_ERR).all()
+    assert np.array_equal(back, want_back)
+    _reset(engine)
+
+
 @pytest.mark.parametrize("n", [16384, 65536])
 def test_flat_coop_search_vs_oracle(engine, n):
     """Round 3: when n is a multiple of 4096 and the units of a 4096-packet group are a multiple of four

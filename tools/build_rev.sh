@@ -1,0 +1,23 @@
+#!/bin/bash
+# Builds the library of a committed revision into tools/build/librg_<name>.so, for an interleaved A/B of
+# the working tree ("base" in tools/ab.sh) against it (load it with RG_AEAD_LIB=...).
+#   usage: tools/build_rev.sh NAME [REV]     (REV defaults to HEAD)
+set -eu
+cd "$(dirname "$0")/.."
+name=$1
+rev=${2:-HEAD}
+src=$(mktemp -d /tmp/rg_rev.XXXXXX)
+git archive "$rev" rustyguard_amd/csrc include | tar -x -C "$src"
+mkdir -p tools/build
+objs=()
+for s in rg_kernels.hip rg_tile.hip rg_pipe.hip rg_flat.hip rg_mac.hip rg_api.cpp; do
+    x=()
+    [[ $s == *.cpp ]] && x=(-x hip)
+    /opt/rocm/bin/hipcc "${x[@]}" --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -I "$src/include" \
+        -c "$src/rustyguard_amd/csrc/$s" -o "$src/$s.o" &
+    objs+=("$src/$s.o")
+done
+wait
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o tools/build/librg_$name.so "${objs[@]}"
+rm -rf "$src"
+echo tools/build/librg_$name.so
