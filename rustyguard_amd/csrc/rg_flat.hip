@@ -101,9 +101,10 @@ constexpr uint32_t kLiveBit = 0x80000000u, kFail = 2u;
 // see flat_coop_ok and DESIGN.md §4.6)
 constexpr uint32_t kCoopGroup = 4096;
 constexpr uint32_t kCoopWPkt = 1, kCoopWChk = 8;
-// the coop search sums work in 32 bits and doubles it for the midpoint targets
-static_assert(kCoopGroup * (kCoopWPkt + kCoopWChk * (kMaxPayload / 64ull + 1)) * 2 < (1ull << 32),
-              "coop work sums overflow 32 bits");
+// the coop search sums work in 32 bits and doubles it for the midpoint targets; the cut counts
+// compare doubled sums by the sign bit of their difference, so they stay below 2^31
+static_assert(kCoopGroup * (kCoopWPkt + kCoopWChk * (kMaxPayload / 64ull + 1)) * 2 < (1ull << 31),
+              "coop work sums overflow 31 bits");
 constexpr uint32_t kCoopLds = 256; // shared slots: wave totals, cut counts
 constexpr uint32_t kFlatWaves = 4; // waves per workgroup (the coop search's four quarters), one per SIMD
 static_assert(kFlatWaves * sizeof(FlatLds) + 256 <= kLdsPerCu, "flat LDS image");
@@ -405,7 +406,7 @@ template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) voi
     extern __shared__ __attribute__((aligned(16))) uint8_t flat_lds[];
     const uint32_t lane = threadIdx.x & 63, wv = uniform_u32(threadIdx.x >> 6);
     FlatLds &L = reinterpret_cast<FlatLds *>(flat_lds)[wv];
-    const uint32_t wid = uniform_u32(blockIdx.x * kFlatWaves + wv), nw = gridDim.x * kFlatWaves;
+    const uint32_t wid = uniform_u32(blockIdx.x * kFlatWaves + wv);
     const uint32_t n = OPEN ? A.oa.n : A.sa.n;
     uint8_t *const buf = OPEN ? A.oa.buf : A.sa.buf;
     const uint64_t buf_len = OPEN ? A.oa.buf_len : A.sa.buf_len;
@@ -419,6 +420,7 @@ template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) voi
     FS.junk = WIN ? nullptr : A.junk + ((uint64_t)wid * 64 + lane) * 4;
 #if RG_DIAG
     // diagnostic builds (debug mode 3): per wave, s_memtime at the end of each phase of its first sub-unit
+    const uint32_t nw = gridDim.x * kFlatWaves;
     uint64_t *const dbg = OPEN ? A.oa.dbg : A.sa.dbg;
     uint64_t mk[8] = {__builtin_amdgcn_s_memtime(), 0, 0, 0, 0, 0, 0, 0};
     const uint64_t rt0 = dbg ? __builtin_amdgcn_s_memrealtime() : 0; // 100 MHz wall clock (wave start / end)
@@ -426,13 +428,25 @@ template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) voi
     do {                                                                    \
         if (dbg && mk[slot] == 0) mk[slot] = __builtin_amdgcn_s_memtime(); \
     } while (0)
+    // the cooperative search's own steps (second block of rows, slots 2..7)
+    uint64_t sk[6] = {0, 0, 0, 0, 0, 0};
+#define RG_FLAT_SUB(slot)                                                   \
+    do {                                                                    \
+        if (dbg && sk[slot] == 0) sk[slot] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
 #else
+#define RG_FLAT_SUB(slot) \
+    do {                  \
+    } while (0)
 #define RG_FLAT_MARK(slot) \
     do {                   \
     } while (0)
 #endif
+    // one unit per wave: launch_flat sizes the grid to exactly A.units waves (a loop over units made hipcc
+    // hoist every path's setup -- the one-wave search's reciprocals among them -- in front of the coop search)
     const uint32_t NU = A.units;
-    for (uint32_t u = wid; u < NU; u += nw) {
+    {
+        const uint32_t u = wid;
         // ---- this unit's packets [s, e) and, when it is read from a group, its first sub-unit staged
         uint32_t s0, e0, staged = 0;
         if (A.coop) {
@@ -446,6 +460,7 @@ template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) voi
             const uint32_t kgc = uniform_u32(A.coop);               // units per group
             const uint32_t g = uniform_u32(u / kgc), j = uniform_u32(u - g * kgc), j0 = j - wv;
             const uint32_t gb = g * kCoopGroup + wv * kFlatGroup;    // this wave's 1024 packets
+            RG_FLAT_SUB(0);
             rg_pkt_desc d[16];
 #pragma unroll
             for (int q = 0; q < 16; ++q) d[q] = desc[gb + lane + 64 * q];
@@ -463,6 +478,7 @@ template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) voi
                 e[12] = a3.x; e[13] = a3.y; e[14] = a3.z; e[15] = a3.w;
             }
             wave_sync();
+            RG_FLAT_SUB(1);
 #pragma unroll
             for (int q = 1; q < 16; ++q) e[q] += e[q - 1];
             const uint32_t lsum = e[15];
@@ -470,7 +486,9 @@ template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) voi
 #pragma unroll
             for (int q = 0; q < 16; ++q) e[q] += lx;
             if (lane == 0) sh[wv] = lane63(lx + lsum); // this wave's total
+            RG_FLAT_SUB(2);
             __syncthreads();
+            RG_FLAT_SUB(3);
             uint32_t off = 0, tot = 0; // work of the group's packets before this wave's; the group's
 #pragma unroll
             for (uint32_t w = 0; w < kFlatWaves; ++w) {
@@ -500,13 +518,19 @@ template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) voi
                     } else if (t2[b] > hi2) {
                         cnt[b] = kFlatGroup;
                     } else {
+                        // Midpoints rise strictly with the packet index (every packet has work >= 1), so the
+                        // lanes whose last midpoint lies below the target are a prefix of the wave: the count
+                        // is 16 per such lane plus the first other lane's own count (a ballot and one
+                        // readlane instead of a wave scan).  Sums stay below 2^31 (static_assert above), so
+                        // (m - t) >> 31 is the comparison m < t without a carry flag (no SGPR hazard nops).
                         uint32_t prev = prev0, c = 0;
 #pragma unroll
                         for (int q = 0; q < 16; ++q) {
-                            c += e[q] + prev + lo2 < t2[b] ? 1u : 0u;
+                            c += (e[q] + prev + lo2 - t2[b]) >> 31;
                             prev = e[q];
                         }
-                        cnt[b] = lane63(wave_scan_incl(c));
+                        const uint32_t full = (uint32_t)__popcll(__ballot(((e[15] + e[14] + lo2 - t2[b]) >> 31) != 0));
+                        cnt[b] = 16u * full + (full < 64 ? (uint32_t)__builtin_amdgcn_readlane((int)c, (int)full) : 0u);
                     }
                 }
             }
@@ -514,7 +538,9 @@ template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) voi
 #pragma unroll
                 for (int b = 0; b < 5; ++b) sh[8 + 5 * wv + b] = cnt[b];
             }
+            RG_FLAT_SUB(4);
             __syncthreads();
+            RG_FLAT_SUB(5);
             uint32_t cut0 = 0, cut1 = 0;
 #pragma unroll
             for (uint32_t w = 0; w < kFlatWaves; ++w) {
@@ -1060,10 +1086,12 @@ template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) voi
             for (int q = 0; q < 8; ++q) dbg[8ull * wid + q] = mk[q];
             dbg[8ull * (nw + wid) + 0] = rt0; // second block of rows: wall-clock start and end
             dbg[8ull * (nw + wid) + 1] = rt1;
+            for (int q = 0; q < 6; ++q) dbg[8ull * (nw + wid) + 2 + q] = sk[q]; // the search's steps
         }
     }
 #endif
 #undef RG_FLAT_MARK
+#undef RG_FLAT_SUB
 }
 
 // The workgroup-cooperative unit search applies when every workgroup's four units lie in one group of

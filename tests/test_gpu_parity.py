@@ -849,6 +849,35 @@ def test_mac_verify_batch_vs_oracle(engine, which):
     assert (st[pick[:500]] == 0).all()
 
 
+def test_mac_verify_key_table_regrow_on_a_busy_stream(engine):
+    """the context's device copy of the MAC key states is wiped and regrown when a call brings
+    more keys; two calls back to back on one non-blocking stream, the second with a larger key table, must
+    not let the regrow (wipe before free) touch the states the first call's kernel is still reading.
+    Both verdicts against the oracle, all scanned (RG_KEY_SCAN: every message reads every key)."""
+    rng = np.random.default_rng(61)
+    s = torch.cuda.Stream()
+    runs = []
+    for nk in (8, 64):
+        keys = rng.integers(0, 256, (nk, 32), dtype=np.uint8)
+        desc, buf = _handshake_batch(rng, 4000, keys, 32, 1)
+        desc["key_idx"][::2] = aead.KEY_SCAN
+        for i in range(0, len(desc), 7):
+            buf[int(desc["offset"][i]) + int(desc["len"][i]) - 29] ^= 0x10
+        want, wkey = oracle.mac_verify_batch(keys, 1, desc, buf)
+        with torch.cuda.stream(s):
+            dk, dd, db = _dev(keys), _dev(desc.view(np.uint8).reshape(-1, 16)), _dev(buf)
+            st = torch.zeros(len(desc), dtype=torch.uint8, device="cuda")
+            ko = torch.zeros(len(desc), dtype=torch.int32, device="cuda")
+        s.synchronize()
+        runs.append((dk, dd, db, st, ko, want, wkey))
+    for dk, dd, db, st, ko, _, _ in runs:  # enqueued back to back, no synchronisation between them
+        engine.mac_verify_dev(dk, 1, dd, db, st, ko, stream=s)
+    s.synchronize()
+    for _, _, _, st, ko, want, wkey in runs:
+        assert list(st.cpu().numpy()) == list(want)
+        assert list(ko.cpu().numpy().view(np.uint32)) == list(wkey)
+
+
 @pytest.mark.parametrize("which", [1, 2])
 def test_mac_verify_any_length(engine, which):
     """The batch MAC check at every message length 32..300 (covered part empty, not a multiple of 4, on

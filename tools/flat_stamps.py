@@ -49,6 +49,8 @@ for op in ("seal", "open"):
     d = dbg.cpu().numpy().reshape(-1, 8).astype(np.int64)
     nwv = int((d[:1024, 0] != 0).sum())
     rt = d[nwv:2 * nwv, :2].astype(np.float64) / 100.0  # wall clock, us (s_memrealtime at 100 MHz)
+    sub = d[nwv:2 * nwv, 2:8].copy()  # the cooperative search's steps (s_memtime), 0 = not reached
+    sub_t0 = d[:nwv, 0:1]
     d = d[:nwv]
     d = d[d[:, 0] != 0]
     t0 = d[:, 0:1]
@@ -72,6 +74,15 @@ for op in ("seal", "open"):
         out["wall_us_start_pct_0_50_100"] = [round(float(x), 2) for x in np.percentile(rt[:, 0] - r0, [0, 50, 100])]
         out["wall_us_end_pct_0_50_90_100"] = [round(float(x), 2) for x in np.percentile(rt[:, 1] - r0, [0, 50, 90, 100])]
         out["clock_ghz"] = round(float(rel[:, 7].sum() / ((rt[:, 1] - rt[:, 0]).sum() * 1e3)), 3)
+    if (sub[:, 5] != 0).any():
+        # search steps: coop entry (kernel arguments, setup), descriptor loads + LDS transpose, prefix and
+        # wave total, first barrier, cut counts, second barrier
+        okw = (sub != 0).all(axis=1) & (sub_t0[:, 0] != 0)
+        st = np.concatenate([sub_t0[okw], sub[okw]], axis=1)
+        dl = np.diff(st, axis=1)
+        nm = ["entry", "desc_loads+transpose", "prefix", "barrier1", "cuts", "barrier2"]
+        out["search_steps"] = {k: {"mean_cyc": int(dl[:, i].mean()), "max_cyc": int(dl[:, i].max())}
+                               for i, k in enumerate(nm)}
     res[op] = out
     print(op, json.dumps(out), flush=True)
     if args.per_wave and op == "seal":
