@@ -406,7 +406,12 @@ template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) voi
     extern __shared__ __attribute__((aligned(16))) uint8_t flat_lds[];
     const uint32_t lane = threadIdx.x & 63, wv = uniform_u32(threadIdx.x >> 6);
     FlatLds &L = reinterpret_cast<FlatLds *>(flat_lds)[wv];
-    const uint32_t wid = uniform_u32(blockIdx.x * kFlatWaves + wv);
+    // Workgroups are dealt to the 8 XCDs round-robin (blockIdx % 8, a speed-only assumption): renumbered so
+    // that consecutive workgroups -- the 16 of one cooperative-search group, which all read that group's
+    // descriptors -- share one XCD and its L2 (one fabric fetch of the group's descriptors, not eight)
+    const uint32_t nb = gridDim.x;
+    const uint32_t lb = nb % 8u == 0 ? (blockIdx.x % 8u) * (nb / 8u) + blockIdx.x / 8u : blockIdx.x;
+    const uint32_t wid = uniform_u32(lb * kFlatWaves + wv);
     const uint32_t n = OPEN ? A.oa.n : A.sa.n;
     uint8_t *const buf = OPEN ? A.oa.buf : A.sa.buf;
     const uint64_t buf_len = OPEN ? A.oa.buf_len : A.sa.buf_len;

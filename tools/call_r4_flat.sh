@@ -16,5 +16,5 @@ tail -2 gpurun_out/r4_flat_tests.log
 [ $rc -eq 0 ] || exit $rc
 bash tools/ab.sh "base head" "cfg3" 3 --no-cold --forged 0 &&
 bash tools/ab.sh "base head" "cfg2" 1 --no-cold --forged 0 &&
-RG_AEAD_LIB=tools/build/librg_diag.so timeout -k 10 200 python tools/flat_stamps.py --workload cfg3 > gpurun_out/r4_cfg3_flat_stamps3.txt 2>&1 && cat gpurun_out/r4_cfg3_flat_stamps3.txt &&
-timeout -k 10 300 python tools/e2e_probe.py cfg2 8,16,32 > gpurun_out/r4_e2e_probe5.jsonl && cat gpurun_out/r4_e2e_probe5.jsonl
+RG_AEAD_LIB=tools/build/librg_diag.so timeout -k 10 200 python tools/flat_stamps.py --workload cfg3 > gpurun_out/r4_cfg3_flat_stamps4.txt 2>&1 && cat gpurun_out/r4_cfg3_flat_stamps4.txt &&
+timeout -k 10 300 python tools/e2e_probe.py cfg2 8,16,32 > gpurun_out/r4_e2e_probe6.jsonl && cat gpurun_out/r4_e2e_probe6.jsonl
