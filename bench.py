@@ -48,7 +48,7 @@ POLY_PEAK_GBS = 15765.0
 MICRO_CLOCK_GHZ = 2.39
 KERNEL_CLOCK_GHZ = {
     "cfg2": (2.135, "profiles/r4_cfg2_twowave.txt (one wave per SIMD, 2.130-2.137 GHz)"),
-    "cfg3": (2.18, "profiles/r3_valu_cfg3.json (flattened kernel stamps)"),
+    "cfg3": (2.15, "profiles/r4_cfg3_flat_ab.txt, r4_cfg3_search_ab.txt, r4_cfg3_xcd_ab.txt (flattened kernel stamps, 2.09-2.19 GHz by box)"),
     "cfg4": (2.09, "profiles/r3_valu_cfg4.json (GRBM quotient over a ~1 ms dispatch)"),
     "cfg5": (2.09, "as cfg4: the same tile kernel on 8 Mi packets"),
 }
