@@ -592,9 +592,10 @@ __device__ __forceinline__ void pipe_open_packet(const OpenArgs &a, uint32_t i, 
 #if RG_DIAG
 // Diagnostic builds: with a stamp buffer (debug mode 3, or any seal mode) lane 0 of every wave records
 // [s_memtime delta, real-time ticks to the end of the wave's first and second unit, XCC_ID << 32 |
-// HW_ID (wave slot, SIMD, CU, SH, SE), start s_memrealtime, 4, 1, s_memrealtime delta]
+// HW_ID (wave slot, SIMD, CU, SH, SE), start s_memrealtime, s_memtime cycles of the prologue (entry to
+// the first unit's start), 1, s_memrealtime delta]
 // (tools/stamps.py, tools/coresidency.py; s_memrealtime ticks at 100 MHz).
-__device__ __forceinline__ void pipe_stamp(uint64_t *dbg, uint64_t t0, uint64_t r0, const uint64_t marks[2]) {
+__device__ __forceinline__ void pipe_stamp(uint64_t *dbg, uint64_t t0, uint64_t r0, const uint64_t marks[3]) {
     const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
     if ((threadIdx.x & 63) == 0) {
         uint64_t *o = dbg + 8ull * (blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64);
@@ -603,7 +604,7 @@ __device__ __forceinline__ void pipe_stamp(uint64_t *dbg, uint64_t t0, uint64_t 
         o[2] = marks[1] ? marks[1] - r0 : 0;
         o[3] = ((uint64_t)(uint32_t)__builtin_amdgcn_s_getreg(0xF814) << 32) | (uint32_t)__builtin_amdgcn_s_getreg(0xF804);
         o[4] = r0;
-        o[5] = 4;
+        o[5] = marks[2] ? marks[2] - t0 : 0; // s_memtime cycles from the kernel's entry to its first unit
         o[6] = 1;
         o[7] = r1 - r0;
     }
@@ -623,7 +624,7 @@ __device__ __forceinline__ void pipe_stamp(uint64_t *dbg, uint64_t t0, uint64_t 
 // arguments in scratch, ~250 VGPRs).
 template <class Body>
 __device__ __forceinline__ void pipe_walk(uint32_t n, uint32_t lg0, const PipePlan &pp, const rg_pkt_desc *desc,
-                                          bool stamp, uint64_t marks[2], Body &&body) {
+                                          bool stamp, uint64_t marks[3], Body &&body) {
     const uint32_t lane = threadIdx.x & 63;
     const bool planned = pp.counts != nullptr;
     uint32_t my_cnt = 0, my_start = 0, my_lg = 0, my_tiles = 0, S = 1, simd = 0, ntiles = 0;
@@ -696,6 +697,7 @@ __device__ __forceinline__ void pipe_walk(uint32_t n, uint32_t lg0, const PipePl
         Unit far = locate(it + 2 * stride, q2);
         if (planned) far.i = pp.lists[q2];
         const rg_pkt_desc dnxt = desc[nxt.live ? nxt.i : 0];
+        if (stamp && it == first) marks[2] = __builtin_amdgcn_s_memtime(); // the prologue's end
         if (cur.live) body(cur.i, dcur, cur.j, 1u << cur.lg);
         if (stamp) { // diagnostics: real-time ticks at the end of a wave's first two units
             const uint64_t now = __builtin_amdgcn_s_memrealtime();
@@ -713,7 +715,7 @@ __device__ __forceinline__ void pipe_walk(uint32_t n, uint32_t lg0, const PipePl
 // an LDS reservation that fixes residency.
 // flags: bits 0-1 log2 lanes per packet (without a plan), kPipeLinesFlag: the LDS ring is reserved
 template <int MODE> __global__ __launch_bounds__(256) void pipe_seal_kernel(SealArgs a, uint32_t flags, PipePlan pp) {
-    uint64_t marks[2] = {0, 0};
+    uint64_t marks[3] = {0, 0, 0};
     const bool lines = (flags & kPipeLinesFlag) != 0;
 #if RG_DIAG
     const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
@@ -730,7 +732,7 @@ template <int MODE> __global__ __launch_bounds__(256) void pipe_seal_kernel(Seal
 }
 
 __global__ __launch_bounds__(256) void pipe_open_kernel(OpenArgs a, uint32_t flags, PipePlan pp) {
-    uint64_t marks[2] = {0, 0};
+    uint64_t marks[3] = {0, 0, 0};
     const bool lines = (flags & kPipeLinesFlag) != 0;
 #if RG_DIAG
     const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();

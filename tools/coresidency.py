@@ -73,6 +73,7 @@ for rep in range(3):
         "last_wave_end_us": round(float(end.max() - t0), 2),
         "start_spread_us": round(float(np.percentile(start - t0, 100)), 2),
         "cycles_per_wave_mean": float(d[:, 0].mean()),
+        "prologue_cycles_mean_max": [float(d[:, 5].mean()), float(d[:, 5].max())],  # entry -> first unit's start
         "clock_ghz": round(float(d[:, 0].sum() / (d[:, 7].sum() / 100e6)) / 1e9, 3),
     })
 out = {"workload": args.workload, "lanes": args.lanes, "wg_per_cu": args.wg_per_cu, "mode": args.mode,
