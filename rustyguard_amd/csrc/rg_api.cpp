@@ -223,6 +223,17 @@ struct rg_ctx {
 
 namespace {
 
+// The caller's current HIP device, put back on the way out: every entry point selects its context's
+// device (and a group call each of its contexts' in turn), while the caller -- a torch program, say --
+// keeps its own device selected.
+struct DeviceGuard {
+    int dev = -1;
+    DeviceGuard() { (void)hipGetDevice(&dev); }
+    ~DeviceGuard() {
+        if (dev >= 0) (void)hipSetDevice(dev);
+    }
+};
+
 int check_ctx(rg_ctx *ctx) {
     if (!ctx) return set_err(RG_EINVAL, "null context");
     hipError_t e = hipSetDevice(ctx->device);
@@ -244,6 +255,7 @@ int rg_create(int device, rg_ctx **out) {
     int ndev = 0;
     RG_HIP(hipGetDeviceCount(&ndev), "hipGetDeviceCount");
     if (device < 0 || device >= ndev) return set_err(RG_EINVAL, "no such HIP device");
+    DeviceGuard dg_;
     RG_HIP(hipSetDevice(device), "hipSetDevice");
     rg_ctx *c = new (std::nothrow) rg_ctx();
     if (!c) return set_err(RG_ENOMEM, "alloc ctx");
@@ -283,6 +295,7 @@ int rg_create(int device, rg_ctx **out) {
 
 void rg_destroy(rg_ctx *ctx) {
     if (!ctx) return;
+    DeviceGuard dg_;
     (void)hipSetDevice(ctx->device);
     for (hipStream_t sp : {ctx->hs_in, ctx->hs_run, ctx->hs_out, ctx->gen_stream})
         if (sp) {
@@ -543,6 +556,7 @@ static hipError_t launch_open_any(rg_ctx *ctx, const rg::OpenArgs &a0, PlanBuf &
 int rg_seal_batch_dev(rg_ctx *ctx, const uint8_t *keys, const uint32_t *receivers, uint32_t nkeys,
                       const rg_pkt_desc *desc, const uint64_t *counters, size_t n, uint8_t *buf, size_t buf_len,
                       uint8_t *status, void *stream) {
+    DeviceGuard dg_;
     int rc = check_ctx(ctx);
     if (rc) return rc;
     if (n == 0) return RG_OK;
@@ -564,6 +578,7 @@ int rg_seal_batch_dev(rg_ctx *ctx, const uint8_t *keys, const uint32_t *receiver
 
 int rg_open_batch_dev(rg_ctx *ctx, const uint8_t *keys, uint32_t nkeys, const rg_pkt_desc *desc, size_t n,
                       uint8_t *buf, size_t buf_len, uint8_t *status, uint64_t *counters_out, void *stream) {
+    DeviceGuard dg_;
     int rc = check_ctx(ctx);
     if (rc) return rc;
     if (n == 0) return RG_OK;
@@ -584,6 +599,7 @@ int rg_open_batch_dev(rg_ctx *ctx, const uint8_t *keys, uint32_t nkeys, const rg
 
 int rg_synth_fill_dev(rg_ctx *ctx, const rg_pkt_desc *desc, const uint32_t *inner_len, size_t n, uint8_t *buf,
                       size_t buf_len, uint64_t seed, void *stream) {
+    DeviceGuard dg_;
     int rc = check_ctx(ctx);
     if (rc) return rc;
     if (n == 0) return RG_OK;
@@ -624,6 +640,7 @@ int64_t rg_rx_table_find(const rg_rx_entry *table, uint32_t cap, uint32_t receiv
 int rg_open_batch_dev_rx(rg_ctx *ctx, const uint8_t *keys, uint32_t nkeys, const rg_rx_entry *rx_table,
                          uint32_t rx_cap, const rg_pkt_desc *desc, size_t n, uint8_t *buf, size_t buf_len,
                          uint8_t *status, uint64_t *counters_out, uint32_t *key_idx_out, void *stream) {
+    DeviceGuard dg_;
     int rc = check_ctx(ctx);
     if (rc) return rc;
     if (n == 0) return RG_OK;
@@ -641,6 +658,7 @@ int rg_open_batch_dev_rx(rg_ctx *ctx, const uint8_t *keys, uint32_t nkeys, const
 int rg_mac_verify_batch_dev(rg_ctx *ctx, const uint8_t *keys, uint32_t key_len, uint32_t nkeys, int which,
                             const rg_pkt_desc *desc, size_t n, const uint8_t *buf, size_t buf_len, uint8_t *status,
                             uint32_t *key_idx_out, void *stream) {
+    DeviceGuard dg_;
     int rc = check_ctx(ctx);
     if (rc) return rc;
     if (n == 0) return RG_OK;
@@ -911,6 +929,7 @@ extern "C" {
 int rg_seal_batch_host(rg_ctx *ctx, const uint8_t *keys, const uint32_t *receivers, uint32_t nkeys,
                        const rg_pkt_desc *desc, const uint64_t *counters, size_t n, uint8_t *buf, size_t buf_len,
                        uint8_t *status) {
+    DeviceGuard dg_;
     int rc = check_ctx(ctx);
     if (rc) return rc;
     if (n == 0) return RG_OK;
@@ -928,6 +947,7 @@ int rg_seal_batch_host(rg_ctx *ctx, const uint8_t *keys, const uint32_t *receive
 
 int rg_open_batch_host(rg_ctx *ctx, const uint8_t *keys, uint32_t nkeys, const rg_pkt_desc *desc, size_t n,
                        uint8_t *buf, size_t buf_len, uint8_t *status, uint64_t *counters_out) {
+    DeviceGuard dg_;
     int rc = check_ctx(ctx);
     if (rc) return rc;
     if (n == 0) return RG_OK;
@@ -972,16 +992,6 @@ void split_bounds(const rg_pkt_desc *desc, size_t n, bool open, int parts, size_
     }
     bounds[parts] = n;
 }
-
-// the caller's current HIP device, put back on the way out: a group call switches devices as it goes,
-// and the caller (a torch program, say) keeps its own device selected
-struct DeviceGuard {
-    int dev = -1;
-    DeviceGuard() { (void)hipGetDevice(&dev); }
-    ~DeviceGuard() {
-        if (dev >= 0) (void)hipSetDevice(dev);
-    }
-};
 
 // every context of the group, locked in index order (a group's calls are serialised per context as
 // a single context's are)
@@ -1116,6 +1126,7 @@ int rg_open_batch_dev_multi(rg_group *g, const rg_dev_shard *sh) {
 // nonce: 12 bytes, or 24 for XChaCha20-Poly1305 (xchacha)
 static int general_one(rg_ctx *ctx, bool dec, const uint8_t key[32], const uint8_t *nonce, const uint8_t *aad,
                        size_t aad_len, uint8_t *payload, size_t len, uint8_t tag[16], bool xchacha = false) {
+    DeviceGuard dg_;
     int rc = check_ctx(ctx);
     if (rc) return rc;
     if (!key || !nonce || !tag || (aad_len && !aad) || (len && !payload))
@@ -1205,6 +1216,7 @@ int rg_xchacha20poly1305_dec(rg_ctx *ctx, const uint8_t key[32], const uint8_t n
 // never into the product library.
 #if RG_TEST_HOOKS
 int rg_debug_read_arena(rg_ctx *ctx, int which, void *dst, size_t bytes) {
+    DeviceGuard dg_;
     int rc = check_ctx(ctx);
     if (rc) return rc;
     if (!dst) return set_err(RG_EINVAL, "debug_read_arena: null dst");
@@ -1428,6 +1440,7 @@ void rg_sessions_destroy(rg_sessions *s) {
     if (!s) return;
     std::fill(s->keys.begin(), s->keys.end(), 0); // zeroize, as prim.rs:227-231 / lib.rs:216-228
     SessDev &D = s->dev;
+    DeviceGuard dg_;
     (void)hipSetDevice(s->ctx->device);
     (void)drain_device_work(D);
     D.keys.release(); D.recv.release(); D.rx.release(); // keys: a secret buffer, zeroed before it is freed
@@ -1673,6 +1686,7 @@ int rg_send_batch_dev(rg_sessions *s, const uint32_t *slots, const rg_pkt_desc *
     if (s->group) return set_err(RG_EINVAL, "send_batch_dev: a group's table takes host frames (rg_send_batch)");
     if (n > 0xFFFFFFFFull) return set_err(RG_EINVAL, "send_batch_dev: too many packets");
     if (n == 0) return RG_OK;
+    DeviceGuard dg_;
     int rc = check_ctx(s->ctx);
     if (rc) return rc;
     rc = sync_tables(s);
@@ -1723,6 +1737,7 @@ int rg_recv_batch_dev(rg_sessions *s, const rg_pkt_desc *desc, size_t n, uint8_t
     if (n > 0xFFFFFFFFull) return set_err(RG_EINVAL, "recv_batch_dev: too many packets");
     RecvStage &R = s->dev.rv;
     if (R.pending) return set_err(RG_EINVAL, "recv_batch_dev: finish the pending batch first");
+    DeviceGuard dg_;
     int rc = check_ctx(s->ctx);
     if (rc) return rc;
     rc = sync_tables(s);
@@ -1776,6 +1791,7 @@ int rg_recv_batch_dev_finish(rg_sessions *s, const uint64_t *src, uint8_t *statu
     R.pending = false;
     const size_t n = R.n;
     if (n == 0) return RG_OK;
+    DeviceGuard dg_;
     int rc = check_ctx(s->ctx);
     if (rc) return rc;
     RG_HIP(hipEventSynchronize(R.ev_meta), "recv metadata");
