@@ -92,7 +92,8 @@ enum rg_pkt_status {
 /* ---------------------------------------------------------------- context */
 
 int rg_abi_version(void);
-/* Create a context bound to HIP device `device` (one per process/GPU). */
+/* Create a context bound to HIP device `device` (one per process/GPU).  Every call on a context works on
+ * its device and leaves the caller's current HIP device as it found it. */
 int rg_create(int device, rg_ctx **out);
 void rg_destroy(rg_ctx *ctx);
 /* Text of the last error on this thread ("" if none). */
