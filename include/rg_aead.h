@@ -205,10 +205,11 @@ int rg_set_debug_mode(rg_ctx *ctx, int mode);
  * buffer, 8 x u64 per wave: mode 3 on the tile kernels (setup, store,
  * dma-issue, dma-wait, chunk, tail, valid, real-time ticks at 100 MHz); any
  * non-zero mode on the pipelined kernel (cycles, two unit marks, XCC_ID << 32 |
- * HW_ID, start tick, 4, valid, real-time ticks); mode 3 on the flattened
- * kernel (s_memtime at the end of each phase) plus a second block of rows after
- * the first CUs x 4 (wall-clock start and end), so size the buffer for
- * 2 x CUs x 4 x 8 u64 there. */
+ * HW_ID, start tick, prologue cycles, valid, real-time ticks); mode 3 on the
+ * flattened kernel (s_memtime at the end of each phase) plus a second block of
+ * rows after the first CUs x 4 (wall-clock start and end, the unit search's
+ * steps) and a third (the first sub-unit's packets / chunks / steps, XCC_ID << 32
+ * | HW_ID), so size the buffer for 3 x CUs x 4 x 8 u64 there. */
 int rg_set_debug_buffer(rg_ctx *ctx, void *dev_ptr);
 
 /* ----------------------------------------- host-memory batch (blocking) */

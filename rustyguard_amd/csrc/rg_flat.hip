@@ -435,6 +435,7 @@ template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) voi
     } while (0)
     // the cooperative search's own steps (second block of rows, slots 2..7)
     uint64_t sk[6] = {0, 0, 0, 0, 0, 0};
+    uint64_t unit_info = 0; // first sub-unit: packets m | chunks D << 16 | steps S << 40 (third block of rows)
 #define RG_FLAT_SUB(slot)                                                   \
     do {                                                                    \
         if (dbg && sk[slot] == 0) sk[slot] = __builtin_amdgcn_s_memtime(); \
@@ -770,6 +771,9 @@ template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) voi
             wave_sync(); // the scratch reads are done before the slots are used again
             if (lane == 0) L.rec[m] = make_uint4(0, 0, 0, D);
             RG_FLAT_MARK(2);
+#if RG_DIAG
+            if (dbg && unit_info == 0) unit_info = (uint64_t)m | ((uint64_t)D << 16) | ((uint64_t)((D + 63) / 64) << 40);
+#endif
             // ---- the lane's chunk range and start packet
             const uint32_t c_lo = (uint32_t)(((uint64_t)lane * D) >> 6), c_hi = (uint32_t)(((uint64_t)(lane + 1) * D) >> 6);
             FLane s;
@@ -1092,6 +1096,9 @@ template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) voi
             dbg[8ull * (nw + wid) + 0] = rt0; // second block of rows: wall-clock start and end
             dbg[8ull * (nw + wid) + 1] = rt1;
             for (int q = 0; q < 6; ++q) dbg[8ull * (nw + wid) + 2 + q] = sk[q]; // the search's steps
+            dbg[8ull * (2 * nw + wid) + 0] = unit_info;
+            dbg[8ull * (2 * nw + wid) + 1] =
+                ((uint64_t)(uint32_t)__builtin_amdgcn_s_getreg(0xF814) << 32) | (uint32_t)__builtin_amdgcn_s_getreg(0xF804);
         }
     }
 #endif

@@ -28,7 +28,7 @@ eng.set_plan(args.plan)
 w = workloads.build(args.workload)
 b = DeviceBatch(eng, w)
 b.fill()
-dbg = torch.zeros(8 * 1024 * 2, dtype=torch.int64, device="cuda")
+dbg = torch.zeros(8 * 1024 * 3, dtype=torch.int64, device="cuda")
 eng.set_debug_buffer(dbg)
 names = ["search", "stage+scan", "phaseA", "phaseC", "carry", "phaseF", "end"]
 res = {}
@@ -86,29 +86,25 @@ for op in ("seal", "open"):
     res[op] = out
     print(op, json.dumps(out), flush=True)
     if args.per_wave and op == "seal":
-        # the unit each wave ran (wave id = unit id: one unit per wave), by the kernel's cut rule
-        P = w.desc["len"].astype(np.int64)
-        n = len(P)
-        NU, G = len(d), 1024
-        chunks = ((P + 15) // 16 + 3) // 4
-        work = 1 + chunks
-        rows = []
+        # each wave's first sub-unit as the kernel recorded it (third block of rows: packets m, chunks D,
+        # steps S; XCC_ID / HW_ID), beside its phase cycles -- what the slowest waves have in common
         raw = dbg.cpu().numpy().reshape(-1, 8).astype(np.int64)
-        for u in range(NU):
-            g = u * n // (G * NU)
-            f0 = (g * G * NU + n - 1) // n
-            f1 = min(NU, ((g + 1) * G * NU + n - 1) // n)
-            kg, j, gb = f1 - f0, u - f0, g * G
-            gn = min(G, n - gb)
-            E = np.cumsum(work[gb:gb + gn])
-            tot = int(E[-1])
-            mid2 = E + np.concatenate([[0], E[:-1]])
-            c0 = 0 if j == 0 else int((mid2 < 2 * (tot * j // kg)).sum())
-            c1 = gn if j + 1 == kg else int((mid2 < 2 * (tot * (j + 1) // kg)).sum())
-            m, D = c1 - c0, int(chunks[gb + c0:gb + c1].sum())
-            r = raw[u]
-            rows.append({"wave": u, "m": m, "D": D, "total": int(r[7] - r[0]) if r[0] else None})
-        rows.sort(key=lambda x: -(x["total"] or 0))
+        info = raw[2 * nwv:3 * nwv]
+        rows = []
+        for u in range(nwv):
+            r, ui = raw[u], int(info[u, 0])
+            if not r[0]:
+                continue
+            hw = int(info[u, 1])
+            rows.append({"wave": u, "m": ui & 0xFFFF, "D": (ui >> 16) & 0xFFFFFF, "S": ui >> 40,
+                         "xcc": (hw >> 32) & 0xF, "total": int(r[7] - r[0]),
+                         "phases": [int(r[i] - r[i - 1]) if r[i] and r[i - 1] else None for i in range(1, 8)]})
+        rows.sort(key=lambda x: -x["total"])
         with open("gpurun_out/flat_per_wave.json", "w") as fo:
             json.dump(rows, fo)
-        print("slowest", rows[:12], flush=True)
+        tot = np.array([x["total"] for x in rows], np.float64)
+        for key in ("m", "S", "xcc"):
+            v = np.array([x[key] for x in rows])
+            out_k = {int(k): [int((v == k).sum()), int(tot[v == k].mean())] for k in np.unique(v)}
+            print("by", key, "(count, mean cycles)", json.dumps(out_k), flush=True)
+        print("slowest", rows[:8], flush=True)
