@@ -425,6 +425,42 @@ def test_flat_subunits_vs_oracle(engine, plan, per_unit):
     _reset(engine)
 
 
+def test_flat_whole_groups_vs_oracle(engine):
+    """The flattened kernel forced (rg_set_staged 3) on more than 1024 packets per unit: units are then
+    whole 1024-packet groups (rg_flat.hip, the third unit rule), each wave runs eight or more 128-packet
+    sub-units.  1 Mi + 5000 small packets (keepalives, 16 and 64 bytes), every byte and status against the
+    oracle, and the open of the result with forged tags."""
+    engine.set_staged(3)
+    engine.set_plan(0)
+    rng = np.random.default_rng(1025)
+    n = 1024 * 1024 + 5000
+    sizes = rng.choice(np.array([0, 16, 64]), n, p=[0.2, 0.4, 0.4])
+    keys, rec, desc, ctr, buf = _random_batch(rng, n, nkeys=2, sizes=sizes, stride=96)
+    want = buf.copy()
+    oracle.seal_batch(keys, rec, desc, ctr, want, nthreads=8)
+    got, st = _gpu_seal(engine, keys, rec, desc, ctr, buf)
+    assert (st == aead.PKT_OK).all()
+    assert np.array_equal(got, want)
+    od = desc.copy()
+    od["len"] += 32
+    forged = rng.choice(n, 64, replace=False)
+    tampered = got.copy()
+    for i in forged:
+        tampered[int(od[i]["offset"]) + int(od[i]["len"]) - 1] ^= 1
+    back, st, co = _gpu_open(engine, keys, od, tampered)
+    bad = np.zeros(n, bool)
+    bad[forged] = True
+    assert (st[~bad] == aead.PKT_OK).all() and (st[bad] == aead.PKT_DECRYPT_ERR).all()
+    assert np.array_equal(co, ctr)
+    for i in forged:
+        o, w = int(od[i]["offset"]), int(od[i]["len"])
+        assert np.array_equal(back[o:o + w], tampered[o:o + w])
+    for i in np.nonzero(~bad)[0][::997]:
+        o, p = int(desc[i]["offset"]), int(desc[i]["len"])
+        assert np.array_equal(back[o + 16: o + 16 + p], buf[o + 16: o + 16 + p])
+    _reset(engine)
+
+
 @pytest.mark.parametrize("plan", [0, 1])
 def test_flat_far_and_empty_descriptors_vs_oracle(engine, plan):
     """Round 4: in the flattened chunk stream every packet holds at least one chunk step; a packet with no
