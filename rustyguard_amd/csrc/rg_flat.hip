@@ -10,11 +10,14 @@
 // a 64-lane wave idle.  Here every step of every lane is one 64-byte ChaCha20
 // block, whichever packet it belongs to:
 //
-//  * The batch is cut into units of whole packets of equal work (1 one-time-key
-//    block + 64-byte chunks per packet), one unit per wave.  A planner kernel
-//    writes per-1024-packet prefix sums of that work; each wave finds its own
-//    unit boundaries from them (two small searches), so nothing is sorted and no
-//    atomics sit on the data path.
+//  * The batch is cut into units of whole packets of equal work (a one-time-key
+//    block + 64-byte chunks per packet), one unit per wave, inside the kernel:
+//    the four waves of a workgroup scan a 4096-packet group's lengths together
+//    and cut their four units by the work midpoint rule (one wave alone scans a
+//    1024-packet group when the batch does not divide into such groups), so
+//    nothing is sorted, no planner launch runs and no atomics sit on the data
+//    path.  The 16 workgroups of a group share an XCD (its descriptors are
+//    fetched into one L2).
 //  * Inside a unit (processed in sub-units of <= kFlatMaxPk packets staged in
 //    LDS) phase A computes every packet's one-time-key block (RFC 8439 §2.6,
 //    spread over the 64 lanes: r and s go to LDS), then phase C deals the
@@ -30,8 +33,9 @@
 //    keystream so the frame is left as it came).
 //
 // Memory: three 64-byte chunks in flight per lane (as rg_pipe.hip), loads
-// clamped inside the frame and stores redirected to a per-lane junk slot when
-// a block is not part of the payload, so every step issues the same memory
+// clamped inside the frame and the stores of blocks that are not payload sent
+// past the arena's buffer descriptor (dropped by the range check; arenas of
+// 2 GiB or more: into a per-lane sink), so every step issues the same memory
 // instructions and the vmcnt waits stay exact.
 #include "rg_device.h"
 #include "rg_internal.h"
@@ -200,7 +204,8 @@ struct FLane {
     FChunk pi;           // seal: ciphertext chunk waiting to be absorbed (one step behind)
     uint32_t pi_cnt, pk; // its blocks and packet
     // r^e for the carry of the lane's last piece (e = data blocks of that packet after the lane),
-    // square-and-multiply from bit pb down, one bit in each of two free slots of a step's rounds
+    // square-and-multiply from bit pb down after phase C (in the keystream rounds' free slots it cost
+    // 20 %: round 2)
     Acc px;
     Mul pr;
     uint32_t pe;
@@ -947,7 +952,7 @@ template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) voi
                 if (j + 1 < S) flat_step<OPEN, WIN>(s, b1, j + 1, L, buf, FS, safe, m);
             }
             RG_FLAT_MARK(4);
-            uint32_t ck = ~0u, after = 0;
+            uint32_t ck = ~0u; // the packet whose Horner sum the next lane continues (its power is s.px)
             if constexpr (!OPEN) { // the last ciphertext chunk
                 // (interleaving these four blocks with the first carry-power steps, independent chains in one
                 // basic block, measured no faster: round 4)
@@ -958,7 +963,6 @@ template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) voi
                 if (s.nsteps > 0 && s.pk < m) {
                     if (s.cur.k == s.pk && s.cur.t > 0) { // the packet goes on in the next lane
                         ck = s.pk;
-                        after = s.cur.nb - 4 * s.cur.t;
                     } else {
                         add_h(L, s.pk, s.h);
                     }
@@ -966,18 +970,16 @@ template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) voi
             } else {
                 if (s.nsteps > 0 && s.cur.k < m && s.cur.t > 0) {
                     ck = s.cur.k;
-                    after = s.cur.nb - 4 * s.cur.t;
                 }
             }
-            // carry = h r^after for the packet the next lane continues (the power was computed during
-            // phase C; after == s.pe whenever there is a carry)
+            // carry = h r^pe for the packet the next lane continues (pe: its blocks after this lane's range,
+            // from the end markers before phase C; square-and-multiply over the wave's largest exponent)
             while (s.pb >= 0) pow_step(s);
             if (ck != ~0u) {
                 Acc cv = s.h;
                 acc_mul_gen(cv, make_gen(s.px));
                 add_h(L, ck, cv);
             }
-            (void)after;
             wave_sync();
             RG_FLAT_MARK(5);
             // ---- phase F: tags
