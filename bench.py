@@ -997,7 +997,7 @@ def _pcie_in_process(nbytes: int):
 
 def e2e_host(eng, w, b):
     """Packets that start and end in pinned host memory (a UDP socket buffer): rg_{seal,open}_batch_host,
-    H2D -> kernel -> D2H pipelined over three streams in 16 MiB slices, so one slice's upload runs beside
+    H2D -> kernel -> D2H pipelined over three streams in 8 MiB slices, so one slice's upload runs beside
     another's download.  Rates per PCIe direction are the wire bytes W = P + 32 moved each way."""
     import torch
 
@@ -1028,7 +1028,7 @@ def e2e_host(eng, w, b):
             "seal_mpkt_s": round(w.n / tsm / 1e6, 3), "open_mpkt_s": round(w.n / tom / 1e6, 3),
             "seal_gb_s_per_dir": round(wire / tsm / 1e9, 2), "open_gb_s_per_dir": round(wire / tom / 1e9, 2),
             "pcie_ceiling": ceil,
-            "note": "pinned hipHostMalloc frames, H2D+kernel+D2H over 3 streams, 16 MiB slices; median of 5"}
+            "note": "pinned hipHostMalloc frames, H2D+kernel+D2H over 3 streams, 8 MiB slices, descriptors/counters/statuses in mapped host memory; median of 5"}
 
 
 if __name__ == "__main__":

@@ -216,7 +216,7 @@ int rg_set_debug_buffer(rg_ctx *ctx, void *dev_ptr);
 /* Same contract with host pointers: frames are staged H2D, sealed/opened on
  * the GPU and copied back D2H, pipelined over three streams.  Pinned memory
  * (rg_host_alloc) gives the full PCIe rate.  rg_set_host_slice sets the byte
- * span of one pipeline slice (default 16 MiB; 64 KiB .. 1 GiB). */
+ * span of one pipeline slice (default 8 MiB; 64 KiB .. 1 GiB). */
 int rg_set_host_slice(rg_ctx *ctx, size_t bytes);
 int rg_seal_batch_host(rg_ctx *ctx, const uint8_t *keys, const uint32_t *receivers, uint32_t nkeys,
                        const rg_pkt_desc *desc, const uint64_t *counters, size_t n, uint8_t *buf, size_t buf_len,

@@ -152,7 +152,7 @@ class Engine:
               "rg_set_debug_buffer")
 
     def set_host_slice(self, nbytes: int):
-        """Byte span of one host-pipeline slice (rg_set_host_slice; default 16 MiB)."""
+        """Byte span of one host-pipeline slice (rg_set_host_slice; default 8 MiB)."""
         self._check(self._L.rg_set_host_slice(self._h, nbytes), "rg_set_host_slice")
 
     def set_wg_per_cu(self, wg: int):

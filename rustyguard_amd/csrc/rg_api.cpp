@@ -84,25 +84,35 @@ struct DevBuf {
     void release() { drop(); }
 };
 
+// Pinned host memory.  A mapped buffer (reserve_mapped) is also read and written by kernels in place,
+// through its device address d: coherent, so a kernel's stores are in host memory when it completes.
 struct HostBuf {
     void *p = nullptr;
+    void *d = nullptr; // device address of a mapped buffer
     size_t cap = 0;
     bool secret = false;
     void drop() {
         if (p && secret) memset(p, 0, cap);
         if (p) (void)hipHostFree(p);
-        p = nullptr;
+        p = d = nullptr;
         cap = 0;
     }
-    hipError_t reserve(size_t bytes) {
+    hipError_t alloc(size_t bytes, unsigned flags) {
         if (bytes <= cap) return hipSuccess;
         drop();
         if (injected_failure()) return hipErrorOutOfMemory;
         size_t want = std::max<size_t>(bytes, 4096);
-        hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
-        if (e == hipSuccess) cap = want;
+        hipError_t e = hipHostMalloc(&p, want, flags);
+        if (e != hipSuccess) return e;
+        cap = want;
+        if (flags & hipHostMallocMapped) {
+            e = hipHostGetDevicePointer(&d, p, 0);
+            if (e != hipSuccess) drop();
+        }
         return e;
     }
+    hipError_t reserve(size_t bytes) { return alloc(bytes, hipHostMallocDefault); }
+    hipError_t reserve_mapped(size_t bytes) { return alloc(bytes, hipHostMallocMapped | hipHostMallocCoherent); }
     void release() { drop(); }
 };
 
@@ -171,11 +181,13 @@ struct PlanBuf {
     }
 };
 
-// one slice buffer set of the host path: the slice's frames, descriptors, counters and statuses on
-// both sides, and the events that order it through the three pipeline streams (rg_ctx::hs_*)
+// one slice buffer set of the host path: the slice's frames on the device, its descriptors, counters and
+// statuses in mapped host memory (the kernel reads and writes them in place: round 4, one copy each way
+// per slice instead of three and two), and the events that order it through the three pipeline streams
+// (rg_ctx::hs_*)
 struct Slot {
     PlanBuf plan;
-    DevBuf d_buf, d_desc, d_ctr, d_status, d_ctr_out;
+    DevBuf d_buf;
     HostBuf h_desc, h_ctr, h_status, h_ctr_out;
     hipEvent_t ev_in = nullptr;  // the slice's inputs are on the device (recorded on hs_in)
     hipEvent_t ev_run = nullptr; // its kernel is done (recorded on hs_run)
@@ -197,7 +209,7 @@ struct rg_ctx {
     int plan = 2;     // size-class planner: 0 off (array order), 1 always, 2 auto (skip for single-class batches)
     int segments = 0; // segments per packet: 0 = automatic, else 1 / 2 / 4
     int last_kernel = -1; // kernel family of the latest batched launch (-1: none yet)
-    size_t host_slice = 16ull << 20; // byte span of one host-pipeline slice (rg_set_host_slice; 16 MiB default)
+    size_t host_slice = 8ull << 20; // byte span of one host-pipeline slice (rg_set_host_slice; 8 MiB default)
     PlanBuf plan_dev; // planner lists of the device API (calls on one ctx are stream-ordered)
     uint64_t *dbg = nullptr; // diagnostics buffer (device), stamp builds only
     int pipe_max_wg[2] = {0, 0}; // [seal, open] resident workgroups per CU of the pipelined kernel
@@ -208,7 +220,8 @@ struct rg_ctx {
     // (round 4: with one stream per slice the three slices' H2D copies ran at once and shared the
     // link, then their D2H copies -- half duplex, 27 GB/s per direction against a 48 GB/s duplex
     // ceiling; profiles/r4_e2e_probe.txt).  Three slots: a fourth (so that the upload of slice k + 1 need
-    // not wait for the download of slice k - 2) measured the same at 16 MiB slices and slower at 8 MiB.
+    // not wait for the download of slice k - 2) measured the same at 16 MiB slices and slower at 8 MiB
+    // (with the small per-slice copies that mapped host memory has since replaced).
     static constexpr int kHostSlots = 3;
     Slot slots[kHostSlots];
     hipStream_t hs_in = nullptr, hs_run = nullptr, hs_out = nullptr;
@@ -306,7 +319,7 @@ void rg_destroy(rg_ctx *ctx) {
         for (hipEvent_t ep : {s.ev_in, s.ev_run, s.ev_out})
             if (ep) (void)hipEventDestroy(ep);
         s.plan.release();
-        s.d_buf.release(); s.d_desc.release(); s.d_ctr.release(); s.d_status.release(); s.d_ctr_out.release();
+        s.d_buf.release();
         s.h_desc.release(); s.h_ctr.release(); s.h_status.release(); s.h_ctr_out.release();
     }
     ctx->plan_dev.release();
@@ -778,31 +791,27 @@ int HostRun::step() {
     const size_t m = j - i;
     const size_t span = hi - lo;
     RG_HIP(s.d_buf.reserve(span + 16), "alloc slice");
-    RG_HIP(s.d_desc.reserve(m * sizeof(rg_pkt_desc)), "alloc desc");
-    RG_HIP(s.d_status.reserve(m), "alloc status");
-    RG_HIP(s.h_desc.reserve(m * sizeof(rg_pkt_desc)), "alloc h_desc");
-    RG_HIP(s.h_status.reserve(m), "alloc h_status");
+    RG_HIP(s.h_desc.reserve_mapped(m * sizeof(rg_pkt_desc)), "alloc h_desc");
+    RG_HIP(s.h_status.reserve_mapped(m), "alloc h_status");
     rg_pkt_desc *hd = static_cast<rg_pkt_desc *>(s.h_desc.p);
     for (size_t k = 0; k < m; ++k) {
         hd[k] = desc[i + k];
         // frames outside the arena get an aligned out-of-range offset: the kernel flags them INVALID
         hd[k].offset = in_arena(desc[i + k], open, buf_len) ? desc[i + k].offset - lo : kOutOfRange;
     }
-    // uploads on hs_in (after the previous use of this slot's device buffers has been downloaded: the
-    // host waited for ev_out above, so nothing of it is still in flight)
+    if (!open) {
+        RG_HIP(s.h_ctr.reserve_mapped(m * 8), "alloc h_ctr");
+        memcpy(s.h_ctr.p, counters + i, m * 8);
+    } else {
+        RG_HIP(s.h_ctr_out.reserve_mapped(m * 8), "alloc h_ctr_out");
+    }
+    // the frames' upload on hs_in (after the previous use of this slot's buffers has been downloaded: the
+    // host waited for ev_out above, so nothing of it is still in flight); descriptors, counters and
+    // statuses stay in mapped host memory, which the kernel reads and writes over the link in place of
+    // three small copies per slice (round 4, profiles/r4_e2e_mapped_ab.txt)
     hipStream_t sin = ctx->hs_in, srun = ctx->hs_run, sout = ctx->hs_out;
-    RG_HIP(hipMemcpyAsync(s.d_desc.p, hd, m * sizeof(rg_pkt_desc), hipMemcpyHostToDevice, sin), "H2D desc");
     if (span) RG_HIP(hipMemcpyAsync(s.d_buf.p, buf + lo, span, hipMemcpyHostToDevice, sin), "H2D frames");
     uint8_t *dbuf = static_cast<uint8_t *>(s.d_buf.p);
-    if (!open) {
-        RG_HIP(s.d_ctr.reserve(m * 8), "alloc ctr");
-        RG_HIP(s.h_ctr.reserve(m * 8), "alloc h_ctr");
-        memcpy(s.h_ctr.p, counters + i, m * 8);
-        RG_HIP(hipMemcpyAsync(s.d_ctr.p, s.h_ctr.p, m * 8, hipMemcpyHostToDevice, sin), "H2D ctr");
-    } else {
-        RG_HIP(s.d_ctr_out.reserve(m * 8), "alloc ctr_out");
-        RG_HIP(s.h_ctr_out.reserve(m * 8), "alloc h_ctr_out");
-    }
     RG_HIP(hipEventRecord(s.ev_in, sin), "slice event");
     // the kernel on hs_run, once the inputs are in
     RG_HIP(hipStreamWaitEvent(srun, s.ev_in, 0), "slice wait");
@@ -810,22 +819,22 @@ int HostRun::step() {
         rg::SealArgs a{};
         a.keys = static_cast<const uint32_t *>(ctx->d_keys.p);
         a.receivers = with_receivers ? static_cast<const uint32_t *>(ctx->d_recv.p) : nullptr;
-        a.desc = static_cast<const rg_pkt_desc *>(s.d_desc.p);
-        a.counters = static_cast<const uint64_t *>(s.d_ctr.p);
+        a.desc = static_cast<const rg_pkt_desc *>(s.h_desc.d);
+        a.counters = static_cast<const uint64_t *>(s.h_ctr.d);
         a.buf = dbuf;
         a.buf_len = span;
-        a.status = static_cast<uint8_t *>(s.d_status.p);
+        a.status = static_cast<uint8_t *>(s.h_status.d);
         a.nkeys = nkeys;
         a.n = (uint32_t)m;
         RG_HIP(launch_seal_any(ctx, a, s.plan, srun), "seal launch");
     } else {
         rg::OpenArgs a{};
         a.keys = static_cast<const uint32_t *>(ctx->d_keys.p);
-        a.desc = static_cast<const rg_pkt_desc *>(s.d_desc.p);
+        a.desc = static_cast<const rg_pkt_desc *>(s.h_desc.d);
         a.buf = dbuf;
         a.buf_len = span;
-        a.status = static_cast<uint8_t *>(s.d_status.p);
-        a.counters_out = static_cast<uint64_t *>(s.d_ctr_out.p);
+        a.status = static_cast<uint8_t *>(s.h_status.d);
+        a.counters_out = static_cast<uint64_t *>(s.h_ctr_out.d);
         a.nkeys = nkeys;
         a.n = (uint32_t)m;
         RG_HIP(launch_open_any(ctx, a, s.plan, srun), "open launch");
@@ -834,8 +843,6 @@ int HostRun::step() {
     // downloads on hs_out, once the kernel is done
     RG_HIP(hipStreamWaitEvent(sout, s.ev_run, 0), "slice wait");
     if (span) RG_HIP(hipMemcpyAsync(buf + lo, s.d_buf.p, span, hipMemcpyDeviceToHost, sout), "D2H frames");
-    if (open) RG_HIP(hipMemcpyAsync(s.h_ctr_out.p, s.d_ctr_out.p, m * 8, hipMemcpyDeviceToHost, sout), "D2H ctr");
-    RG_HIP(hipMemcpyAsync(s.h_status.p, s.d_status.p, m, hipMemcpyDeviceToHost, sout), "D2H status");
     RG_HIP(hipEventRecord(s.ev_out, sout), "slice event");
     s.i0 = i;
     s.i1 = j;
