@@ -648,6 +648,36 @@ def test_host_path_matches_oracle(engine):
     assert np.array_equal(got[16:16 + int(desc[0]["len"])], buf[16:16 + int(desc[0]["len"])])
 
 
+def test_host_path_pinned_buffer_matches_oracle(engine):
+    """The caller's frames in pinned host memory (rg_host_alloc): downloads are host_store_kernel writes
+    over the link, not copies.  Several slices, and a last frame with P % 16 != 0 (INVALID by the
+    rg_aead.h contract, left as it came) whose bytes still lie in the last slice's span, so that the span
+    ends off a 16-byte boundary (the kernel's byte tail)."""
+    rng = np.random.default_rng(23)
+    n = 6000
+    keys, rec, desc, ctr, buf = _random_batch(rng, n, nkeys=5)
+    desc[-1]["len"] = 40  # the span's end is 8 bytes past a 16-byte boundary
+    want = buf.copy()
+    oracle.seal_batch(keys, rec, desc[:-1], ctr[:-1], want, nthreads=8)
+    got = aead.host_alloc(len(buf))
+    got[:] = buf
+    engine.set_host_slice(1 << 20)
+    try:
+        st = engine.seal_host(keys, rec, desc, ctr, got)
+        assert st[-1] == aead.PKT_INVALID and (st[:-1] == aead.PKT_OK).all()
+        assert np.array_equal(got, want)
+        od = desc[:-1].copy()
+        od["len"] += 32
+        ow = want.copy()
+        so_w, co_w = oracle.open_batch(keys, od, ow)
+        so, co = engine.open_host(keys, od, got)
+        assert (so == aead.PKT_OK).all() and np.array_equal(so, so_w) and np.array_equal(co, co_w)
+        assert np.array_equal(got, ow)
+    finally:
+        engine.set_host_slice(8 << 20)
+        del got
+
+
 # ------------------------------------------------------- full configurations
 @pytest.mark.parametrize("name", ["cfg2", "cfg3", "cfg4"])
 def test_full_config_digest(engine, name):
