@@ -560,7 +560,7 @@ template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) voi
             }
             if (j == 0) cut0 = 0;
             if (j + 1 == kgc) cut1 = kCoopGroup;
-            __syncthreads(); // the shared slots are read before any wave reuses them
+            // (no barrier after these reads: one unit per wave, so no wave writes the shared slots again)
             // the first sub-unit is staged from memory below (L2-resident: this workgroup just read it);
             // staging it from the four waves' registers into each other's images measured 2x slower
             s0 = g * kCoopGroup + cut0;
