@@ -465,13 +465,17 @@ __global__ __launch_bounds__(512) void tile_kernel(SealArgs sa, OpenArgs oa, Til
         // ---- chunk loop, software-pipelined: the keystream block of chunk c+1
         // is generated in the same basic block as the XOR / Poly1305 of chunk c
         // iterations: the longest segment of the wave (the last window may be partial)
-        uint32_t Cl = myC;
+        uint32_t Cl = myC, Cs = myC;
 #pragma unroll
         for (int m = 32; m >= 1; m >>= 1) {
-            const uint32_t o = __shfl_xor(Cl, m);
+            const uint32_t o = __shfl_xor(Cl, m), p = __shfl_xor(Cs, m);
             Cl = o > Cl ? o : Cl;
+            Cs = p < Cs ? p : Cs;
         }
         const uint32_t Cmax = uniform_u32(Cl);
+        // chunks c with c + 1 < Cmin are whole (four blocks) in every lane: their Poly1305 blocks need no
+        // predicate (20 v_cndmask per chunk fewer)
+        const uint32_t Cmin = uniform_u32(Cs);
         const uint32_t f = swz<G>(lane);
         // segments after the first also track q = r^{blocks absorbed} (one
         // more clamped multiply per block) for the combine below
@@ -540,30 +544,50 @@ __global__ __launch_bounds__(512) void tile_kernel(SealArgs sa, OpenArgs oa, Til
                 // XOR + write-back after double round 0, Poly1305 blocks after 1, 3, 5, 7
                 uint4 x0, x1, x2, x3;
                 uint32_t ksn[16];
-                stream_block_hooked(stm, c0 + c + 2, ksn, [&](int dr) {
-                    if (dr == 0) {
-                        x0 = xor4(m0, ksc + 0);
-                        x1 = xor4(m1, ksc + 4);
-                        x2 = xor4(m2, ksc + 8);
-                        x3 = xor4(m3, ksc + 12);
-                        lds4[sl0] = x0; // pieces outside the payload are never stored
-                        lds4[sl1] = x1;
-                        lds4[sl2] = x2;
-                        lds4[sl3] = x3;
-                    }
-                    if (dr == 1) acc_block_pred(acc, OPEN ? m0 : x0, r, cnt4 > 0);
-                    if (dr == 3) acc_block_pred(acc, OPEN ? m1 : x1, r, cnt4 > 1);
-                    if (dr == 5) acc_block_pred(acc, OPEN ? m2 : x2, r, cnt4 > 2);
-                    if (dr == 7) acc_block_pred(acc, OPEN ? m3 : x3, r, cnt4 > 3);
-                    if (dr % 2 == 1) pin_acc(acc);
-                    if constexpr (TRACK) {
-                        if (dr == 2) acc_mul_pred(pw, r, cnt4 > 0);
-                        if (dr == 4) acc_mul_pred(pw, r, cnt4 > 1);
-                        if (dr == 6) acc_mul_pred(pw, r, cnt4 > 2);
-                        if (dr == 8) acc_mul_pred(pw, r, cnt4 > 3);
-                        if (dr % 2 == 0 && dr > 0) pin_acc(pw);
-                    }
-                });
+                auto body = [&](auto full_tag) {
+                    constexpr bool FULL = decltype(full_tag)::value;
+                    stream_block_hooked(stm, c0 + c + 2, ksn, [&](int dr) {
+                        if (dr == 0) {
+                            x0 = xor4(m0, ksc + 0);
+                            x1 = xor4(m1, ksc + 4);
+                            x2 = xor4(m2, ksc + 8);
+                            x3 = xor4(m3, ksc + 12);
+                            lds4[sl0] = x0; // pieces outside the payload are never stored
+                            lds4[sl1] = x1;
+                            lds4[sl2] = x2;
+                            lds4[sl3] = x3;
+                        }
+                        if constexpr (FULL) {
+                            if (dr == 1) acc_block(acc, OPEN ? m0 : x0, r);
+                            if (dr == 3) acc_block(acc, OPEN ? m1 : x1, r);
+                            if (dr == 5) acc_block(acc, OPEN ? m2 : x2, r);
+                            if (dr == 7) acc_block(acc, OPEN ? m3 : x3, r);
+                        } else {
+                            if (dr == 1) acc_block_pred(acc, OPEN ? m0 : x0, r, cnt4 > 0);
+                            if (dr == 3) acc_block_pred(acc, OPEN ? m1 : x1, r, cnt4 > 1);
+                            if (dr == 5) acc_block_pred(acc, OPEN ? m2 : x2, r, cnt4 > 2);
+                            if (dr == 7) acc_block_pred(acc, OPEN ? m3 : x3, r, cnt4 > 3);
+                        }
+                        if (dr % 2 == 1) pin_acc(acc);
+                        if constexpr (TRACK) {
+                            if constexpr (FULL) {
+                                if (dr == 2) acc_mul(pw, r);
+                                if (dr == 4) acc_mul(pw, r);
+                                if (dr == 6) acc_mul(pw, r);
+                                if (dr == 8) acc_mul(pw, r);
+                            } else {
+                                if (dr == 2) acc_mul_pred(pw, r, cnt4 > 0);
+                                if (dr == 4) acc_mul_pred(pw, r, cnt4 > 1);
+                                if (dr == 6) acc_mul_pred(pw, r, cnt4 > 2);
+                                if (dr == 8) acc_mul_pred(pw, r, cnt4 > 3);
+                            }
+                            if (dr % 2 == 0 && dr > 0) pin_acc(pw);
+                        }
+                    });
+                };
+                // (seal only: the open kernel's second copy of the body spilled 9 more VGPRs)
+                if (!OPEN && c + 1 < Cmin) body(std::true_type{});
+                else body(std::false_type{});
 #pragma unroll
                 for (int t = 0; t < 16; ++t) ksc[t] = ksn[t];
             }
