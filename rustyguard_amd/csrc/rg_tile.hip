@@ -480,8 +480,11 @@ __global__ __launch_bounds__(512) void tile_kernel(SealArgs sa, OpenArgs oa, Til
         // segments after the first also track q = r^{blocks absorbed} (one
         // more clamped multiply per block) for the combine below
         Acc pw = {1, 0, 0, 0, 0};
-        auto run_chunks = [&](auto track_tag) {
+        auto run_chunks = [&](auto track_tag, auto whole_tag) {
         constexpr bool TRACK = decltype(track_tag)::value;
+        // WHOLE: every lane has the wave's Cmax chunks, so every chunk before the last is whole in every
+        // lane and absorbs its blocks unpredicated (a loop of its own: one body, no per-chunk choice)
+        constexpr bool WHOLE = decltype(whole_tag)::value;
         uint32_t ksc[16];
         if (Cmax > 0) stream_block(stm, c0 + 1, ksc);
         // Window schedule (wave-uniform): DMA(0), DMA(1) up front; before chunk c, wait for the
@@ -586,7 +589,8 @@ __global__ __launch_bounds__(512) void tile_kernel(SealArgs sa, OpenArgs oa, Til
                     });
                 };
                 // (seal only: the open kernel's second copy of the body spilled 9 more VGPRs)
-                if (!OPEN && c + 1 < Cmin) body(std::true_type{});
+                if constexpr (WHOLE) body(std::true_type{});
+                else if (!OPEN && c + 1 < Cmin) body(std::true_type{});
                 else body(std::false_type{});
 #pragma unroll
                 for (int t = 0; t < 16; ++t) ksc[t] = ksn[t];
@@ -612,8 +616,14 @@ __global__ __launch_bounds__(512) void tile_kernel(SealArgs sa, OpenArgs oa, Til
         }
         };
         const bool track = K > 1 && seg > 0; // wave-uniform
-        if (track) run_chunks(std::true_type{});
-        else run_chunks(std::false_type{});
+        const bool whole = Cmin == Cmax; // wave-uniform
+        if (track) {
+            if (whole) run_chunks(std::true_type{}, std::true_type{});
+            else run_chunks(std::true_type{}, std::false_type{});
+        } else {
+            if (whole) run_chunks(std::false_type{}, std::true_type{});
+            else run_chunks(std::false_type{}, std::false_type{});
+        }
         if constexpr (STAMP) {
             const uint64_t t = stamp();
             t_chunk += t - t_mark;
