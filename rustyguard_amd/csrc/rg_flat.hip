@@ -974,6 +974,11 @@ template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) voi
             }
             // carry = h r^pe for the packet the next lane continues (pe: its blocks after this lane's range,
             // from the end markers before phase C; square-and-multiply over the wave's largest exponent)
+            if (s.pb >= 0) { // the top bit: x = 1 squared is 1, so the first step is a choice of 1 or r
+                const bool bit = (s.pe >> s.pb) & 1u;
+                s.px = bit ? Acc{s.pr.r0, s.pr.r1, s.pr.r2, s.pr.r3, 0} : Acc{1, 0, 0, 0, 0};
+                --s.pb;
+            }
             while (s.pb >= 0) pow_step(s);
             if (ck != ~0u) {
                 Acc cv = s.h;
