@@ -50,3 +50,28 @@ def test_world_size_mismatch_is_an_error():
     assert "WORLD_SIZE=2" in r.stderr
     r = _run(["--gpus", "1", "--dry-run"], {"WORLD_SIZE": "8", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode == 2
+
+
+def test_pcie_ceiling_reads_the_duplex_tool(monkeypatch):
+    """`e2e.pcie_ceiling` takes tools/build/pcie's figures (run as a child process): the in-process copies on
+    two torch streams ran the directions one after the other (28.5 GB/s per direction against 47.7)."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(REPO, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    out = {"bytes": 100663296, "piece_bytes": 16777216,
+           "gb_s_per_direction": {"h2d_copy": 56.8, "d2h_copy": 56.4, "both_copies": 47.7,
+                                  "both_copies_16MiB_pieces": 46.7}}
+    seen = {}
+
+    def fake_run(cmd, **kw):
+        seen["cmd"] = cmd
+        return subprocess.CompletedProcess(cmd, 0, stdout="noise\n" + json.dumps(out) + "\n", stderr="")
+
+    monkeypatch.setattr(os.path, "exists", lambda p: True)
+    monkeypatch.setattr(subprocess, "run", fake_run)
+    got = bench.pcie_ceiling(96 << 20)
+    assert seen["cmd"][0].endswith(os.path.join("tools", "build", "pcie")) and seen["cmd"][1] == "96"
+    assert got["h2d_gb_s"] == 56.8 and got["d2h_gb_s"] == 56.4 and got["bidir_gb_s_per_dir"] == 47.7
+    assert got["bidir_16MiB_pieces_gb_s_per_dir"] == 46.7 and "lower_bound" not in got
