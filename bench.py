@@ -934,15 +934,18 @@ def pcie_ceiling(nbytes: int):
 
     tool = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools", "build", "pcie")
     if os.path.exists(tool):
-        p = subprocess.run([tool, str(max(1, nbytes >> 20))], capture_output=True, text=True, timeout=120)
-        if p.returncode == 0:
-            d = json.loads(p.stdout.strip().splitlines()[-1])
-            g = d["gb_s_per_direction"]
-            return {"h2d_gb_s": g["h2d_copy"], "d2h_gb_s": g["d2h_copy"], "bidir_gb_s_per_dir": g["both_copies"],
-                    "bidir_16MiB_pieces_gb_s_per_dir": g["both_copies_16MiB_pieces"], "bytes": d["bytes"],
-                    "how": "tools/build/pcie in a child process: hipMemcpyAsync on two non-blocking streams, "
-                           "hipHostMalloc buffers, HIP events"}
-        print(f"pcie tool failed ({p.returncode}): {p.stderr[-500:]}", file=sys.stderr)
+        try:
+            p = subprocess.run([tool, str(max(1, nbytes >> 20))], capture_output=True, text=True, timeout=120)
+            if p.returncode == 0:
+                d = json.loads(p.stdout.strip().splitlines()[-1])
+                g = d["gb_s_per_direction"]
+                return {"h2d_gb_s": g["h2d_copy"], "d2h_gb_s": g["d2h_copy"], "bidir_gb_s_per_dir": g["both_copies"],
+                        "bidir_16MiB_pieces_gb_s_per_dir": g["both_copies_16MiB_pieces"], "bytes": d["bytes"],
+                        "how": "tools/build/pcie in a child process: hipMemcpyAsync on two non-blocking streams, "
+                               "hipHostMalloc buffers, HIP events"}
+            print(f"pcie tool failed ({p.returncode}): {p.stderr[-500:]}", file=sys.stderr)
+        except (OSError, subprocess.SubprocessError, ValueError, KeyError, IndexError) as e:
+            print(f"pcie tool failed: {e!r}", file=sys.stderr)
     return dict(_pcie_in_process(nbytes), lower_bound=True)
 
 
