@@ -4,8 +4,9 @@ set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-/usr/bin/time -v timeout -k 10 400 python bench.py > gpurun_out/r4_default_noflags.jsonl 2> gpurun_out/r4_default_noflags.err
+t0=$(date +%s)
+timeout -k 10 400 python bench.py > gpurun_out/r4_default_noflags.jsonl 2> gpurun_out/r4_default_noflags.err
 rc=$?
-grep -E "Elapsed|Maximum resident" gpurun_out/r4_default_noflags.err
+echo "wall $(( $(date +%s) - t0 )) s, rc $rc"
 python3 -c "import json; d=json.loads(open('gpurun_out/r4_default_noflags.jsonl').read().strip().splitlines()[-1]); print(d['value'], d.get('e2e'))"
 exit $rc
