@@ -87,9 +87,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="CPU baseline budget: port and OpenSSL, 1 thread and all cores, 5 runs each (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="all-core thread count (0 = this host's share)")
-    ap.add_argument("--e2e", action="store_true",
-                    help="also time the pinned host->GPU->host path (on by default for a one-GPU config-2 line)")
-    ap.add_argument("--no-e2e", action="store_true", help="skip the host path on the default line")
+    ap.add_argument("--e2e", action="store_true", help="also time the pinned host->GPU->host path")
     ap.add_argument("--single-process", action="store_true",
                     help="one process and one thread drive all --gpus N GPUs (rg_group: config 5's split, "
                          "rg_{seal,open}_batch_dev_multi) instead of one rank per GPU")
@@ -884,9 +882,10 @@ def main():
         out["cold_cache"] = cold
     if forged:
         out["forged_open"] = forged
-    # the host path (never `value`): on by default for the N = 1 config-2 line, so that the driver's own run
-    # records it beside the device-resident rate; a failure there is reported, not fatal
-    if rank == 0 and (args.e2e or (world == 1 and workload == "cfg2" and not args.no_e2e)):
+    # the host path (never `value`), on request: its 8 MiB slice launches would otherwise sit in a rocprofv3
+    # summary of the default command beside the batch launches the roofline is quoted on (round 4:
+    # profiles/r4_default_kernel_stats.csv, average 62 us against 78 us); a failure there is reported, not fatal
+    if rank == 0 and args.e2e:
         try:
             out["e2e"] = e2e_host(eng, w, b)
         except Exception as e:  # noqa: BLE001 -- an auxiliary leg: the line stands without it
