@@ -390,7 +390,10 @@ int rg_open_batch_host_multi(rg_group *g, const uint8_t *keys, uint32_t nkeys, c
                              uint8_t *buf, size_t buf_len, uint8_t *status, uint64_t *counters_out);
 /* Device-resident shards: shard i lives on context i's device (its own keys, descriptors, frames,
  * statuses and stream there); rg_seal_batch_dev / rg_open_batch_dev enqueued for every shard, from
- * this thread, without waiting (counters_out and receivers may be NULL as there). */
+ * this thread, without waiting (counters_out and receivers may be NULL as there).  Every shard's
+ * arguments are checked before any shard is enqueued: RG_EINVAL names the bad shard and nothing ran.
+ * A launch that fails after the checks (a device error) returns its code with rg_last_error naming
+ * the shard k; shards 0..k-1 are enqueued, k and later are not. */
 typedef struct rg_dev_shard {
     const uint8_t *keys;
     const uint32_t *receivers; /* seal only */

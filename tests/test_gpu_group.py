@@ -4,8 +4,12 @@ per-peer endpoint record (rg_sessions_insert_peer).
 The reference's host is one thread owning one Sessions (rustyguard-core/src/lib.rs:349-352); a group
 splits each batch into contiguous ranges over its contexts and runs their pipelines from that thread.
 Packets are independent, so every result must equal the one-context / oracle result
-byte for byte.  These tests put N = 2 and 4 contexts on device 0 (one GPU is enough to run every code
-path: streams, splits, the round-robin issue, the gather)."""
+byte for byte.  The groups: N = 2 and 4 contexts on device 0 (one GPU runs every code path: streams,
+splits, the round-robin issue, the gather) and, on a box with several GPUs, one context on each
+visible device and contexts alternating over devices 0 and 1 (per-device streams,
+hipSetDevice switching and pinned buffers of another device's context then run too)."""
+import ctypes
+
 import numpy as np
 import pytest
 import torch
@@ -17,13 +21,35 @@ from rustyguard_amd.workloads import DESC_DTYPE
 
 pytestmark = pytest.mark.gpu
 S = 1_000_000_000
+NDEV = torch.cuda.device_count()  # counting devices does not initialise the GPU on this image
+
+GROUPS = {"2x dev0": [0, 0], "4x dev0": [0, 0, 0, 0],
+          "all devices": list(range(NDEV)), "alternating 0,1": [0, 1, 0, 1]}
 
 
-@pytest.fixture(scope="module", params=[2, 4])
+@pytest.fixture(scope="module", params=list(GROUPS))
 def group(request):
-    g = Group([0] * request.param)
+    devs = GROUPS[request.param]
+    if max(devs, default=0) >= NDEV or (request.param == "all devices" and NDEV < 2):
+        pytest.skip(f"needs {max(devs) + 1 if devs else 2} GPUs, {NDEV} visible")
+    g = Group(devs)
     yield g
     g.close()
+
+
+def _hip():
+    for name in ("libamdhip64.so.7", "libamdhip64.so.6", "libamdhip64.so"):
+        try:
+            return ctypes.CDLL(name)  # the runtime torch already loaded (same soname)
+        except OSError:
+            continue
+    raise OSError("libamdhip64 not found")
+
+
+def hip_get_device() -> int:
+    d = ctypes.c_int(-1)
+    assert _hip().hipGetDevice(ctypes.byref(d)) == 0
+    return d.value
 
 
 def _ragged(rng, n, keys=5):
@@ -100,31 +126,39 @@ def test_group_device_shards(group):
     b = aead.split_batch(desc, len(group))
     want = buf.copy()
     oracle.seal_batch(kt, rec, desc, ctr, want)
-    streams = [torch.cuda.Stream() for _ in range(len(group))]
+    devs = group.devices
+    streams = [torch.cuda.Stream(device=devs[k]) for k in range(len(group))]
     shards = []
     for k in range(len(group)):
         d = desc[b[k]:b[k + 1]].copy()
-        shards.append({"keys": torch.from_numpy(kt.reshape(-1)).cuda(), "receivers": torch.from_numpy(rec).cuda(),
-                       "desc": torch.from_numpy(d.view(np.uint8)).cuda(), "counters": torch.from_numpy(ctr[b[k]:b[k + 1]].copy()).cuda(),
-                       "buf": torch.from_numpy(buf.copy()).cuda(), "status": torch.zeros(max(len(d), 1), dtype=torch.uint8, device="cuda"),
+        dv = f"cuda:{devs[k]}"
+        shards.append({"keys": torch.from_numpy(kt.reshape(-1)).to(dv), "receivers": torch.from_numpy(rec).to(dv),
+                       "desc": torch.from_numpy(d.view(np.uint8)).to(dv),
+                       "counters": torch.from_numpy(ctr[b[k]:b[k + 1]].copy()).to(dv),
+                       "buf": torch.from_numpy(buf.copy()).to(dv),
+                       "status": torch.full((max(len(d), 1),), 0xEE, dtype=torch.uint8, device=dv),
                        "stream": streams[k]})
-    torch.cuda.synchronize()
+    _sync_all(devs)
     group.seal_dev(shards)
-    torch.cuda.synchronize()
+    _sync_all(devs)
+    fams = [group.engine(k).last_kernel() for k in range(len(group))]
     for k, sh in enumerate(shards):
         got = sh["buf"].cpu().numpy()
-        assert (sh["status"].cpu().numpy()[: b[k + 1] - b[k]] == 0).all()
-        for i in range(b[k], b[k + 1]):
-            o, p = int(desc[i]["offset"]), int(desc[i]["len"]) + 32
-            assert np.array_equal(got[o:o + p], want[o:o + p]), i
-    for sh in shards:
+        st = sh["status"].cpu().numpy()[: b[k + 1] - b[k]]
+        bad = [i for i in range(b[k], b[k + 1]) if not np.array_equal(
+            got[int(desc[i]["offset"]):int(desc[i]["offset"]) + int(desc[i]["len"]) + 32],
+            want[int(desc[i]["offset"]):int(desc[i]["offset"]) + int(desc[i]["len"]) + 32])]
+        assert (st == 0).all() and not bad, (f"shard {k} of {len(group)} [{b[k]}, {b[k + 1]}) family {fams[k]}: "
+                                             f"statuses {np.unique(st, return_counts=True)}, {len(bad)} frames "
+                                             f"differ, first {bad[:8]}, sizes {[int(desc[i]['len']) for i in bad[:8]]}")
+    for k, sh in enumerate(shards):
         od = sh["desc"].cpu().numpy().view(DESC_DTYPE).copy()
         od["len"] += 32
-        sh["desc"] = torch.from_numpy(od.view(np.uint8)).cuda()
-        sh["counters_out"] = torch.zeros(len(od), dtype=torch.int64, device="cuda")
-    torch.cuda.synchronize()
+        sh["desc"] = torch.from_numpy(od.view(np.uint8)).to(f"cuda:{devs[k]}")
+        sh["counters_out"] = torch.zeros(len(od), dtype=torch.int64, device=f"cuda:{devs[k]}")
+    _sync_all(devs)
     group.open_dev(shards)
-    torch.cuda.synchronize()
+    _sync_all(devs)
     for k, sh in enumerate(shards):
         assert (sh["status"].cpu().numpy()[: b[k + 1] - b[k]] == 0).all()
         assert np.array_equal(sh["counters_out"].cpu().numpy().astype(np.uint64), ctr[b[k]:b[k + 1]])
@@ -132,6 +166,70 @@ def test_group_device_shards(group):
         for i in range(b[k], b[k + 1]):
             o, p = int(desc[i]["offset"]), int(desc[i]["len"]) + 32
             assert np.array_equal(got[o + 16:o + p - 16], buf[o + 16:o + p - 16]), i
+
+
+def _sync_all(devs):
+    for d in sorted(set(devs)):
+        torch.cuda.synchronize(d)
+
+
+def test_group_calls_leave_the_current_device_selected(group):
+    """every group call selects each context's device in turn and puts the caller's
+    current HIP device back (hipGetDevice read through the HIP runtime itself, not torch's view of it),
+    whichever device the caller had selected -- also after a call that fails."""
+    rng = np.random.default_rng(3)
+    kt, rec, desc, ctr, buf = _ragged(rng, 600)
+    od = desc.copy()
+    od["len"] += 32
+    for cur in sorted(set(group.devices)):
+        torch.cuda.set_device(cur)
+        assert hip_get_device() == cur
+        group.seal_host(kt, rec, desc, ctr, buf)
+        assert hip_get_device() == cur, "seal_host_multi"
+        group.open_host(kt, od, buf)
+        assert hip_get_device() == cur, "open_host_multi"
+        a = Sessions(group, 4)
+        s0 = a.insert(1, 2, bytes(range(32)), bytes(range(32, 64)))
+        a.send_batch([s0] * 3, desc[:3].copy(), buf.copy())
+        assert hip_get_device() == cur, "send_batch on a group"
+        bad = (aead._DevShard * len(group))()
+        for x in bad:
+            x.n = 1  # one packet, no buffers: refused by the shard check before anything runs
+        with pytest.raises(Exception):
+            group.seal_dev(bad)
+        assert hip_get_device() == cur, "failed seal_dev_multi"
+        del a
+    torch.cuda.set_device(0)
+
+
+def test_dev_multi_checks_every_shard_before_enqueuing(group):
+    """a bad argument in the LAST shard is refused before shard 0 is enqueued (its statuses stay
+    at the sentinel), and the error names the shard."""
+    from rustyguard_amd import _lib
+
+    rng = np.random.default_rng(4)
+    kt, rec, desc, ctr, buf = _ragged(rng, 200)
+    shards = []
+    for k, dv in enumerate(group.devices):
+        t = f"cuda:{dv}"
+        shards.append({"keys": torch.from_numpy(kt.reshape(-1)).to(t), "receivers": torch.from_numpy(rec).to(t),
+                       "desc": torch.from_numpy(desc.view(np.uint8)).to(t), "counters": torch.from_numpy(ctr).to(t),
+                       "buf": torch.from_numpy(buf.copy()).to(t),
+                       "status": torch.full((len(desc),), 0xEE, dtype=torch.uint8, device=t),
+                       "stream": torch.cuda.Stream(device=dv)})
+    arr = Group.shards(shards, True)
+    arr[len(group) - 1].counters = None  # seal needs counters
+    _sync_all(group.devices)
+    with pytest.raises(_lib.RgError) as ei:
+        group.seal_dev(arr)
+    assert f"shard {len(group) - 1}" in str(ei.value) and "nothing enqueued" in str(ei.value)
+    _sync_all(group.devices)
+    for sh in shards:
+        assert (sh["status"] == 0xEE).all().item(), "a shard ran although the call was refused"
+    group.seal_dev(Group.shards(shards, True))  # the same shards, valid: every one runs
+    _sync_all(group.devices)
+    for sh in shards:
+        assert (sh["status"] == 0).all().item()
 
 
 def _keys(seed):
