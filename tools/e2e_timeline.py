@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Round 4: the host path's timeline from a rocprofv3 --kernel-trace --memory-copy-trace run of
-tools/e2e_probe.py (tools/call_r4_e2etrace.sh): for the last seal call, every H2D copy, kernel and D2H
+tools/e2e_probe.py (tools/recipes.sh r4_e2etrace): for the last seal call, every H2D copy, kernel and D2H
 blit in start order, relative to the call's first copy, with the gaps on each engine.
    usage: tools/e2e_timeline.py DIR [KERNEL_SUBSTRING]"""
 import csv
