@@ -926,16 +926,16 @@ RG_BENCH_SHARE_GPU=1 timeout -k 10 400 python bench.py --single-process --gpus 2
 
 recipe_r5_e2eenv() {
 # Round 5: which engine carries the host path's download.  tools/e2e_probe.py (cfg2,
-# 8 MiB slices) under runtime settings that may move the D2H copy off the shader blit kernel, then a
-# kernel + copy trace of each setting (which engine: a D2H memory-copy record = SDMA, a copyBuffer
-# kernel = blit).
+# 8 MiB slices) under runtime settings that may move the D2H copy off the shader blit kernel, each with a
+# kernel + memory-copy trace (a D2H memory-copy record = SDMA, a __amd_rocclr_copyBuffer kernel = blit).
 mkdir -p gpurun_out/e2eenv
-export HSA_ENABLE_IPC_MODE_LEGACY=0
-for cfg in "base" "GPU_FORCE_BLIT_COPY_SIZE=0" "DEBUG_CLR_LIMIT_BLIT_WG=16" "DEBUG_CLR_LIMIT_BLIT_WG=64" "GPU_CP_DMA_COPY_SIZE=0"; do
-    if [ "$cfg" = base ]; then envs=(); else envs=("$cfg"); fi
+for cfg in base GPU_FORCE_BLIT_COPY_SIZE=0 DEBUG_CLR_LIMIT_BLIT_WG=16 DEBUG_CLR_LIMIT_BLIT_WG=64 GPU_CP_DMA_COPY_SIZE=0; do
     echo "== $cfg"
-    env "${envs[@]}" timeout -k 10 120 python3 tools/e2e_probe.py cfg2 8 > gpurun_out/e2eenv/$cfg.log 2>&1 || { echo "rc=$?"; tail -5 gpurun_out/e2eenv/$cfg.log; exit 1; }
-    tail -1 gpurun_out/e2eenv/$cfg.log
+    if [ "$cfg" = base ]; then envs=(X_RG_NONE=1); else envs=("$cfg"); fi
+    env "${envs[@]}" timeout -k 10 120 python3 tools/e2e_probe.py cfg2 8 > "gpurun_out/e2eenv/$cfg.log" 2>&1 || { echo "rc=$?"; tail -5 "gpurun_out/e2eenv/$cfg.log"; return 1; }
+    tail -1 "gpurun_out/e2eenv/$cfg.log"
+    env "${envs[@]}" timeout -k 10 150 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d "gpurun_out/e2eenv/tr_$cfg" -o run -- python3 tools/e2e_probe.py cfg2 8 > "gpurun_out/e2eenv/tr_$cfg.log" 2>&1 || { echo "trace rc=$?"; return 1; }
+    python3 tools/e2e_timeline.py "gpurun_out/e2eenv/tr_$cfg" seal 2>&1 | tail -14
 done
 }
 
@@ -1068,6 +1068,96 @@ G="bash tools/gpu_run.sh"
 for W in cfg2 cfg3 cfg4 cfg5; do RG_WORKLOAD=$W $G pmc_hbm || exit $?; done
 RG_WORKLOADS="cfg2 cfg3 cfg4" $G valu || exit $?
 echo "round profiles B done"
+}
+
+recipe_r5_hostpoll() {
+# Round 5: the host path's chain.  The round-4 HIP API trace shows every slice's kernel
+# and download reaching the GPU only at the host thread's next HIP call after a blocking hipEventSynchronize
+# (deferred submission of commands behind a cross-stream event).  A/B: the thread polls hipEventQuery
+# instead of blocking (tools/build/librg_poll.so, -DRG_HOST_POLL=1) against the in-tree build, interleaved,
+# then a kernel + copy + HIP API trace of the poll build.
+mkdir -p gpurun_out/hostpoll
+for rep in 1 2; do
+    for lib in base poll; do
+        if [ $lib = base ]; then L=(X_RG_NONE=1); else L=(RG_AEAD_LIB=tools/build/librg_$lib.so); fi
+        env "${L[@]}" timeout -k 10 120 python3 tools/e2e_probe.py cfg2 4,8,16 > gpurun_out/hostpoll/${lib}_$rep.jsonl 2>&1 || { echo "rc=$?"; tail -3 gpurun_out/hostpoll/${lib}_$rep.jsonl; return 1; }
+        echo "== $lib $rep"; cat gpurun_out/hostpoll/${lib}_$rep.jsonl
+    done
+done
+RG_AEAD_LIB=tools/build/librg_poll.so timeout -k 10 150 rocprofv3 --hip-trace --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/hostpoll/tr -o run -- python3 tools/e2e_probe.py cfg2 8 > gpurun_out/hostpoll/tr.log 2>&1 || { echo "trace rc=$?"; return 1; }
+python3 tools/e2e_timeline.py gpurun_out/hostpoll/tr seal 2>&1 | tail -16
+}
+
+recipe_r5_hostup() {
+# Round 5: the host path's upload chain.  Polling instead of a blocking wait changed nothing
+# (r5_hostpoll): consecutive 8 MiB uploads on one stream leave ~33 us gaps, and each slice's kernel
+# starts with the NEXT upload, ~35 us after its own upload ended.  A/B of one upload stream per slot
+# (up1) and of the kernel in its upload's stream as well (up2) against the in-tree build, interleaved,
+# with a trace of each variant.
+mkdir -p gpurun_out/hostup
+for rep in 1 2; do
+    for lib in base up1 up2; do
+        if [ $lib = base ]; then L=(X_RG_NONE=1); else L=(RG_AEAD_LIB=tools/build/librg_$lib.so); fi
+        env "${L[@]}" timeout -k 10 120 python3 tools/e2e_probe.py cfg2 4,8,16 > gpurun_out/hostup/${lib}_$rep.jsonl 2>&1 || { echo "rc=$?"; tail -3 gpurun_out/hostup/${lib}_$rep.jsonl; return 1; }
+        echo "== $lib $rep"; grep slice gpurun_out/hostup/${lib}_$rep.jsonl
+    done
+done
+for lib in up1 up2; do
+    RG_AEAD_LIB=tools/build/librg_$lib.so timeout -k 10 150 rocprofv3 --hip-trace --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/hostup/tr_$lib -o run -- python3 tools/e2e_probe.py cfg2 8 > gpurun_out/hostup/tr_$lib.log 2>&1 || { echo "trace rc=$?"; return 1; }
+    echo "== trace $lib"; python3 tools/e2e_timeline.py gpurun_out/hostup/tr_$lib seal 2>&1 | tail -14
+done
+}
+
+recipe_r5_hostslots() {
+# Round 5: per-slot upload streams moved nothing (r5_hostup): in their trace each upload starts ~35 us
+# after the download three slices back ends -- the slot it reuses.  A/B of 4 and 6 slots (s4, s6) and of 6
+# slots with one upload stream each (s6up) against the in-tree 3-slot build, then a trace of s6.
+mkdir -p gpurun_out/hostslots
+for rep in 1 2; do
+    for lib in base s4 s6 s6up; do
+        if [ $lib = base ]; then L=(X_RG_NONE=1); else L=(RG_AEAD_LIB=tools/build/librg_$lib.so); fi
+        env "${L[@]}" timeout -k 10 120 python3 tools/e2e_probe.py cfg2 2,4,8,16 > gpurun_out/hostslots/${lib}_$rep.jsonl 2>&1 || { echo "rc=$?"; tail -3 gpurun_out/hostslots/${lib}_$rep.jsonl; return 1; }
+        echo "== $lib $rep"; grep slice gpurun_out/hostslots/${lib}_$rep.jsonl
+    done
+done
+RG_AEAD_LIB=tools/build/librg_s6.so timeout -k 10 150 rocprofv3 --hip-trace --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/hostslots/tr_s6 -o run -- python3 tools/e2e_probe.py cfg2 8 > gpurun_out/hostslots/tr_s6.log 2>&1 || { echo "trace rc=$?"; return 1; }
+python3 tools/e2e_timeline.py gpurun_out/hostslots/tr_s6 seal 2>&1 | tail -14
+}
+
+recipe_r5_hostalloc() {
+# Round 5: more slots made the host path slower, and a trace of six slots shows each slice's kernel and
+# the next upload released only when the previous download (a __amd_rocclr_copyBuffer shader blit) ends.
+# Does the caller's host allocation decide the download's engine?  tools/e2e_probe.py with the frames in
+# hipHostMalloc buffers of other flags (coherent, non-coherent, mapped+portable, write-combined; variant
+# libraries' rg_host_alloc) against the default, then a trace of each.
+mkdir -p gpurun_out/hostalloc
+for lib in base hcoh hnc hmap hwc; do
+    if [ $lib = base ]; then L=(X_RG_NONE=1); else L=(RG_AEAD_LIB=tools/build/librg_$lib.so); fi
+    env "${L[@]}" timeout -k 10 120 python3 tools/e2e_probe.py cfg2 8,16 > gpurun_out/hostalloc/$lib.jsonl 2>&1 || { echo "rc=$?"; tail -3 gpurun_out/hostalloc/$lib.jsonl; return 1; }
+    echo "== $lib"; grep slice gpurun_out/hostalloc/$lib.jsonl
+    env "${L[@]}" timeout -k 10 150 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/hostalloc/tr_$lib -o run -- python3 tools/e2e_probe.py cfg2 8 > gpurun_out/hostalloc/tr_$lib.log 2>&1 || { echo "trace rc=$?"; return 1; }
+    python3 tools/e2e_timeline.py gpurun_out/hostalloc/tr_$lib seal 2>&1 | tail -7
+done
+}
+
+recipe_r5_hostev() {
+# Round 5: in the round-4 API trace the host's wait for slot k-3's download event returns only when the
+# download of slice k-2 ends: the event recorded behind a download seems to complete with the NEXT
+# packet of that stream, so the three-slot pipeline runs two deep.  A/B: events with timing (ev1), a
+# hipStreamQuery of the download stream after each record (ev2), an empty kernel behind each record
+# (ev3), against the in-tree build, interleaved; then the HIP API + kernel + copy trace of each.
+mkdir -p gpurun_out/hostev
+for rep in 1 2; do
+    for lib in base ev1 ev2 ev3; do
+        if [ $lib = base ]; then L=(X_RG_NONE=1); else L=(RG_AEAD_LIB=tools/build/librg_$lib.so); fi
+        env "${L[@]}" timeout -k 10 120 python3 tools/e2e_probe.py cfg2 4,8,16 > gpurun_out/hostev/${lib}_$rep.jsonl 2>&1 || { echo "rc=$?"; tail -3 gpurun_out/hostev/${lib}_$rep.jsonl; return 1; }
+        echo "== $lib $rep"; grep slice gpurun_out/hostev/${lib}_$rep.jsonl
+    done
+done
+for lib in ev1 ev3; do
+    RG_AEAD_LIB=tools/build/librg_$lib.so timeout -k 10 150 rocprofv3 --hip-trace --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/hostev/tr_$lib -o run -- python3 tools/e2e_probe.py cfg2 8 > gpurun_out/hostev/tr_$lib.log 2>&1 || { echo "trace rc=$?"; return 1; }
+    echo "== trace $lib"; python3 tools/e2e_timeline.py gpurun_out/hostev/tr_$lib seal 2>&1 | tail -8
+done
 }
 
 if [ "${1:-}" = "--list" ] || [ $# -eq 0 ]; then
