@@ -89,6 +89,14 @@ __host__ __device__ __forceinline__ uint32_t class_hi(uint32_t c) {
     const uint32_t j = c - 17;
     return (j & 1u) ? (1u << (j / 2 + 5)) : (3u << (j / 2 + 3));
 }
+// size class of a packet of `chunks` 64-byte chunks (the planner's lists; the flattened kernel's deal)
+__device__ __forceinline__ uint32_t class_of(uint32_t chunks) {
+    if (chunks <= 16) return chunks;
+    uint32_t c = 17;
+    while (c < kClasses - 1 && class_hi(c) < chunks) ++c;
+    return c;
+}
+
 struct TilePlan {
     const uint32_t *counts; // [kClasses] packets per class, then [kClasses] = finished-workgroup count
     const uint32_t *lists;  // [kClasses][cap] packet indices

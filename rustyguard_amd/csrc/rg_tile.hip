@@ -35,12 +35,7 @@ namespace rg {
 
 // ------------------------------------------------------------ size classes
 
-__device__ __forceinline__ uint32_t class_of(uint32_t chunks) {
-    if (chunks <= 16) return chunks;
-    uint32_t c = 17;
-    while (c < kClasses - 1 && class_hi(c) < chunks) ++c;
-    return c;
-}
+// class_of: rg_internal.h
 
 // Each workgroup classifies kPlanPer x 256 consecutive packets: per wave and
 // class one ballot -> one LDS atomic (runs of consecutive packets stay

@@ -501,12 +501,13 @@ def test_flat_far_and_empty_descriptors_vs_oracle(engine, plan):
     _reset(engine)
 
 
-@pytest.mark.parametrize("n", [16384, 65536])
+@pytest.mark.parametrize("n", [4096, 16384, 65536, 131072])
 def test_flat_coop_search_vs_oracle(engine, n):
-    """Round 3: when n is a multiple of 4096 and the units of a 4096-packet group are a multiple of four
-    (CUs x 4 units), the four waves of a workgroup cut their units together (rg_flat.hip, A.coop).
-    Random sizes 0..2048 B over three keys, 40 forged frames: every byte and status against the
-    oracle."""
+    """When n is a multiple of 4096 and the units of a 4096-packet group are a multiple of four (CUs x 4
+    units), the four waves of a workgroup cut their units together (rg_flat.hip, A.coop): ~4, 16, 64 and
+    128 packets per unit here (the last with sub-units and lane-quad key blocks).  Random sizes 0..2048 B
+    over three keys, descriptors that fail their checks (far offsets, unaligned lengths) among them (round
+    5), 40 forged frames: every byte and status against the oracle."""
     import torch
 
     units = 4 * torch.cuda.get_device_properties(0).multi_processor_count
@@ -516,22 +517,31 @@ def test_flat_coop_search_vs_oracle(engine, n):
     engine.set_plan(1)
     rng = np.random.default_rng(n)
     keys, rec, desc, ctr, buf = _random_batch(rng, n, nkeys=3)
+    bad = rng.choice(n, 24, replace=False)
+    for j, i in enumerate(bad):
+        if j % 2:
+            desc[i]["offset"] = 1 << 40
+        else:
+            desc[i]["len"] = 17
+    good = np.ones(n, bool)
+    good[bad] = False
     want = buf.copy()
-    oracle.seal_batch(keys, rec, desc, ctr, want, nthreads=8)
+    oracle.seal_batch(keys, rec, desc[good], ctr[good], want, nthreads=8)
     got, st = _gpu_seal(engine, keys, rec, desc, ctr, buf)
-    assert (st == aead.PKT_OK).all()
+    assert (st[good] == aead.PKT_OK).all() and (st[bad] == aead.PKT_INVALID).all()
     assert np.array_equal(got, want)
     od = desc.copy()
     od["len"] += 32
-    forged = rng.choice(n, 40, replace=False)
+    forged = rng.choice(np.nonzero(good)[0], 40, replace=False)
     tampered = got.copy()
     for i in forged:
         tampered[int(od[i]["offset"]) + int(od[i]["len"]) - 1] ^= 1
-    back, st, co = _gpu_open(engine, keys, od, tampered)
+    back, st, co = _gpu_open(engine, keys, od, tampered)  # all n descriptors: the cooperative deal again
     want_back = tampered.copy()
-    wst, wctr = oracle.open_batch(keys, od, want_back, nthreads=8)
-    assert np.array_equal(st, wst) and (wst[forged] == oracle.DECRYPT_ERR).all()
-    assert np.array_equal(co[wst == 0], wctr[wst == 0])
+    wst, wctr = oracle.open_batch(keys, od[good], want_back, nthreads=8)
+    assert np.array_equal(st[good], wst) and (st[bad] != aead.PKT_OK).all()
+    assert (wst[np.searchsorted(np.nonzero(good)[0], forged)] == oracle.DECRYPT_ERR).all()
+    assert np.array_equal(co[good][wst == 0], wctr[wst == 0])
     assert np.array_equal(back, want_back)
     _reset(engine)
 

@@ -75,12 +75,14 @@ for op in ("seal", "open"):
         out["wall_us_end_pct_0_50_90_100"] = [round(float(x), 2) for x in np.percentile(rt[:, 1] - r0, [0, 50, 90, 100])]
         out["clock_ghz"] = round(float(rel[:, 7].sum() / ((rt[:, 1] - rt[:, 0]).sum() * 1e3)), 3)
     if (sub[:, 5] != 0).any():
-        # search steps: coop entry (kernel arguments, setup), descriptor loads + LDS transpose, prefix and
-        # wave total, first barrier, cut counts, second barrier
+        # search steps (round 5, the cooperative deal): entry (kernel arguments, setup), length loads and
+        # size classes, ranks within the classes, first barrier, sorted positions and the unit lists,
+        # second barrier.  (Round 4's contiguous cuts: entry, descriptor loads + LDS transpose, prefix,
+        # first barrier, cut counts, second barrier -- the same six stamp slots.)
         okw = (sub != 0).all(axis=1) & (sub_t0[:, 0] != 0)
         st = np.concatenate([sub_t0[okw], sub[okw]], axis=1)
         dl = np.diff(st, axis=1)
-        nm = ["entry", "desc_loads+transpose", "prefix", "barrier1", "cuts", "barrier2"]
+        nm = ["entry", "len_loads+classes", "class_ranks", "barrier1", "positions+lists", "barrier2"]
         out["search_steps"] = {k: {"mean_cyc": int(dl[:, i].mean()), "max_cyc": int(dl[:, i].max())}
                                for i, k in enumerate(nm)}
     res[op] = out

@@ -1160,6 +1160,24 @@ for lib in ev1 ev3; do
 done
 }
 
+recipe_r5_deal() {
+# Round 5: the flattened kernel's units dealt in size order, snake-wise (every unit 4096 / kgc packets; config
+# 3: 64) instead of contiguous cuts: flat / forged / digest / coop GPU tests, interleaved A/B against the
+# committed build (tools/build_rev.sh head) on config 3, per-wave phases of the diag build, the splitbench
+# two-chain Poly1305 variants.
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_forged.py -x -q -m gpu \
+    -k "flat or open_failures or bad_descriptors or malformed or digest or auto or coop" --timeout 300 --timeout-method thread \
+    > gpurun_out/r5_deal_tests.log 2>&1
+rc=$?
+tail -3 gpurun_out/r5_deal_tests.log
+[ $rc -eq 0 ] || return $rc
+bash tools/ab.sh "base head" "cfg3" 3 --no-cold --forged 0 || return $?
+RG_AEAD_LIB=tools/build/librg_diag.so timeout -k 10 200 python tools/flat_stamps.py --workload cfg3 --per-wave > gpurun_out/r5_cfg3_perwave.txt 2>&1 && tail -6 gpurun_out/r5_cfg3_perwave.txt | cut -c1-1500 || return $?
+[ -n "${R5_SPLIT:-}" ] && { timeout -k 10 60 tools/build/splitbench > gpurun_out/r5_splitbench.json && cat gpurun_out/r5_splitbench.json; }
+[ -n "${R5_PMC:-}" ] && { RG_WORKLOAD=cfg3 bash tools/gpu_run.sh pmc_hbm || return $?; }
+return 0
+}
+
 if [ "${1:-}" = "--list" ] || [ $# -eq 0 ]; then
     grep -A1 '^recipe_[a-z0-9_]*() {' "$SELF" | sed -n 's/^recipe_\([a-z0-9_]*\)() {/\1/p;s/^# \(.*\)/    \1/p'
     exit 0
