@@ -255,10 +255,12 @@ struct PlanBuf {
         h_classes = nullptr;
         d_classes = nullptr;
     }
-    // auto mode: plan unless the last planned batch held a single size class;
-    // re-check every 32nd call
-    bool want_plan() {
-        const bool check = (calls++ % 32) == 0;
+    // auto mode: plan unless the last planned batch held a single size class; re-check every 32nd call,
+    // but never inside a stream capture (a captured graph replays the route it captured: a re-check
+    // captured there would plan a uniform batch on every replay -- a bench warm-up count of 16 would
+    // have put it in the timed graph)
+    bool want_plan(hipStream_t st) {
+        const bool check = (calls++ % 32) == 0 && !capturing(st);
         return check || !h_classes || *h_classes != 1u;
     }
 };
@@ -560,7 +562,7 @@ static hipError_t launch_tiles_any(rg_ctx *ctx, const rg::SealArgs *sa, const rg
     if (ctx->plan == 2) {
         hipError_t e = pb.reserve(n, st);
         if (e != hipSuccess) return e;
-        plan = pb.want_plan();
+        plan = pb.want_plan(st);
     }
     if (plan) {
         hipError_t e = pb.reserve(n, st);
@@ -586,7 +588,7 @@ static hipError_t launch_pipe_any(rg_ctx *ctx, const rg::SealArgs *sa, const rg:
     if (ctx->plan == 2) {
         hipError_t e = pb.reserve(n, st);
         if (e != hipSuccess) return e;
-        plan = pb.want_plan();
+        plan = pb.want_plan(st);
     }
     if (!plan) return rg::launch_pipe(sa, oa, L, nullptr, st);
     rg::Launch Lp = L;
