@@ -93,7 +93,11 @@ enum rg_pkt_status {
 
 int rg_abi_version(void);
 /* Create a context bound to HIP device `device` (one per process/GPU).  Every call on a context works on
- * its device and leaves the caller's current HIP device as it found it. */
+ * its device and leaves the caller's current HIP device as it found it.  Key material the context keeps
+ * in device memory (the host calls' key table, the MAC key states, the per-message arena) is zeroed
+ * before its memory is reused or freed, in stream order: behind the launches that read it, without
+ * waiting for the device or for other streams (prim.rs:227-231 zeroizes keys on drop).  A call that would
+ * have to regrow such a buffer while its stream is being captured into a graph fails with RG_EDEVICE. */
 int rg_create(int device, rg_ctx **out);
 void rg_destroy(rg_ctx *ctx);
 /* Text of the last error on this thread ("" if none). */

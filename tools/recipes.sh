@@ -1178,6 +1178,21 @@ RG_AEAD_LIB=tools/build/librg_diag.so timeout -k 10 200 python tools/flat_stamps
 return 0
 }
 
+recipe_r5_check() {
+# Round 5: every GPU test on the current build, smoke(), the default bench line as the driver runs it, and
+# the N = 2 launcher path rehearsed on one GPU (torch.distributed.run, two ranks sharing the GPU over gloo;
+# its line now carries e2e_multi).
+bash tools/gpu_run.sh test smoke || return $?
+timeout -k 10 600 python bench.py > gpurun_out/r5_default.jsonl 2> gpurun_out/r5_default.err || { tail -5 gpurun_out/r5_default.err; return 1; }
+cut -c1-600 gpurun_out/r5_default.jsonl
+RG_BENCH_SHARE_GPU=1 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+    --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --steps 5 --warmup 2 --cpu-seconds 2 \
+    > gpurun_out/r5_rehearse_tr2.log 2>&1
+rc=$?; grep '^{' gpurun_out/r5_rehearse_tr2.log | python3 -c "import sys,json; d=json.loads(sys.stdin.read()); print(d['value'], d.get('speedup'), json.dumps(d.get('e2e_multi'))[:800])"
+[ $rc -ne 0 ] && { tail -20 gpurun_out/r5_rehearse_tr2.log; return $rc; }
+return 0
+}
+
 if [ "${1:-}" = "--list" ] || [ $# -eq 0 ]; then
     grep -A1 '^recipe_[a-z0-9_]*() {' "$SELF" | sed -n 's/^recipe_\([a-z0-9_]*\)() {/\1/p;s/^# \(.*\)/    \1/p'
     exit 0
