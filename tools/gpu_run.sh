@@ -66,6 +66,8 @@ for s in "$@"; do
         summ gpurun_out/bench_cfg[2-5].log ;;
     e2e) run e2e 400 python bench.py --steps 10 --warmup 3 --cpu-seconds 0 --e2e ;;
     default) run bench_default 600 python bench.py ;;
+    defprof) run prof_default 700 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_default -o run -- \
+        python3 bench.py ;;
     cfg1) run bench_cfg1 300 python bench.py --workload cfg1 ;;
     prof)
         W=${RG_WORKLOAD:-cfg2}
