@@ -1193,6 +1193,31 @@ rc=$?; grep '^{' gpurun_out/r5_rehearse_tr2.log | python3 -c "import sys,json; d
 return 0
 }
 
+recipe_r5_sw() {
+# Round 5: store waves for the pipelined kernel's line stores (RG_STORE_WAVE builds: a partner wave per
+# SIMD reads the ring back and stores): every GPU test on that build, per-wave stamps of the diag builds
+# with and without, and the SQ issue counters of both on config 2.
+if [ -z "${R5_NOTEST:-}" ]; then
+    RG_AEAD_LIB=tools/build/librg_${R5_SW:-sw}.so timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 \
+        --timeout-method thread > gpurun_out/r5_sw_tests.log 2>&1
+    rc=$?; tail -2 gpurun_out/r5_sw_tests.log; [ $rc -eq 0 ] || return $rc
+fi
+for v in dg dgsw; do
+    RG_AEAD_LIB=tools/build/librg_$v.so timeout -k 10 200 python tools/stamps.py --workload cfg2 > gpurun_out/r5_sw_st_$v.log 2>&1 \
+        || { tail -5 gpurun_out/r5_sw_st_$v.log; return 1; }
+    tail -4 gpurun_out/r5_sw_st_$v.log | cut -c1-600
+done
+for v in base ${R5_SW:-sw}; do
+    if [ $v = base ]; then unset RG_AEAD_LIB; else export RG_AEAD_LIB=tools/build/librg_$v.so; fi
+    timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_WAVES SQ_ACTIVE_INST_VALU \
+        SQ_WAIT_ANY SQ_WAIT_INST_ANY --kernel-trace --output-format csv -d gpurun_out/r5_sw_pmc_$v -o p -- \
+        python3 bench.py --workload cfg2 --steps 5 --warmup 2 --cpu-seconds 0 --no-graph > gpurun_out/r5_sw_pmc_$v.log 2>&1 || return $?
+done
+unset RG_AEAD_LIB
+python3 tools/pmc_clock.py gpurun_out/r5_sw_pmc_* 2>&1 | tail -12
+return 0
+}
+
 if [ "${1:-}" = "--list" ] || [ $# -eq 0 ]; then
     grep -A1 '^recipe_[a-z0-9_]*() {' "$SELF" | sed -n 's/^recipe_\([a-z0-9_]*\)() {/\1/p;s/^# \(.*\)/    \1/p'
     exit 0
