@@ -109,9 +109,13 @@ constexpr uint32_t kCoopWPkt = 1, kCoopWChk = 8;
 // compare doubled sums by the sign bit of their difference, so they stay below 2^31
 static_assert(kCoopGroup * (kCoopWPkt + kCoopWChk * (kMaxPayload / 64ull + 1)) * 2 < (1ull << 31),
               "coop work sums overflow 31 bits");
-constexpr uint32_t kCoopLds = 256; // shared slots: wave totals, cut counts
+constexpr uint32_t kCoopLds = 256; // shared slots: wave totals
 constexpr uint32_t kFlatWaves = 4; // waves per workgroup (the coop search's four quarters), one per SIMD
-static_assert(kFlatWaves * sizeof(FlatLds) + 256 <= kLdsPerCu, "flat LDS image");
+// the group's work prefix, quarter by quarter (each wave writes its 1024 inclusive sums once): every wave
+// reads off its own two cut points after one barrier
+constexpr uint32_t kCoopPrefix = kCoopGroup * 4;
+constexpr uint32_t kFlatLdsBytes = kFlatWaves * sizeof(FlatLds) + kCoopLds + kCoopPrefix;
+static_assert(kFlatLdsBytes <= kLdsPerCu, "flat LDS image");
 
 
 struct FChunk {
@@ -469,7 +473,7 @@ template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) voi
             // group's units a multiple of four, n a multiple of kCoopGroup.
             uint32_t *const sh = reinterpret_cast<uint32_t *>(flat_lds + kFlatWaves * sizeof(FlatLds));
             const uint32_t kgc = uniform_u32(A.coop);               // units per group
-            const uint32_t g = uniform_u32(u / kgc), j = uniform_u32(u - g * kgc), j0 = j - wv;
+            const uint32_t g = uniform_u32(u / kgc), j = uniform_u32(u - g * kgc);
             const uint32_t gb = g * kCoopGroup + wv * kFlatGroup;    // this wave's 1024 packets
             RG_FLAT_SUB(0);
             rg_pkt_desc d[16];
@@ -496,71 +500,78 @@ template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) voi
             const uint32_t lx = wave_scan_incl(lsum) - lsum;
 #pragma unroll
             for (int q = 0; q < 16; ++q) e[q] += lx;
+            // the quarter's inclusive work prefix (packet 16 lane + q) for every wave of the workgroup
+            uint32_t *const pf_all = sh + kCoopLds / 4;
+            {
+                uint4 *p4 = reinterpret_cast<uint4 *>(pf_all + kFlatGroup * wv) + 4 * lane;
+                p4[0] = make_uint4(e[0], e[1], e[2], e[3]);
+                p4[1] = make_uint4(e[4], e[5], e[6], e[7]);
+                p4[2] = make_uint4(e[8], e[9], e[10], e[11]);
+                p4[3] = make_uint4(e[12], e[13], e[14], e[15]);
+            }
             if (lane == 0) sh[wv] = lane63(lx + lsum); // this wave's total
             RG_FLAT_SUB(2);
             __syncthreads();
             RG_FLAT_SUB(3);
-            uint32_t off = 0, tot = 0; // work of the group's packets before this wave's; the group's
+            uint32_t qt[kFlatWaves], tot = 0; // the quarters' totals; the group's
 #pragma unroll
             for (uint32_t w = 0; w < kFlatWaves; ++w) {
-                const uint32_t tw_ = uniform_u32(sh[w]);
-                off += w < wv ? tw_ : 0u;
-                tot += tw_;
+                qt[w] = uniform_u32(sh[w]);
+                tot += qt[w];
             }
-            // the workgroup's five cut points, as packet counts of this wave's quarter below each target
-            // (midpoint rule: packet i goes to the unit its work midpoint falls in)
-            uint32_t cnt[5];
+            // This unit's two cut points (midpoint rule: packet i goes to the unit its work midpoint falls
+            // in), each wave its own: targets 2 tot j / kgc and 2 tot (j + 1) / kgc.  Any rounding is fine as
+            // long as every workgroup of the group computes the same function of (tot, boundary index) --
+            // they do, so a boundary shared by two workgroups lands on the same packet in both.
+            // A cut = the packets of the quarters wholly below the target + the count inside the quarter
+            // holding it.  Midpoints rise strictly with the packet index (every packet has work >= 1), so in
+            // that quarter the 16-packet rows whose last midpoint lies below the target are a prefix (one
+            // ballot), and the next row's count is a second ballot.  Sums stay below 2^31 (static_assert
+            // above), so (m - t) >> 31 is m < t without a carry flag (no SGPR hazard nops).
+            uint32_t cut0, cut1;
             {
-                // targets 2 tot (j0 + b) / kgc: any rounding is fine as long as every workgroup of the
-                // group computes the same function of (tot, boundary index) -- they do, so a boundary
-                // shared by two workgroups lands on the same packet in both
                 const double per = (double)tot * __builtin_amdgcn_rcp((double)kgc);
-                uint32_t t2[5];
+                uint32_t T[2], base[2], qw[2];
 #pragma unroll
-                for (int b = 0; b < 5; ++b) t2[b] = uniform_u32(2 * (uint32_t)(per * (double)(j0 + b)));
-                const uint32_t sh1 = wave_shr1(e[15]);
-                const uint32_t prev0 = lane ? sh1 : 0u;
-                const uint32_t lo2 = 2 * off, hi2 = 2 * (off + uniform_u32(sh[wv]));
+                for (int b = 0; b < 2; ++b) {
+                    T[b] = uniform_u32(2 * (uint32_t)(per * (double)(j + b)));
+                    // the quarter w with 2 off_w < T <= 2 (off_w + qt_w) (none: T = 0, or T past the group)
+                    uint32_t off = 0, w_ = kFlatWaves, lo = 0;
 #pragma unroll
-                for (int b = 0; b < 5; ++b) {
-                    // this wave's packets have midpoints in [lo2, hi2): a target outside needs no count
-                    if (t2[b] <= lo2) {
-                        cnt[b] = 0;
-                    } else if (t2[b] > hi2) {
-                        cnt[b] = kFlatGroup;
-                    } else {
-                        // Midpoints rise strictly with the packet index (every packet has work >= 1), so the
-                        // lanes whose last midpoint lies below the target are a prefix of the wave: the count
-                        // is 16 per such lane plus the first other lane's own count (a ballot and one
-                        // readlane instead of a wave scan).  Sums stay below 2^31 (static_assert above), so
-                        // (m - t) >> 31 is the comparison m < t without a carry flag (no SGPR hazard nops).
-                        uint32_t prev = prev0, c = 0;
-#pragma unroll
-                        for (int q = 0; q < 16; ++q) {
-                            c += (e[q] + prev + lo2 - t2[b]) >> 31;
-                            prev = e[q];
+                    for (uint32_t w = 0; w < kFlatWaves; ++w) {
+                        if (w_ == kFlatWaves && T[b] <= 2 * (off + qt[w])) {
+                            w_ = w;
+                            lo = 2 * off;
                         }
-                        const uint32_t full = (uint32_t)__popcll(__ballot(((e[15] + e[14] + lo2 - t2[b]) >> 31) != 0));
-                        cnt[b] = 16u * full + (full < 64 ? (uint32_t)__builtin_amdgcn_readlane((int)c, (int)full) : 0u);
+                        off += qt[w];
                     }
+                    qw[b] = uniform_u32(w_);
+                    base[b] = uniform_u32(lo);
                 }
-            }
-            if (lane == 0) {
+                uint32_t full[2];
 #pragma unroll
-                for (int b = 0; b < 5; ++b) sh[8 + 5 * wv + b] = cnt[b];
+                for (int b = 0; b < 2; ++b) {
+                    const uint32_t *pf = pf_all + kFlatGroup * (qw[b] < kFlatWaves ? qw[b] : 0u);
+                    const uint32_t a = pf[16 * lane + 15], c = pf[16 * lane + 14];
+                    full[b] = (uint32_t)__popcll(__ballot(((a + c + base[b] - T[b]) >> 31) != 0));
+                }
+                uint32_t cnt[2];
+#pragma unroll
+                for (int b = 0; b < 2; ++b) {
+                    const uint32_t *pf = pf_all + kFlatGroup * (qw[b] < kFlatWaves ? qw[b] : 0u);
+                    const uint32_t row = full[b] < 64 ? full[b] : 63u, q = lane & 15u;
+                    const uint32_t i = 16 * row + q;
+                    const uint32_t cur = pf[i], prv = i ? pf[i - 1] : 0u;
+                    const uint32_t in = (uint32_t)__popcll(__ballot(lane < 16 && ((cur + prv + base[b] - T[b]) >> 31) != 0));
+                    cnt[b] = qw[b] >= kFlatWaves ? kCoopGroup : kFlatGroup * qw[b] + 16u * full[b] + (full[b] < 64 ? in : 0u);
+                }
+                cut0 = j == 0 ? 0u : cnt[0];
+                cut1 = j + 1 == kgc ? kCoopGroup : cnt[1];
             }
             RG_FLAT_SUB(4);
-            __syncthreads();
             RG_FLAT_SUB(5);
-            uint32_t cut0 = 0, cut1 = 0;
-#pragma unroll
-            for (uint32_t w = 0; w < kFlatWaves; ++w) {
-                cut0 += uniform_u32(sh[8 + 5 * w + wv]);
-                cut1 += uniform_u32(sh[8 + 5 * w + wv + 1]);
-            }
-            if (j == 0) cut0 = 0;
-            if (j + 1 == kgc) cut1 = kCoopGroup;
-            // (no barrier after these reads: one unit per wave, so no wave writes the shared slots again)
+            // (no barrier after these reads: one unit per wave, so no wave writes the shared slots or the
+            // prefix again)
             // the first sub-unit is staged from memory below (L2-resident: this workgroup just read it);
             // staging it from the four waves' registers into each other's images measured 2x slower
             s0 = g * kCoopGroup + cut0;
@@ -1138,7 +1149,7 @@ hipError_t launch_flat(const SealArgs *sa, const OpenArgs *oa, bool balance, uin
     A.coop = flat_coop_ok(n, A.units, balance);
     A.wpkt = kCoopWPkt;
     A.wchk = kCoopWChk;
-    const uint32_t lds = kFlatWaves * (uint32_t)sizeof(FlatLds) + kCoopLds;
+    const uint32_t lds = kFlatLdsBytes;
     const bool win = (sa ? sa->buf_len : oa->buf_len) < 0x7FFFFFF0ull; // frame offsets below 2 GiB
     if (sa && win) hipLaunchKernelGGL((flat_kernel<false, true>), dim3(blocks), dim3(64 * kFlatWaves), lds, s, A);
     else if (sa) hipLaunchKernelGGL((flat_kernel<false, false>), dim3(blocks), dim3(64 * kFlatWaves), lds, s, A);
@@ -1150,7 +1161,7 @@ hipError_t launch_flat(const SealArgs *sa, const OpenArgs *oa, bool balance, uin
 uint32_t flat_junk_bytes(int cus) { return (uint32_t)(cus > 0 ? cus : 1) * kFlatWaves * 64 * 64; }
 
 hipError_t prepare_flat_kernels() {
-    const int lds = (int)(kFlatWaves * sizeof(FlatLds) + kCoopLds);
+    const int lds = (int)kFlatLdsBytes;
     const void *f[4] = {(const void *)flat_kernel<false, true>, (const void *)flat_kernel<false, false>,
                         (const void *)flat_kernel<true, true>, (const void *)flat_kernel<true, false>};
     hipError_t e = hipSuccess;

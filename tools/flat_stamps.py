@@ -75,14 +75,15 @@ for op in ("seal", "open"):
         out["wall_us_end_pct_0_50_90_100"] = [round(float(x), 2) for x in np.percentile(rt[:, 1] - r0, [0, 50, 90, 100])]
         out["clock_ghz"] = round(float(rel[:, 7].sum() / ((rt[:, 1] - rt[:, 0]).sum() * 1e3)), 3)
     if (sub[:, 5] != 0).any():
-        # search steps (round 5, the cooperative deal): entry (kernel arguments, setup), length loads and
-        # size classes, ranks within the classes, first barrier, sorted positions and the unit lists,
-        # second barrier.  (Round 4's contiguous cuts: entry, descriptor loads + LDS transpose, prefix,
-        # first barrier, cut counts, second barrier -- the same six stamp slots.)
+        # search steps: entry (kernel arguments, setup), length loads + LDS transpose, prefix (+ the shared
+        # prefix rows), the barrier, this wave's two cut points, and a sixth slot that round 5's single-barrier
+        # search leaves empty (round 4 had a second barrier there; the round-5 deal record
+        # profiles/r5_cfg3_deal_ab.txt labels the same six slots length loads + classes, class ranks,
+        # barrier, sorted positions + unit lists, barrier).
         okw = (sub != 0).all(axis=1) & (sub_t0[:, 0] != 0)
         st = np.concatenate([sub_t0[okw], sub[okw]], axis=1)
         dl = np.diff(st, axis=1)
-        nm = ["entry", "len_loads+classes", "class_ranks", "barrier1", "positions+lists", "barrier2"]
+        nm = ["entry", "len_loads+transpose", "prefix", "barrier", "cut_points", "(none)"]
         out["search_steps"] = {k: {"mean_cyc": int(dl[:, i].mean()), "max_cyc": int(dl[:, i].max())}
                                for i, k in enumerate(nm)}
     res[op] = out

@@ -1218,6 +1218,24 @@ python3 tools/pmc_clock.py gpurun_out/r5_sw_pmc_* 2>&1 | tail -12
 return 0
 }
 
+recipe_r5_cut() {
+# Round 5: the flattened kernel's cut points, each wave its own two from a workgroup-shared prefix (one
+# barrier instead of two, no wave computing the others' cuts): flat / forged / digest / coop GPU tests on the
+# variant, interleaved A/B on config 3, per-wave phases of both diag builds.
+V=${R5_CUT:-cut2}
+RG_AEAD_LIB=tools/build/librg_$V.so timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_forged.py -x -q \
+    -m gpu -k "flat or open_failures or bad_descriptors or malformed or digest or auto or coop" --timeout 300 \
+    --timeout-method thread > gpurun_out/r5_cut_tests.log 2>&1
+rc=$?; tail -2 gpurun_out/r5_cut_tests.log; [ $rc -eq 0 ] || return $rc
+bash tools/ab.sh "base ${R5_CUT_AB:-$V}" "cfg3" 3 --no-cold --forged 0 || return $?
+for v in ${R5_CUT_ST:-diag ${V}dg}; do
+    RG_AEAD_LIB=tools/build/librg_$v.so timeout -k 10 200 python tools/flat_stamps.py --workload cfg3 > gpurun_out/r5_cut_st_$v.txt 2>&1 \
+        || { tail -5 gpurun_out/r5_cut_st_$v.txt; return 1; }
+    grep -E "^(seal|open)" gpurun_out/r5_cut_st_$v.txt | cut -c1-900
+done
+return 0
+}
+
 if [ "${1:-}" = "--list" ] || [ $# -eq 0 ]; then
     grep -A1 '^recipe_[a-z0-9_]*() {' "$SELF" | sed -n 's/^recipe_\([a-z0-9_]*\)() {/\1/p;s/^# \(.*\)/    \1/p'
     exit 0
