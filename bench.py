@@ -628,12 +628,12 @@ def single_process_run(devices, steps: int, warmup: int, verify: bool = True):
 
 def e2e_multi_run(devices, reps: int = 3, verify: bool = True):
     """Packets that start and end in pinned host memory (the reference's UDP buffers,
-    rustyguard-tun/src/main.rs:41-57), driven over several GPUs by ONE thread (the reference's single
-    event loop, rustyguard-core/src/lib.rs:349-352): rg_seal_batch_host_multi then rg_open_batch_host_multi
-    on config 5's whole batch (8 Mi x 1500 B, 12.9 GB of frames) in one hipHostMalloc buffer, split by
-    equal work over the group's contexts (one per entry of `devices`), each running its own three-stream
-    H2D -> kernel -> D2H slice pipeline; the thread steps whichever context has a free slot (never waits
-    on one GPU while another could take a slice).  Beside it the same batch through one context (device
+    rustyguard-tun/src/main.rs:41-57), driven over several GPUs from ONE calling thread (the reference's
+    single event loop, rustyguard-core/src/lib.rs:349-352): rg_seal_batch_host_multi then
+    rg_open_batch_host_multi on config 5's whole batch (8 Mi x 1500 B, 12.9 GB of frames) in one
+    hipHostMalloc buffer, split by equal work over the group's contexts (one per entry of `devices`), each
+    running its own three-stream H2D -> kernel -> D2H slice pipeline from a worker thread of the library
+    (round 5; no context waits on another's GPU).  Beside it the same batch through one context (device
     devices[0]) -- the e2e speed-up of the group.  Median of `reps` timed passes after one warm pass;
     every open must verify, and sampled payloads must come back to what they were before the first seal."""
     from rustyguard_amd import workloads
@@ -681,7 +681,8 @@ def e2e_multi_run(devices, reps: int = 3, verify: bool = True):
             assert np.array_equal(buf[o:o + len(v)], v), f"e2e packet {k} not restored by seal + open"
     if "one_context" in out:
         out["speedup"] = round(out["group"]["seal_open_gib_s"] / out["one_context"]["seal_open_gib_s"], 3)
-    out["how"] = ("one thread: rg_{seal,open}_batch_host_multi over an rg_group, 8 MiB slices, 3 slots per context, "
+    out["how"] = ("one calling thread: rg_{seal,open}_batch_host_multi over an rg_group (the library drives each context's "
+                  "pipeline from a worker thread of its own), 8 MiB slices, 3 slots per context, "
                   "descriptors/counters/statuses in mapped host memory; host clock per call, median of reps")
     del buf
     return out

@@ -1236,6 +1236,26 @@ done
 return 0
 }
 
+recipe_r5_gthr() {
+# Round 5: a group's host calls with one worker thread per context (RG_GROUP_THREADS, default on) against the
+# single-thread loop (tools/build_variant.sh gthr0 -DRG_GROUP_THREADS=0): every GPU test and smoke() on the
+# in-tree build first, config 3's profiles for the one-barrier search, then the --single-process line with
+# 2 and 4 contexts sharing the one GPU (e2e_multi).
+bash tools/gpu_run.sh test smoke || return $?
+RG_WORKLOAD=cfg3 bash tools/gpu_run.sh prof pmc_hbm || return $?
+RG_WORKLOADS=cfg3 bash tools/gpu_run.sh valu bench_all || return $?
+for v in base gthr0; do
+    for n in 2 4; do
+        if [ $v = base ]; then unset RG_AEAD_LIB; else export RG_AEAD_LIB=tools/build/librg_$v.so; fi
+        RG_BENCH_SHARE_GPU=1 timeout -k 10 400 python bench.py --single-process --gpus $n --steps 5 --warmup 2 \
+            --cpu-seconds 0 > gpurun_out/r5_gthr_${v}_$n.log 2>&1 || return $?
+        grep '^{' gpurun_out/r5_gthr_${v}_$n.log | python3 -c "import sys,json; d=json.loads(sys.stdin.read()); print('$v', $n, json.dumps(d.get('e2e_multi'))[:700])"
+    done
+done
+unset RG_AEAD_LIB
+return 0
+}
+
 if [ "${1:-}" = "--list" ] || [ $# -eq 0 ]; then
     grep -A1 '^recipe_[a-z0-9_]*() {' "$SELF" | sed -n 's/^recipe_\([a-z0-9_]*\)() {/\1/p;s/^# \(.*\)/    \1/p'
     exit 0
