@@ -2,7 +2,8 @@
 per-peer endpoint record (rg_sessions_insert_peer).
 
 The reference's host is one thread owning one Sessions (rustyguard-core/src/lib.rs:349-352); a group
-splits each batch into contiguous ranges over its contexts and runs their pipelines from that thread.
+splits each batch into contiguous ranges over its contexts and runs their pipelines for that thread (since
+round 5 on one library worker thread per context).
 Packets are independent, so every result must equal the one-context / oracle result
 byte for byte.  The groups: N = 2 and 4 contexts on device 0 (one GPU runs every code path: streams,
 splits, the round-robin issue, the gather) and, on a box with several GPUs, one context on each
@@ -386,3 +387,42 @@ def test_host_batch_in_any_frame_order(use_group, engine, group):
     so, co = runner.open_host(kt, od, got)
     assert so[7] == aead.PKT_DECRYPT_ERR and (np.delete(so, 7) == 0).all()
     assert np.array_equal(np.delete(co, 7), np.delete(ctr, 7))
+
+
+def test_group_host_call_survives_failing_allocations():
+    """Round 5 runs each context's host pipeline on a worker thread of the library.  A group host call whose
+    k-th allocation fails (rg_debug_fail_reserve, test library) -- in the calling thread while the key tables
+    go up (k <= 6 here: three contexts, a key table and a receiver table each), or in some context's worker
+    while it reserves its slot buffers -- returns an error (the first failing context's, carried over to the
+    calling thread), leaves no worker behind, and the same group's next call seals every frame bit-exactly."""
+    from rustyguard_amd import _lib
+
+    L = _lib.lib_test()
+    rng = np.random.default_rng(91)
+    n = 24000
+    desc = np.zeros(n, DESC_DTYPE)
+    desc["len"] = 1504
+    desc["offset"] = np.arange(n, dtype=np.uint64) * 1536
+    desc["key_idx"] = rng.integers(0, 3, n)
+    kt = rng.integers(0, 256, (3, 32), dtype=np.uint8)
+    rec = np.arange(3, dtype=np.uint32) + 11
+    ctr = rng.integers(0, 2**50, n, dtype=np.uint64)
+    base = rng.integers(0, 256, n * 1536, dtype=np.uint8)
+    want = base.copy()
+    oracle.seal_batch(kt, rec, desc, ctr, want)
+    for k in (1, 4, 7, 12, 19, 30):
+        g = Group([0, 0, 0], library=L)
+        try:
+            for i in range(3):
+                g.engine(i).set_host_slice(2 << 20)  # ~12 MiB per context: six 2 MiB slices, all three slots used
+            L.rg_debug_fail_reserve(k)
+            try:
+                with pytest.raises(_lib.RgError):
+                    g.seal_host(kt, rec, desc, ctr, base.copy())
+            finally:
+                L.rg_debug_fail_reserve(0)
+            got = base.copy()
+            st = g.seal_host(kt, rec, desc, ctr, got)
+            assert (st == 0).all() and np.array_equal(got, want), f"after a failure at allocation {k}"
+        finally:
+            g.close()

@@ -1256,6 +1256,25 @@ unset RG_AEAD_LIB
 return 0
 }
 
+recipe_r5_seg() {
+# Round 5: the flattened kernel's stores in whole 64-byte segments (a chunk's pieces whose segment the next chunk
+# completes held one step; a seal's DataHeader stored with the packet's first chunk): flat / forged / digest /
+# coop / auto / malformed GPU tests on the variant (tools/build_variant.sh seg) and the group tests on the in-tree
+# build, interleaved A/B on config 3, FETCH / WRITE passes of the variant (gpurun_out/pmc_*_cfg3).
+RG_AEAD_LIB=tools/build/librg_seg.so timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_forged.py -x -q \
+    -m gpu -k "flat or open_failures or bad_descriptors or malformed or digest or auto or coop" --timeout 300 \
+    --timeout-method thread > gpurun_out/r5_seg_tests.log 2>&1
+rc=$?; tail -2 gpurun_out/r5_seg_tests.log; [ $rc -eq 0 ] || return $rc
+timeout -k 10 600 python -u -m pytest tests/test_gpu_group.py -x -q -m gpu --timeout 300 --timeout-method thread \
+    > gpurun_out/r5_group_tests.log 2>&1
+rc=$?; tail -2 gpurun_out/r5_group_tests.log; [ $rc -eq 0 ] || return $rc
+bash tools/ab.sh "base seg" "cfg3" 3 --no-cold --forged 0 || return $?
+RG_AEAD_LIB=tools/build/librg_seg.so RG_WORKLOAD=cfg3 bash tools/gpu_run.sh pmc_hbm > /dev/null || return $?
+python3 tools/make_profiles.py --tag r5seg --workload cfg3 --fetch gpurun_out/pmc_fetch_cfg3 --write gpurun_out/pmc_write_cfg3 \
+    --bench gpurun_out/ab_seg_cfg3_1.log 2>&1 | tail -12
+return 0
+}
+
 if [ "${1:-}" = "--list" ] || [ $# -eq 0 ]; then
     grep -A1 '^recipe_[a-z0-9_]*() {' "$SELF" | sed -n 's/^recipe_\([a-z0-9_]*\)() {/\1/p;s/^# \(.*\)/    \1/p'
     exit 0
