@@ -325,9 +325,10 @@ class DecryptionKey:
 
 # ------------------------------------------------------------------ Sessions
 class Group:
-    """rg_group: one thread driving several GPUs (one context per entry of `devices`; a device may
-    repeat).  Host-memory batches are split into contiguous ranges of about equal AEAD work, one per
-    context, all pipelines enqueued from this thread (include/rg_aead.h, "several GPUs, one thread")."""
+    """rg_group: one calling thread driving several GPUs (one context per entry of `devices`; a device
+    may repeat).  Host-memory batches are split into contiguous ranges of about equal AEAD work, one per
+    context; the library runs each context's pipeline on a worker thread of its own and returns when all
+    are done (include/rg_aead.h, "several GPUs, one thread")."""
 
     def __init__(self, devices, library=None):
         self._L = library if library is not None else lib()
