@@ -1275,6 +1275,28 @@ python3 tools/make_profiles.py --tag r5seg --workload cfg3 --fetch gpurun_out/pm
 return 0
 }
 
+recipe_r5_nosdma() {
+# Round 5: the host path with every copy on a shader blit kernel (HSA_ENABLE_SDMA=0: no SDMA engine, so no
+# cross-engine completion in the slice chain) against the default (SDMA uploads, blit downloads):
+# tools/e2e_probe.py cfg2 at 4 / 8 / 16 MiB slices, interleaved, then a kernel + memory-copy trace of each.
+mkdir -p gpurun_out/nosdma
+for rep in 1 2; do
+    for cfg in base HSA_ENABLE_SDMA=0; do
+        if [ "$cfg" = base ]; then envs=(X_RG_NONE=1); else envs=("$cfg"); fi
+        env "${envs[@]}" timeout -k 10 200 python3 tools/e2e_probe.py cfg2 4,8,16 > "gpurun_out/nosdma/${cfg}_$rep.log" 2>&1 \
+            || { echo "rc=$?"; tail -5 "gpurun_out/nosdma/${cfg}_$rep.log"; return 1; }
+        echo "$cfg $rep: $(tail -3 gpurun_out/nosdma/${cfg}_$rep.log | tr '\n' ' ')"
+    done
+done
+for cfg in base HSA_ENABLE_SDMA=0; do
+    if [ "$cfg" = base ]; then envs=(X_RG_NONE=1); else envs=("$cfg"); fi
+    env "${envs[@]}" timeout -k 10 150 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d "gpurun_out/nosdma/tr_$cfg" \
+        -o run -- python3 tools/e2e_probe.py cfg2 8 > "gpurun_out/nosdma/tr_$cfg.log" 2>&1 || { echo "trace rc=$?"; return 1; }
+    python3 tools/e2e_timeline.py "gpurun_out/nosdma/tr_$cfg" seal 2>&1 | tail -16
+done
+return 0
+}
+
 if [ "${1:-}" = "--list" ] || [ $# -eq 0 ]; then
     grep -A1 '^recipe_[a-z0-9_]*() {' "$SELF" | sed -n 's/^recipe_\([a-z0-9_]*\)() {/\1/p;s/^# \(.*\)/    \1/p'
     exit 0
