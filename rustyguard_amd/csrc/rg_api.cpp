@@ -9,6 +9,7 @@
 #include <atomic>
 #include <cstdio>
 #include <cstring>
+#include <exception>
 #include <mutex>
 #include <new>
 #include <string>
@@ -1023,19 +1024,30 @@ int run_host(HostRun *runs, size_t nruns) {
 int run_host_group(std::vector<HostRun> &runs) {
     if (!RG_GROUP_THREADS || runs.size() < 2) return run_host(runs.data(), runs.size());
     const size_t n = runs.size();
-    std::vector<int> rcs(n, RG_OK);
-    std::vector<std::string> errs(n);
+    std::vector<int> rcs;
+    std::vector<std::string> errs;
     std::vector<std::thread> workers;
-    workers.reserve(n);
+    try { // (no exception may cross the C ABI: without the bookkeeping, the calling thread runs them all)
+        rcs.assign(n, RG_OK);
+        errs.resize(n);
+        workers.reserve(n);
+    } catch (const std::exception &) {
+        return run_host(runs.data(), n);
+    }
     size_t started = 0;
     try {
         for (; started < n; ++started)
             workers.emplace_back([&runs, &rcs, &errs, started]() {
                 rcs[started] = run_host(&runs[started], 1);
-                if (rcs[started] != RG_OK) errs[started] = g_err;
+                if (rcs[started] != RG_OK) {
+                    try {
+                        errs[started] = g_err;
+                    } catch (const std::exception &) { // the code still reaches the caller
+                    }
+                }
             });
-    } catch (const std::system_error &) {
-        // fewer threads than runs: the rest run here, stepped together as before
+    } catch (const std::exception &) {
+        // fewer threads than runs (std::system_error): the rest run here, stepped together as before
     }
     int rc_here = RG_OK;
     std::string err_here;
