@@ -22,6 +22,7 @@ ap.add_argument("--wg-per-cu", type=int, default=0)
 ap.add_argument("--plan", type=int, default=-1)
 ap.add_argument("--segments", type=int, default=0)
 ap.add_argument("--lanes", type=int, default=0)
+ap.add_argument("--world", type=int, default=1, help="config 5: rank 0's shard of an N-GPU strong split")
 ap.add_argument("--mode", type=int, default=3, help="seal debug mode while stamping (pipelined kernel: 1/2/4/5/6 too)")
 args = ap.parse_args()
 eng = Engine(0)
@@ -33,7 +34,7 @@ if args.plan >= 0:
 eng.set_segments(args.segments)
 if args.lanes:
     eng.set_lanes_per_packet(args.lanes)
-w = workloads.build(args.workload)
+w = workloads.build(args.workload, 0, args.world) if args.world > 1 else workloads.build(args.workload)
 b = DeviceBatch(eng, w)
 b.fill()
 dbg = torch.zeros(8 * 256 * 32, dtype=torch.int64, device="cuda")
