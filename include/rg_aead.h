@@ -375,8 +375,9 @@ int rg_recv_batch_dev_finish(rg_sessions *s, const uint64_t *src, uint8_t *statu
  * GPU).  A batch given to a group is split into contiguous index ranges of about equal AEAD work
  * (payload bytes + one 64-byte key block per packet; rg_split_batch), one per context; every
  * context's H2D -> kernel -> D2H pipeline runs on its own streams, driven by a worker thread of the
- * library per context (the calling thread waits; if a thread cannot be started, the calling thread
- * steps the remaining contexts itself), and the call returns when all are done.  The caller's
+ * library per context once some part spans more than two slices (rg_set_host_slice; smaller batches,
+ * and contexts whose thread cannot be started, are stepped by the calling thread itself), and the call
+ * returns when all are done.  The caller's
  * current device is left as it was.  Results are those of one context: the
  * packets are independent, counters are reserved before the split (rg_send_batch)
  * and the in-order anti-replay pass runs after the gather (rg_recv_batch_ex). */

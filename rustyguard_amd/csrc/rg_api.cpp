@@ -1023,6 +1023,18 @@ int run_host(HostRun *runs, size_t nruns) {
 #endif
 int run_host_group(std::vector<HostRun> &runs) {
     if (!RG_GROUP_THREADS || runs.size() < 2) return run_host(runs.data(), runs.size());
+    // Threads pay off once a context has a few slices to pipeline; a small batch (every part within two
+    // slices) runs from the calling thread, without starting and joining a thread per context.
+    bool big = false;
+    for (const HostRun &r : runs) {
+        uint64_t bytes = 0;
+        for (size_t k = r.i; k < r.end && !big; ++k) {
+            bytes += (uint64_t)r.desc[k].len + 32;
+            big = bytes > 2 * (uint64_t)r.ctx->host_slice;
+        }
+        if (big) break;
+    }
+    if (!big) return run_host(runs.data(), runs.size());
     const size_t n = runs.size();
     std::vector<int> rcs;
     std::vector<std::string> errs;
