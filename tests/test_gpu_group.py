@@ -426,3 +426,41 @@ def test_group_host_call_survives_failing_allocations():
             assert (st == 0).all() and np.array_equal(got, want), f"after a failure at allocation {k}"
         finally:
             g.close()
+
+
+def test_group_host_calls_alternate_threaded_and_inline(group):
+    """Round 5: a group call drives its contexts from worker threads when some context's part spans more
+    than two slices and from the calling thread otherwise.  Calls of both kinds, alternating on one group
+    (slots, key tables and events reused across the switch), each seal then open bit-exactly."""
+    rng = np.random.default_rng(93)
+    kt = rng.integers(0, 256, (4, 32), dtype=np.uint8)
+    rec = np.arange(4, dtype=np.uint32) + 5
+    for c in range(len(group)):
+        group.engine(c).set_host_slice(2 << 20)  # the large batches span several slices on every context
+    try:
+        _alternate(group, rng, kt, rec)
+    finally:
+        for c in range(len(group)):
+            group.engine(c).set_host_slice(8 << 20)
+
+
+def _alternate(group, rng, kt, rec):
+    for i, n in enumerate([30000, 300, 26000, 40, 28000]):
+        desc = np.zeros(n, DESC_DTYPE)
+        desc["len"] = 1504
+        desc["offset"] = np.arange(n, dtype=np.uint64) * 1536
+        desc["key_idx"] = rng.integers(0, 4, n)
+        ctr = rng.integers(0, 2**50, n, dtype=np.uint64)
+        buf = rng.integers(0, 256, n * 1536, dtype=np.uint8)
+        want = buf.copy()
+        oracle.seal_batch(kt, rec, desc, ctr, want)
+        got = buf.copy()
+        st = group.seal_host(kt, rec, desc, ctr, got)
+        assert (st == 0).all() and np.array_equal(got, want), f"call {i} ({n} packets)"
+        od = desc.copy()
+        od["len"] += 32
+        so, co = group.open_host(kt, od, got)
+        assert (so == 0).all() and np.array_equal(co, ctr), f"open {i}"
+        for k in (0, n // 2, n - 1):
+            o = int(desc["offset"][k]) + 16
+            assert np.array_equal(got[o:o + 1504], buf[o:o + 1504]), f"open {i} packet {k}"
