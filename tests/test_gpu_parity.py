@@ -501,6 +501,40 @@ def test_flat_far_and_empty_descriptors_vs_oracle(engine, plan):
     _reset(engine)
 
 
+def test_flat_coop_search_skewed_quarters_vs_oracle(engine):
+    """Round 5's one-barrier search: every wave reads its own two cut points out of the workgroup's shared
+    prefix, from whichever quarter of the 4096-packet group holds each target.  Here each group's first
+    quarter holds only 1504-byte packets and the other three only keepalives and 16-byte packets, so most
+    units lie in quarter 0 (a few packets each), the cut points between the last of those and the next
+    cross the quarter boundary, and the remaining units hold several hundred packets each (sub-units of
+    kFlatMaxPk, staged one after another).  Seal and open, every byte and status against the oracle."""
+    import torch
+
+    n = 65536
+    units = 4 * torch.cuda.get_device_properties(0).multi_processor_count
+    if (units * 4096) % n or ((units * 4096) // n) % 4:
+        pytest.skip("the cooperative search does not apply at this CU count")
+    engine.set_staged(3)
+    engine.set_plan(1)
+    rng = np.random.default_rng(505)
+    pos = np.arange(n) % 4096
+    sizes = np.where(pos < 1024, 1504, rng.choice([0, 16], n))
+    keys, rec, desc, ctr, buf = _random_batch(rng, n, nkeys=2, sizes=sizes)
+    want = buf.copy()
+    oracle.seal_batch(keys, rec, desc, ctr, want, nthreads=8)
+    got, st = _gpu_seal(engine, keys, rec, desc, ctr, buf)
+    assert (st == aead.PKT_OK).all()
+    assert np.array_equal(got, want)
+    od = desc.copy()
+    od["len"] += 32
+    back, st, co = _gpu_open(engine, keys, od, got)
+    want_back = want.copy()
+    wst, wctr = oracle.open_batch(keys, od, want_back, nthreads=8)
+    assert (wst == 0).all() and (st == aead.PKT_OK).all() and np.array_equal(co, wctr)
+    assert np.array_equal(back, want_back)
+    _reset(engine)
+
+
 @pytest.mark.parametrize("n", [4096, 16384, 65536, 131072])
 def test_flat_coop_search_vs_oracle(engine, n):
     """When n is a multiple of 4096 and the units of a 4096-packet group are a multiple of four (CUs x 4
