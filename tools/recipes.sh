@@ -1297,6 +1297,40 @@ done
 return 0
 }
 
+recipe_r5_pmcst() {
+# Round 5: where config 2's store cost goes -- memory-pipe issue and stall counters of the pipelined seal
+# with payload stores (mode 0), without them (mode 7) and compute only (mode 1), diag build, two --pmc passes
+# each (8 SQ; 2 SQ + 2 TA + 3 TCP), summarised per wave by tools/valu_profile.py's reader.
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || return 1
+mkdir -p gpurun_out/pmcst
+local P1="SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_VMEM_WR SQ_INST_CYCLES_VMEM_RD SQ_WAIT_INST_ANY SQ_WAVES GRBM_GUI_ACTIVE"
+local P2="SQ_WAVE_CYCLES SQ_WAVES TA_DATA_STALLED_BY_TC_CYCLES TA_ADDR_STALLED_BY_TC_CYCLES TCP_PENDING_STALL_CYCLES TCP_LFIFO_STALL_CYCLES TCP_RFIFO_STALL_CYCLES GRBM_GUI_ACTIVE"
+local mode pass C extra
+for mode in 0 7 1; do
+    extra=""; [ $mode != 0 ] && extra="--debug-mode $mode --no-verify"
+    for pass in 1 2; do
+        if [ $pass = 1 ]; then C=$P1; else C=$P2; fi
+        RG_AEAD_LIB=tools/build/librg_diag.so timeout -s KILL 120 rocprofv3 --pmc $C --kernel-trace --output-format csv \
+            -d gpurun_out/pmcst/m${mode}_p$pass -o p -- python3 bench.py --workload cfg2 --steps 5 --warmup 2 \
+            --cpu-seconds 0 --no-cold --no-graph --forged 0 $extra > gpurun_out/pmcst/m${mode}_p$pass.log 2>&1 \
+            || { echo "fail mode $mode pass $pass"; tail -5 gpurun_out/pmcst/m${mode}_p$pass.log; return 1; }
+    done
+done
+python3 - <<'PY'
+import sys
+sys.path.insert(0, "tools")
+from valu_profile import summarise
+for mode in (0, 7, 1):
+    for p in (1, 2):
+        for k, v in summarise(f"gpurun_out/pmcst/m{mode}_p{p}").items():
+            if "seal" not in k:
+                continue
+            w = max(v["raw_means"].get("SQ_WAVES", 1), 1)
+            per = {c: round(x / w) for c, x in v["raw_means"].items() if c not in ("SQ_WAVES", "GRBM_GUI_ACTIVE")}
+            print(f"mode {mode} pass {p} {k.split('(')[0][-28:]} dur={v['duration_us_median']}us per-wave {per}")
+PY
+}
+
 if [ "${1:-}" = "--list" ] || [ $# -eq 0 ]; then
     grep -A1 '^recipe_[a-z0-9_]*() {' "$SELF" | sed -n 's/^recipe_\([a-z0-9_]*\)() {/\1/p;s/^# \(.*\)/    \1/p'
     exit 0
