@@ -1051,12 +1051,7 @@ int run_host_group(std::vector<HostRun> &runs) {
         for (; started < n; ++started)
             workers.emplace_back([&runs, &rcs, &errs, started]() {
                 rcs[started] = run_host(&runs[started], 1);
-                if (rcs[started] != RG_OK) {
-                    try {
-                        errs[started] = g_err;
-                    } catch (const std::exception &) { // the code still reaches the caller
-                    }
-                }
+                if (rcs[started] != RG_OK) errs[started].swap(g_err); // the worker's own message, moved out
             });
     } catch (const std::exception &) {
         // fewer threads than runs (std::system_error): the rest run here, stepped together as before
@@ -1065,15 +1060,15 @@ int run_host_group(std::vector<HostRun> &runs) {
     std::string err_here;
     if (started < n) {
         rc_here = run_host(&runs[started], n - started);
-        if (rc_here != RG_OK) err_here = g_err;
+        if (rc_here != RG_OK) err_here.swap(g_err); // (swaps: no string copy that could throw)
     }
     for (auto &t : workers) t.join();
     for (size_t k = 0; k < started; ++k)
         if (rcs[k] != RG_OK) {
-            g_err = errs[k];
+            g_err.swap(errs[k]);
             return rcs[k];
         }
-    if (rc_here != RG_OK) g_err = err_here;
+    if (rc_here != RG_OK) g_err.swap(err_here);
     return rc_here;
 }
 
