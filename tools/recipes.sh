@@ -1331,6 +1331,22 @@ for mode in (0, 7, 1):
 PY
 }
 
+recipe_r5_rtenv() {
+# Round 5: runtime signal settings against the host path's ~33 us completion chain (end-to-end):
+# interrupts off (busy-polled signals) and an active-wait window; tools/e2e_probe.py cfg2
+# at 8 / 16 MiB slices, interleaved with the default, two rounds.
+mkdir -p gpurun_out/rtenv
+local rep cfg
+for rep in 1 2; do
+    for cfg in X_RG_NONE=1 HSA_ENABLE_INTERRUPT=0 ROC_ACTIVE_WAIT_TIMEOUT=200; do  # (ROC_SYSTEM_SCOPE_SIGNAL=0 hangs)
+        env "$cfg" timeout -k 10 200 python3 tools/e2e_probe.py cfg2 8,16 > "gpurun_out/rtenv/${cfg}_$rep.log" 2>&1 \
+            || { echo "rc=$? $cfg"; tail -5 "gpurun_out/rtenv/${cfg}_$rep.log"; return 1; }
+        echo "$cfg $rep: $(grep '^{' gpurun_out/rtenv/${cfg}_$rep.log | tr '\n' ' ')"
+    done
+done
+return 0
+}
+
 if [ "${1:-}" = "--list" ] || [ $# -eq 0 ]; then
     grep -A1 '^recipe_[a-z0-9_]*() {' "$SELF" | sed -n 's/^recipe_\([a-z0-9_]*\)() {/\1/p;s/^# \(.*\)/    \1/p'
     exit 0
