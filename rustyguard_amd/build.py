@@ -28,11 +28,21 @@ API = "rg_api.cpp"
 SOURCES = KERNELS + [API]
 HEADERS = ["rg_device.h", "rg_internal.h"]
 ARCH = os.environ.get("RG_OFFLOAD_ARCH", "gfx950")
+# Per-file code generation.  The pipelined and flattened kernels run one wave per SIMD, so nothing hides a
+# hazard wait state: LLVM's iterative-ILP machine scheduler fills most of the s_nops the default strategy
+# leaves between a carry-flag write and its read (pipelined seal 604 -> 159, flattened 425 -> 135) and
+# needs fewer VGPRs there.  Config 2 +2-3 %, config 3 +0.6-1 % (profiles/r5_sched_ab.txt).  The tile kernel
+# keeps the default: at G = 2 the ILP schedule spills (scratch 52 -> 104 bytes) and its open ran 1-2 % slower.
+FILE_FLAGS = {
+    "rg_pipe.hip": ("-mllvm", "-amdgpu-sched-strategy=iterative-ilp"),
+    "rg_flat.hip": ("-mllvm", "-amdgpu-sched-strategy=iterative-ilp"),
+}
 
 
 def _inputs():
     return ([os.path.join(CSRC, f) for f in SOURCES + HEADERS] +
-            [os.path.join(REPO, "include", h) for h in ("rg_aead.h", "rg_aead_test.h")])
+            [os.path.join(REPO, "include", h) for h in ("rg_aead.h", "rg_aead_test.h")] +
+            [os.path.abspath(__file__)])  # the flags above
 
 
 def up_to_date() -> bool:
@@ -43,7 +53,7 @@ def up_to_date() -> bool:
 
 
 def _compile(hipcc: str, src: str, obj: str, defines, verbose: bool):
-    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", *defines,
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", *FILE_FLAGS.get(src, ()), *defines,
            "-I", os.path.join(REPO, "include"), "-c", os.path.join(CSRC, src), "-o", obj]
     if src.endswith(".cpp"):
         cmd[1:1] = ["-x", "hip"]

@@ -1347,6 +1347,35 @@ done
 return 0
 }
 
+recipe_r5_sched() {
+# Round 5: LLVM's machine scheduler strategy. iterative-ilp fills most hazard s_nops with independent
+# instructions (pipelined seal 604 -> 159 s_nop, flattened 425 -> 135, tile 893 -> 383) but spills in the
+# G = 2 tile kernel. Builds: tools/build_variant.sh iilp -mllvm -amdgpu-sched-strategy=iterative-ilp (all
+# kernels), VAR_ONLY="rg_pipe.hip rg_flat.hip" ... iilppf (pipelined and flattened only), ilp (max-ilp).
+# Parity on iilp (the whole GPU suite), then an interleaved A/B.
+cd "$GRAFT_REPO_ROOT" || return 1
+RG_AEAD_LIB=tools/build/librg_iilp.so timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 \
+    --timeout-method thread > gpurun_out/sched_tests.log 2>&1 || { echo "tests rc=$?"; tail -20 gpurun_out/sched_tests.log; return 1; }
+tail -2 gpurun_out/sched_tests.log
+bash tools/ab.sh "${R5_SCHED_LIBS:-base iilp iilppf}" "${R5_SCHED_WS:-cfg2 cfg3 cfg4}" "${R5_SCHED_REPS:-2}"
+}
+
+recipe_r5_sched2() {
+# Round 5: the kept build (iterative-ilp for the pipelined and flattened kernels, rustyguard_amd/build.py
+# FILE_FLAGS) against the commit before it (tools/build_rev.sh old, built from that commit:
+# default scheduler), three interleaved rounds on configs 2 and 3, then the GPU suite on the kept build and
+# a rocprofv3 kernel-trace of the default command.
+cd "$GRAFT_REPO_ROOT" || return 1
+bash tools/ab.sh "base old" "cfg2 cfg3" 3 || return 1
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+    > gpurun_out/sched2_tests.log 2>&1 || { echo "tests rc=$?"; tail -20 gpurun_out/sched2_tests.log; return 1; }
+tail -1 gpurun_out/sched2_tests.log
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || return 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/sched2_prof -o run \
+    -- python3 bench.py > gpurun_out/sched2_default.jsonl 2> gpurun_out/sched2_default.err || { echo "prof rc=$?"; return 1; }
+grep -h "seal_kernel\|open_kernel" $(find gpurun_out/sched2_prof -name "*kernel_stats.csv") | cut -c1-160
+}
+
 if [ "${1:-}" = "--list" ] || [ $# -eq 0 ]; then
     grep -A1 '^recipe_[a-z0-9_]*() {' "$SELF" | sed -n 's/^recipe_\([a-z0-9_]*\)() {/\1/p;s/^# \(.*\)/    \1/p'
     exit 0
