@@ -1376,6 +1376,18 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun
 grep -h "seal_kernel\|open_kernel" $(find gpurun_out/sched2_prof -name "*kernel_stats.csv") | cut -c1-160
 }
 
+recipe_r5_stamps_ilp() {
+# Round 5: per-wave stamps on the kept build (ILP schedule; diag build with the same flags): the pipelined
+# kernel's wave cycles at config 2 (seal mode 3, and compute-only mode 1), the flattened kernel's phases at
+# config 3.
+cd "$GRAFT_REPO_ROOT" || return 1
+export RG_AEAD_LIB=tools/build/librg_diag.so
+timeout -k 10 200 python tools/stamps.py --workload cfg2 > gpurun_out/r5_stamps_cfg2_ilp.txt 2>&1 || { tail -5 gpurun_out/r5_stamps_cfg2_ilp.txt; return 1; }
+timeout -k 10 200 python tools/stamps.py --workload cfg2 --mode 1 > gpurun_out/r5_stamps_cfg2_m1_ilp.txt 2>&1 || { tail -5 gpurun_out/r5_stamps_cfg2_m1_ilp.txt; return 1; }
+timeout -k 10 200 python tools/flat_stamps.py --workload cfg3 > gpurun_out/r5_flat_stamps_ilp.txt 2>&1 || { tail -5 gpurun_out/r5_flat_stamps_ilp.txt; return 1; }
+grep -v "^/opt" gpurun_out/r5_stamps_cfg2_ilp.txt gpurun_out/r5_stamps_cfg2_m1_ilp.txt gpurun_out/r5_flat_stamps_ilp.txt | cut -c1-220
+}
+
 if [ "${1:-}" = "--list" ] || [ $# -eq 0 ]; then
     grep -A1 '^recipe_[a-z0-9_]*() {' "$SELF" | sed -n 's/^recipe_\([a-z0-9_]*\)() {/\1/p;s/^# \(.*\)/    \1/p'
     exit 0
