@@ -75,11 +75,12 @@ template <bool WIN> __device__ __forceinline__ void fstore(const FStore &S, cons
 // ------------------------------------------------------ unit boundaries
 // Work of a packet: its one-time-key block and its 64-byte chunks (from the
 // descriptor alone).
-__device__ __forceinline__ uint32_t flat_work(const rg_pkt_desc &d, bool open) {
-    uint32_t P = open ? (d.len >= 32 ? d.len - 32 : 0u) : d.len;
+__device__ __forceinline__ uint32_t flat_work_len(uint32_t len, bool open) {
+    uint32_t P = open ? (len >= 32 ? len - 32 : 0u) : len;
     if (P > kMaxPayload) P = 0;
     return 1u + (P + 63) / 64;
 }
+__device__ __forceinline__ uint32_t flat_work(const rg_pkt_desc &d, bool open) { return flat_work_len(d.len, open); }
 
 // -------------------------------------------------------------- LDS image
 // One per wave, one record set per packet of the sub-unit, laid out so that a
@@ -476,12 +477,19 @@ template <bool OPEN, bool WIN> __global__ __launch_bounds__(64 * kFlatWaves) voi
             const uint32_t g = uniform_u32(u / kgc), j = uniform_u32(u - g * kgc);
             const uint32_t gb = g * kCoopGroup + wv * kFlatGroup;    // this wave's 1024 packets
             RG_FLAT_SUB(0);
-            rg_pkt_desc d[16];
+            // the lengths only (the work needs nothing else), as buffer loads at this lane's offset plus a
+            // scalar offset per row: all 16 issue back to back, with no 64-bit address arithmetic in front
+            // of them (the ILP schedule had put ~80 address instructions before the first load)
+            const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<rg_pkt_desc *>(desc + gb), (short)0, (int)(kFlatGroup * sizeof(rg_pkt_desc)), 0x00020000);
+            uint32_t ln[16];
 #pragma unroll
-            for (int q = 0; q < 16; ++q) d[q] = desc[gb + lane + 64 * q];
+            for (int q = 0; q < 16; ++q)
+                ln[q] = __builtin_amdgcn_raw_buffer_load_b32(drs, (int)(sizeof(rg_pkt_desc) * lane + offsetof(rg_pkt_desc, len)),
+                                                              (int)(sizeof(rg_pkt_desc) * 64 * q), 0);
             uint32_t *const tw = &L.kr[0][0];
 #pragma unroll
-            for (int q = 0; q < 16; ++q) tw[lane + 64 * q] = A.wpkt + A.wchk * (flat_work(d[q], OPEN) - 1u);
+            for (int q = 0; q < 16; ++q) tw[lane + 64 * q] = A.wpkt + A.wchk * (flat_work_len(ln[q], OPEN) - 1u);
             wave_sync();
             uint32_t e[16];
             {

@@ -1388,6 +1388,20 @@ timeout -k 10 200 python tools/flat_stamps.py --workload cfg3 > gpurun_out/r5_fl
 grep -v "^/opt" gpurun_out/r5_stamps_cfg2_ilp.txt gpurun_out/r5_stamps_cfg2_m1_ilp.txt gpurun_out/r5_flat_stamps_ilp.txt | cut -c1-220
 }
 
+recipe_r5_dlen() {
+# Round 5: the cooperative search's 16 length loads as buffer loads with a scalar offset per row (no 64-bit
+# address arithmetic before them) against the commit before (tools/build_rev.sh prev): flat/coop/forged/
+# digest GPU tests on the working tree, three interleaved config-3 rounds, then stamps of the phases.
+cd "$GRAFT_REPO_ROOT" || return 1
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "flat or coop or forged or digest or imix or random" \
+    > gpurun_out/dlen_tests.log 2>&1 || { echo "tests rc=$?"; tail -20 gpurun_out/dlen_tests.log; return 1; }
+tail -1 gpurun_out/dlen_tests.log
+bash tools/ab.sh "base prev" "cfg3" 3 || return 1
+RG_AEAD_LIB=tools/build/librg_diag.so timeout -k 10 200 python tools/flat_stamps.py --workload cfg3 > gpurun_out/r5_flat_stamps_dlen.txt 2>&1 \
+    || { tail -5 gpurun_out/r5_flat_stamps_dlen.txt; return 1; }
+grep -v "^/opt" gpurun_out/r5_flat_stamps_dlen.txt | cut -c1-700
+}
+
 if [ "${1:-}" = "--list" ] || [ $# -eq 0 ]; then
     grep -A1 '^recipe_[a-z0-9_]*() {' "$SELF" | sed -n 's/^recipe_\([a-z0-9_]*\)() {/\1/p;s/^# \(.*\)/    \1/p'
     exit 0
