@@ -1402,6 +1402,18 @@ RG_AEAD_LIB=tools/build/librg_diag.so timeout -k 10 200 python tools/flat_stamps
 grep -v "^/opt" gpurun_out/r5_flat_stamps_dlen.txt | cut -c1-700
 }
 
+recipe_r5_tile_sched() {
+# Round 5: the tile kernel under iterative-maxocc (VAR_ONLY="rg_tile.hip" tools/build_variant.sh tmaxocc
+# -mllvm -amdgpu-sched-strategy=iterative-maxocc): the G = 2 open kernel's scratch 52 -> 16 bytes, s_nop
+# 940 / 771 -> 846 / 801. Tile GPU tests on the variant, then three interleaved rounds on configs 4 and 5.
+cd "$GRAFT_REPO_ROOT" || return 1
+RG_AEAD_LIB=tools/build/librg_tmaxocc.so timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+    -k "tile or cfg4 or cfg5 or forged or digest or random or large" > gpurun_out/tsched_tests.log 2>&1 \
+    || { echo "tests rc=$?"; tail -20 gpurun_out/tsched_tests.log; return 1; }
+tail -1 gpurun_out/tsched_tests.log
+bash tools/ab.sh "base tmaxocc" "cfg4 cfg5" 3
+}
+
 if [ "${1:-}" = "--list" ] || [ $# -eq 0 ]; then
     grep -A1 '^recipe_[a-z0-9_]*() {' "$SELF" | sed -n 's/^recipe_\([a-z0-9_]*\)() {/\1/p;s/^# \(.*\)/    \1/p'
     exit 0
