@@ -306,29 +306,6 @@ __device__ __forceinline__ void flat_step(FLane &s, FChunk &b, uint32_t j, FlatL
     }
 }
 
-// h * r^e (e < 2^21), left to right over the wave's largest exponent; lanes
-// with e = 0 keep h
-__device__ __forceinline__ Acc flat_pow_mul(Acc h, const Mul &r, uint32_t e) {
-    uint32_t mx = e;
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
-    const uint32_t bits = 32 - __clz((int)uniform_u32(mx));
-    if (bits == 0) return h;
-    Acc x = {1, 0, 0, 0, 0};
-    for (int b = (int)bits - 1; b >= 0; --b) {
-        Acc sq = x;
-        acc_sqr_gen(sq);
-        Acc xr = sq;
-        acc_mul(xr, r);
-        const bool bit = (e >> b) & 1u;
-        x.h0 = bit ? xr.h0 : sq.h0; x.h1 = bit ? xr.h1 : sq.h1; x.h2 = bit ? xr.h2 : sq.h2;
-        x.h3 = bit ? xr.h3 : sq.h3; x.h4 = bit ? xr.h4 : sq.h4;
-    }
-    Acc y = h;
-    acc_mul_gen(y, make_gen(x));
-    return y;
-}
-
 // ------------------------------------------------ quad key blocks
 // One ChaCha20 block on a lane quad: lane j holds column j (rows a, b, c, d = state words j, 4 + j,
 // 8 + j, 12 + j); the diagonal rounds rotate rows b, c, d across the quad with DPP quad_perm.  Only

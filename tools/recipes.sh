@@ -1414,6 +1414,20 @@ tail -1 gpurun_out/tsched_tests.log
 bash tools/ab.sh "base tmaxocc" "cfg4 cfg5" 3
 }
 
+recipe_r5_r2l() {
+# Round 5: the flattened kernel's carry power right to left with h folded in (the multiply by r^(2^i) and
+# the next squaring are independent) against the commit before (tools/build_rev.sh prev): flat/forged/
+# digest GPU tests, three interleaved config-3 rounds, phase stamps.
+cd "$GRAFT_REPO_ROOT" || return 1
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "flat or coop or forged or digest or imix or random or large" \
+    > gpurun_out/r2l_tests.log 2>&1 || { echo "tests rc=$?"; tail -20 gpurun_out/r2l_tests.log; return 1; }
+tail -1 gpurun_out/r2l_tests.log
+bash tools/ab.sh "base prev" "cfg3" 3 || return 1
+RG_AEAD_LIB=tools/build/librg_diag.so timeout -k 10 200 python tools/flat_stamps.py --workload cfg3 > gpurun_out/r5_flat_stamps_r2l.txt 2>&1 \
+    || { tail -5 gpurun_out/r5_flat_stamps_r2l.txt; return 1; }
+grep -v "^/opt" gpurun_out/r5_flat_stamps_r2l.txt | cut -c1-600
+}
+
 if [ "${1:-}" = "--list" ] || [ $# -eq 0 ]; then
     grep -A1 '^recipe_[a-z0-9_]*() {' "$SELF" | sed -n 's/^recipe_\([a-z0-9_]*\)() {/\1/p;s/^# \(.*\)/    \1/p'
     exit 0
