@@ -542,6 +542,7 @@ __device__ __forceinline__ void acc_fold(Acc &h) {
 // s_waitcnt vmcnt(N) (loads, stores and LDS-DMA retire in issue order on one counter).
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) v4u g_v4u; // global memory, explicitly (not flat)
 
 __device__ __forceinline__ v4i make_rsrc(const uint8_t *base, uint32_t num_records) {
     const uint64_t a = (uint64_t)base;
@@ -624,17 +625,19 @@ __device__ __forceinline__ void restore_forged(bool forged, const Key8 &key, uin
         const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)plv, src), hi = (uint32_t)__shfl((int)(uint32_t)(plv >> 32), src);
         const uint32_t oc0 = (uint32_t)__shfl((int)c0, src), onb = (uint32_t)__shfl((int)nb, src);
         if (own >= 0) {
-            uint4 *p = reinterpret_cast<uint4 *>(((uint64_t)hi << 32) | lo) + 4 * oc;
+            // the shuffled address as a global pointer: a generic one compiles to flat_* accesses, which
+            // wait on the LDS counter too
+            g_v4u *p = reinterpret_cast<g_v4u *>(((uint64_t)hi << 32) | lo) + 4 * oc;
             const uint32_t b0 = 4 * oc, last = onb - 1;
-            const uint4 q0 = p[min(b0, last) - b0], q1 = p[min(b0 + 1, last) - b0];
-            const uint4 q2 = p[min(b0 + 2, last) - b0], q3 = p[min(b0 + 3, last) - b0];
+            const v4u q0 = p[min(b0, last) - b0], q1 = p[min(b0 + 1, last) - b0];
+            const v4u q2 = p[min(b0 + 2, last) - b0], q3 = p[min(b0 + 3, last) - b0];
             const Stream stm = make_stream(k, 0u, m1, m2);
             uint32_t ks[16];
             stream_block(stm, oc0 + oc + 1, ks);
-            if (b0 < onb) p[0] = xor4(q0, ks + 0);
-            if (b0 + 1 < onb) p[1] = xor4(q1, ks + 4);
-            if (b0 + 2 < onb) p[2] = xor4(q2, ks + 8);
-            if (b0 + 3 < onb) p[3] = xor4(q3, ks + 12);
+            if (b0 < onb) p[0] = q0 ^ v4u{ks[0], ks[1], ks[2], ks[3]};
+            if (b0 + 1 < onb) p[1] = q1 ^ v4u{ks[4], ks[5], ks[6], ks[7]};
+            if (b0 + 2 < onb) p[2] = q2 ^ v4u{ks[8], ks[9], ks[10], ks[11]};
+            if (b0 + 3 < onb) p[3] = q3 ^ v4u{ks[12], ks[13], ks[14], ks[15]};
         }
         own = -1;
     };

@@ -1428,6 +1428,22 @@ RG_AEAD_LIB=tools/build/librg_diag.so timeout -k 10 200 python tools/flat_stamps
 grep -v "^/opt" gpurun_out/r5_flat_stamps_r2l.txt | cut -c1-600
 }
 
+recipe_r5_restore_global() {
+# Round 5: the forged-frame restore (rg_device.h restore_forged) through explicit global pointers instead of
+# generic ones (the pipelined open had 16 flat_* accesses there, now none): forged/open GPU tests, then the
+# bench's forged-open legs (1 % and 10 % forged) on config 2 and the tile geometry, against the commit before.
+cd "$GRAFT_REPO_ROOT" || return 1
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "forged or open or roundtrip" \
+    > gpurun_out/rg_tests.log 2>&1 || { echo "tests rc=$?"; tail -20 gpurun_out/rg_tests.log; return 1; }
+tail -1 gpurun_out/rg_tests.log
+for r in 1 2; do for v in base prev; do
+    if [ $v = base ]; then unset RG_AEAD_LIB; else export RG_AEAD_LIB=tools/build/librg_$v.so; fi
+    timeout -k 10 200 python bench.py --workload cfg2 --steps 10 --warmup 3 --cpu-seconds 0 --no-cold > gpurun_out/rg_${v}_$r.log 2>&1 || return 1
+    echo "$v $r $(grep '"value"' gpurun_out/rg_${v}_$r.log | python3 -c 'import sys,json; d=json.loads(sys.stdin.read()); print(d["value"], [(f["forged_frac"], f["open_ms"], f["clean_open_ms"], f["ratio"]) for f in d["forged_open"]])')"
+done; done
+unset RG_AEAD_LIB
+}
+
 if [ "${1:-}" = "--list" ] || [ $# -eq 0 ]; then
     grep -A1 '^recipe_[a-z0-9_]*() {' "$SELF" | sed -n 's/^recipe_\([a-z0-9_]*\)() {/\1/p;s/^# \(.*\)/    \1/p'
     exit 0
