@@ -161,51 +161,71 @@ def host_cpu_info() -> dict:
     return {"cpu_model": model, "nproc": os.cpu_count(), "affinity": aff}
 
 
-def all_core_threads(requested: int) -> int:
-    """The host's CPU share: on the GPU box nproc and the affinity mask show the whole machine while
-    the job's share is OMP_NUM_THREADS (16 per GPU); here it is the affinity mask."""
-    if requested:
-        return requested
+def cgroup_cpu_quota():
+    """The job's CPU quota from its cgroup (v2 cpu.max, else v1 cfs quota / period) in CPUs, or None when
+    unlimited / unreadable."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        return None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = int(f.read())
+        return None if q <= 0 else q / per
+    except (OSError, ValueError):
+        return None
+
+
+def all_core_threads(requested: int):
+    """(threads, how): the host's CPU share for the all-core baseline -- the smallest of the affinity mask,
+    the cgroup CPU quota (cpu.max, rounded down) and OMP_NUM_THREADS (16 per GPU on the GPU box, where
+    nproc and the affinity mask show the whole 256-CPU machine)."""
     aff = host_cpu_info()["affinity"]
+    quota = cgroup_cpu_quota()
     omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-    return max(1, min(aff, omp) if omp > 0 else aff)
+    limits = {"affinity": aff}
+    if quota is not None:
+        limits["cgroup_cpu_max"] = quota
+    if omp > 0:
+        limits["OMP_NUM_THREADS"] = omp
+    if requested:
+        return requested, {"requested": requested, **limits}
+    t = max(1, min([aff] + ([int(quota)] if quota is not None else []) + ([omp] if omp > 0 else [])))
+    return t, limits
 
 
-def cpu_rate(w, impl: str, threads: int, rep_seconds: float, reps: int = 5):
-    """Median of `reps` timed runs (after one warm-up run) of seal+open over a bounded sample of the
-    workload on `threads` host threads: GiB/s of payload and Mpkt/s."""
+CPU_SAMPLE = 65536  # packets: >= 64 Ki (VERDICT r5 item 4); config 2's whole batch
+
+
+def cpu_rate(w, impl: str, threads: int, rep_seconds: float, reps: int = 3):
+    """Median of `reps` timed runs of seal+open over a sample of the workload (its first CPU_SAMPLE
+    packets) by a persistent pool of `threads` workers (oracle/rg_openssl_batch.c rg_cpu_bench: threads
+    and OpenSSL cipher contexts live for the whole run, one untimed round first): GiB/s of payload and
+    Mpkt/s."""
     from oracle import oracle  # checker / baseline only
 
-    seal = oracle.openssl_seal_batch if impl == "openssl" else oracle.seal_batch
-    n = min(w.n, 4096)
+    n = min(w.n, CPU_SAMPLE)
     desc = w.desc[:n].copy()
     base = int(desc["offset"][0])
     desc["offset"] -= np.uint64(base)
     span = int(desc["offset"][-1]) + int(desc["len"][-1]) + 32
     buf = np.zeros(span, np.uint8)
     oracle.synth_fill(buf, desc, w.inner_len[:n], w.data_seed)
-    od = desc.copy()
-    od["len"] += np.uint32(32)
+    plain = buf.copy()
     ctr = w.counters[:n]
     payload = int(desc["len"].astype(np.int64).sum())
-
-    def one(seconds):
-        reps_, t0 = 0, time.perf_counter()
-        while True:
-            seal(w.keys, w.receivers, desc, ctr, buf, nthreads=threads)
-            if impl == "openssl":
-                st = oracle.openssl_open_batch(w.keys, od, buf, nthreads=threads)
-            else:
-                st, _ = oracle.open_batch(w.keys, od, buf, nthreads=threads)
-            reps_ += 1
-            el = time.perf_counter() - t0
-            if el >= seconds:
-                break
-        assert (st == 0).all()
-        return 2 * payload * reps_ / el / 2**30, 2 * n * reps_ / el / 1e6
-
-    one(min(0.2, rep_seconds))
-    runs = [one(rep_seconds) for _ in range(reps)]
+    runs = []
+    for _ in range(reps):
+        el, rounds = oracle.cpu_bench(impl, threads, w.keys, w.receivers, desc, ctr, buf, rep_seconds)
+        runs.append((2 * payload * rounds / el / 2**30, 2 * n * rounds / el / 1e6))
+    pay = np.zeros(span, bool)  # payload bytes (headers and tags are rewritten by every seal)
+    for o, ln in zip(desc["offset"].astype(np.int64), desc["len"].astype(np.int64)):
+        pay[o + 16:o + 16 + ln] = True
+    assert np.array_equal(buf[pay], plain[pay]), "a seal+open round did not give the plaintext back"
     gib = sorted(r[0] for r in runs)[reps // 2]
     mpkt = sorted(r[1] for r in runs)[reps // 2]
     return {"value": round(gib, 4), "unit": "GiB/s", "cores": threads, "mpkt_s": round(mpkt, 4),
@@ -213,16 +233,18 @@ def cpu_rate(w, impl: str, threads: int, rep_seconds: float, reps: int = 5):
             "mean_payload": round(payload / n, 1)}
 
 
-def cpu_baselines(w, seconds: float, threads: int):
+def cpu_baselines(w, seconds: float, threads_how):
     """CPU baselines of BASELINE.md §2, in the same run as the GPU numbers: the C restatement
     (kind "port": the reference's Rust + graviola 0.2.0 path cannot be built here -- no cargo, crate
     not vendored) and OpenSSL EVP ChaCha20-Poly1305 (an assembly-optimised stand-in for graviola),
-    each on 1 thread and on the host's cores, median of 5 runs over a bounded sample."""
+    each on 1 thread and on the host's share of cores, median of 3 runs over a 64 Ki-packet sample.
+    scaling = all-core rate / (threads x 1-thread rate)."""
     from oracle import oracle
 
+    threads, limits = threads_how
     info = host_cpu_info()
     impls = ["port"] + (["openssl"] if oracle.openssl_available() else [])
-    rep = max(0.1, seconds / (len(impls) * 2 * 5))
+    rep = max(0.2, seconds / (len(impls) * 2 * 3))
     out = {}
     for impl in impls:
         many = cpu_rate(w, impl, threads, rep)
@@ -233,8 +255,13 @@ def cpu_baselines(w, seconds: float, threads: int):
         d["kind"] = "port" if impl == "port" else "openssl (stand-in for graviola)"
         d["one_thread"] = {"value": one["value"], "unit": "GiB/s", "mpkt_s": one["mpkt_s"],
                            "runs_gib_s": one["runs_gib_s"]}
+        eff = many["value"] / (threads * one["value"]) if one["value"] > 0 else None
+        d["scaling"] = {"speedup": round(many["value"] / one["value"], 2) if one["value"] else None,
+                        "efficiency": round(eff, 3) if eff is not None else None, "threads": threads,
+                        "thread_limits": limits}
         d["sample"] = (f"first {many['n_sample']} packets of {w.name} (mean P={many['mean_payload']}) sealed then "
-                       f"opened, {rep:.2f} s per run, median of 5 runs on {threads} threads and on 1 thread; {what}")
+                       f"opened by a persistent pool (threads and cipher contexts kept across rounds), {rep:.2f} s "
+                       f"per run, median of 3 runs on {threads} threads and on 1 thread; {what}")
         d.update(info)
         out[impl] = d
     return out.get("port"), out.get("openssl")

@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define RG_ABI_VERSION 5
+#define RG_ABI_VERSION 6
 
 typedef struct rg_ctx rg_ctx;
 
@@ -87,7 +87,20 @@ enum rg_pkt_status {
     RG_PKT_UNALIGNED = 4,   /* Error::Unaligned: frame not 16-byte aligned */
     RG_PKT_NOT_DATA = 5,    /* type 1, 2 or 3 (handshake init/resp, cookie): route to the
                                handshake path (lib.rs:622-624) */
+    RG_PKT_PENDING = 6,     /* no verdict: the packet was never finished (the call failed, a device
+                               error, or a batch still in flight).  Never an accept. */
 };
+
+/* Statuses fail closed.  A packet reads RG_PKT_OK only after the kernel that processed it wrote that
+ * verdict: every launch that hands packets from one workgroup to another (the planned pipelined kernel,
+ * the tile kernels) is preceded, on the same stream, by a preset pass that sets the batch's statuses to
+ * RG_PKT_PENDING and clears the planner's control words; the launches without a hand-off (the pipelined
+ * kernel in array order, the flattened kernel) deal every packet to a lane by its index alone, and that
+ * lane writes its status.  The host-memory calls (rg_*_batch_host*, rg_send_batch, rg_recv_batch*) check
+ * after the device work that no status is still RG_PKT_PENDING (RG_EDEVICE otherwise), and every host-memory
+ * call that returns an error leaves all n statuses RG_PKT_PENDING: no replay window or endpoint moves on
+ * a failed batch.  rg_recv_batch_dev_finish runs the replay pass only over RG_PKT_OK / RG_PKT_DECRYPT_ERR
+ * verdicts and returns RG_EDEVICE when any packet is still pending. */
 
 /* ---------------------------------------------------------------- context */
 
@@ -97,7 +110,11 @@ int rg_abi_version(void);
  * in device memory (the host calls' key table, the MAC key states, the per-message arena) is zeroed
  * before its memory is reused or freed, in stream order: behind the launches that read it, without
  * waiting for the device or for other streams (prim.rs:227-231 zeroizes keys on drop).  A call that would
- * have to regrow such a buffer while its stream is being captured into a graph fails with RG_EDEVICE. */
+ * have to regrow such a buffer while its stream is being captured into a graph fails with RG_EDEVICE.  A
+ * block that a captured launch reads is never freed under the graph: a later regrow takes a new block and
+ * keeps the captured one allocated until rg_destroy (rg_sessions_destroy for a session table's rows),
+ * which zeroes and frees it; such a graph must not be replayed after that.  rg_create refuses (RG_EINVAL) to run under ROC_SYSTEM_SCOPE_SIGNAL=0: agent-scope completion
+ * signals hung the host pipeline's waits in round 5 (profiles/r5_e2e_rtenv.txt). */
 int rg_create(int device, rg_ctx **out);
 void rg_destroy(rg_ctx *ctx);
 /* Text of the last error on this thread ("" if none). */
@@ -106,11 +123,16 @@ const char *rg_last_error(void);
 /* --------------------------------------- device-resident batch (async) */
 /* Every pointer is device memory; work is enqueued on `stream`
  * (hipStream_t, NULL = legacy default stream) and the call returns without
- * synchronising.  status/counters_out may be NULL for seal.  The kernels
- * bounds-check every descriptor against buf_len and never touch memory
- * outside [buf, buf + buf_len).  Calls on one context are ordered on one stream
- * (they share the planner buffers and the tile kernel's work pool, see
- * rg_set_plan); use a context per concurrent stream. */
+ * synchronising.  status is required (ABI 6: it is how a caller knows a packet
+ * was sealed; RG_PKT_OK is written only by the lane that sealed it), receivers /
+ * counters_out may be NULL.  The kernels bounds-check every descriptor against
+ * buf_len and never touch memory outside [buf, buf + buf_len).  Calls on one
+ * context are ordered on one stream (they share the planner buffers and the tile
+ * kernel's work pool, see rg_set_plan); use a context per concurrent stream.  A
+ * call on another stream while this context's last batch is still in flight on
+ * its stream fails with RG_EINVAL and enqueues nothing (the check needs no
+ * wait: an event query; launches captured into a graph are not tracked, so a
+ * graph counts as work of the stream it was captured on). */
 int rg_seal_batch_dev(rg_ctx *ctx, const uint8_t *keys, const uint32_t *receivers, uint32_t nkeys,
                       const rg_pkt_desc *desc, const uint64_t *counters, size_t n, uint8_t *buf, size_t buf_len,
                       uint8_t *status, void *stream);
@@ -220,8 +242,15 @@ int rg_set_debug_buffer(rg_ctx *ctx, void *dev_ptr);
 /* Same contract with host pointers: frames are staged H2D, sealed/opened on
  * the GPU and copied back D2H, pipelined over three streams.  Pinned memory
  * (rg_host_alloc) gives the full PCIe rate.  rg_set_host_slice sets the byte
- * span of one pipeline slice (default 8 MiB; 64 KiB .. 1 GiB). */
+ * span of one pipeline slice (default 8 MiB; 64 KiB .. 1 GiB).
+ *
+ * Every host wait of the library is bounded: a completion the device does not
+ * report within rg_set_wait_timeout's limit (default 10 000 ms per wait; 1 ..
+ * 3 600 000) ends the call with RG_EDEVICE ("... timed out") and every status
+ * RG_PKT_PENDING, instead of blocking forever.  Waits poll (hipEventQuery),
+ * yielding the CPU between polls and sleeping once a wait has run 2 ms. */
 int rg_set_host_slice(rg_ctx *ctx, size_t bytes);
+int rg_set_wait_timeout(rg_ctx *ctx, uint32_t ms);
 int rg_seal_batch_host(rg_ctx *ctx, const uint8_t *keys, const uint32_t *receivers, uint32_t nkeys,
                        const rg_pkt_desc *desc, const uint64_t *counters, size_t n, uint8_t *buf, size_t buf_len,
                        uint8_t *status);
@@ -350,8 +379,8 @@ int rg_sessions_keepalive(rg_sessions *s, uint32_t slot, uint64_t *dst_out);
  * (the packet's session decides it).  Counters are reserved on the host in array order as
  * rg_send_batch does; since the lengths are on the device, a frame with P % 16 != 0 still takes
  * a counter and the kernel reports it RG_PKT_INVALID (nonces stay unique).  status (device,
- * nullable) gets the per-packet statuses.  Two sends may be in flight; a third waits for the
- * first one's seal. */
+ * required as for rg_seal_batch_dev) gets the per-packet statuses.  Two sends may be in flight; a
+ * third waits for the first one's seal. */
 int rg_send_batch_dev(rg_sessions *s, const uint32_t *slots, const rg_pkt_desc *desc, size_t n, uint8_t *buf,
                       size_t buf_len, uint8_t *status, uint8_t *rekey_out, void *stream);
 /* rg_recv_batch_dev enqueues receiver resolution (rg_open_batch_dev_rx), the GPU open and

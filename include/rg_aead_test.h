@@ -26,6 +26,24 @@ extern "C" {
 int rg_debug_read_arena(rg_ctx *ctx, int which, void *dst, size_t bytes);
 void rg_debug_fail_reserve(int nth);
 
+/* Fail-closed hooks.  rg_debug_plan_handoff(1) starts the planner's finished-workgroup count
+ * stale in the preset pass, so no planner workgroup finds itself last and the pipelined kernel's schedule
+ * is never handed over; (2) starts the tile kernel's grid-wide pool past its end, so the pooled tiles are
+ * never taken; (0) off.  Every packet such a launch never reaches must read RG_PKT_PENDING.
+ * rg_debug_lose_completions(1) makes every library wait see its event as never completing (the bounded
+ * waits then time out).  rg_debug_wait_selftest runs the bounded wait loop against a fake completion that
+ * arrives on poll ready_after + 1 (never, for UINT32_MAX) -- no HIP call, so it runs without a GPU -- and
+ * returns RG_OK or RG_EDEVICE (timed out), with the polls made and the time taken.
+ * rg_debug_last_wipe copies the first bytes of the most recently wiped key block, read back from the device
+ * after its wipe and before its free, and reports how many blocks were wiped so far.
+ * rg_debug_secret_state reports whether a key buffer of the context is read by a captured launch (1) or
+ * not (0), how many captured blocks a regrow retired, and how many stream events guard it. */
+void rg_debug_plan_handoff(int mode);
+void rg_debug_lose_completions(int on);
+int rg_debug_wait_selftest(uint32_t timeout_ms, uint32_t ready_after, uint32_t *polls_out, uint32_t *elapsed_ms_out);
+int64_t rg_debug_last_wipe(void *dst, size_t bytes, uint64_t *wipes_out);
+int rg_debug_secret_state(rg_ctx *ctx, int which, uint32_t *retired_out, uint32_t *users_out);
+
 #ifdef __cplusplus
 }
 #endif

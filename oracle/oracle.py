@@ -62,6 +62,9 @@ def lib():
         L.rg_openssl_seal_batch.restype = ctypes.c_int
         L.rg_openssl_open_batch.argtypes = [u8p, u8p, ctypes.c_size_t, u8p, u8p, ctypes.c_int]
         L.rg_openssl_open_batch.restype = ctypes.c_int
+        L.rg_cpu_bench.argtypes = [ctypes.c_int, ctypes.c_int, u8p, u8p, u8p, u8p, ctypes.c_size_t, u8p,
+                                   ctypes.c_double, u8p]
+        L.rg_cpu_bench.restype = ctypes.c_int
         L.rg_cpu_time_one.argtypes = [ctypes.c_int, u8p, ctypes.c_uint32, ctypes.c_uint64, u8p]
         L.rg_cpu_time_one.restype = ctypes.c_int
         _lib = L
@@ -235,6 +238,23 @@ def openssl_open_batch(keys, desc, buf, nthreads=1):
     if rc != 0:
         raise RuntimeError("libcrypto.so.3 not available")
     return status[: len(desc)]
+
+
+def cpu_bench(impl: str, nthreads: int, keys, receivers, desc, counters, buf, seconds: float):
+    """CPU baseline harness (rg_openssl_batch.c rg_cpu_bench): a persistent pool of `nthreads` workers
+    seals then opens its slice of the sample in rounds for `seconds`; impl "port" (the C restatement) or
+    "openssl" (EVP, one cipher context per worker, re-keyed per packet).  Returns (elapsed_s, rounds)."""
+    keys = np.ascontiguousarray(keys, dtype=np.uint8)
+    counters = np.ascontiguousarray(counters, dtype=np.uint64)
+    rec = None if receivers is None else np.ascontiguousarray(receivers, dtype=np.uint32)
+    out = np.zeros(3, np.float64)
+    rc = lib().rg_cpu_bench(1 if impl == "openssl" else 0, nthreads, _ptr(keys), _ptr(rec), _ptr(desc),
+                            _ptr(counters), len(desc), _ptr(buf), seconds, _ptr(out))
+    if rc != 0:
+        raise RuntimeError(f"rg_cpu_bench({impl}, {nthreads}) failed: {rc}")
+    if out[2] != 0:
+        raise RuntimeError(f"rg_cpu_bench({impl}): {int(out[2])} packets failed to seal or open")
+    return float(out[0]), int(out[1])
 
 
 def time_one(impl: str, key: bytes, P: int, iters: int) -> tuple[float, float]:

@@ -221,3 +221,158 @@ int rg_cpu_time_one(int impl, const uint8_t key[32], uint32_t P, uint64_t iters,
     out_ns[1] = t_open / (double)(iters ? iters : 1);
     return ok ? 0 : -3;
 }
+
+/* ---- CPU baseline harness (bench.py cpu_baseline) ----
+ * Round 5 timed the baselines through rg_*_batch above, which start fresh threads -- and, for OpenSSL, a
+ * fresh EVP_CIPHER_CTX and cipher fetch -- per call, on a 4096-packet sample: 256 packets (~200 us) per
+ * thread per call, so thread start-up and joins dominated the all-core figure (OpenSSL 3.3x on 16 threads).
+ * rg_cpu_bench keeps one pool for the whole measurement: nthreads workers, each owning a fixed slice of
+ * the sample and (OpenSSL) one cipher context for its lifetime, run in rounds between two barriers; a
+ * round seals the slice then opens it again (the frames return to plaintext, so every round does the same
+ * work).  One untimed round first; then rounds until `seconds` have passed.
+ * impl 0: the C restatement (rg_oracle_seal_one / _open_one); 1: OpenSSL EVP, re-keyed per packet.
+ * out[0] = elapsed seconds of the timed rounds, out[1] = timed rounds, out[2] = packets whose seal or open
+ * failed (0 expected). */
+#include <sched.h>
+
+typedef struct {
+    int impl;
+    const uint8_t *keys;
+    const uint32_t *receivers;
+    const rg_oracle_desc *desc;
+    const uint64_t *counters;
+    uint8_t *buf;
+    size_t n;
+    int nthreads;
+    pthread_barrier_t start, done;
+    volatile int stop;
+    volatile uint64_t bad;
+    pthread_mutex_t mu;
+} pool_t;
+
+typedef struct {
+    pool_t *p;
+    int t;
+} pool_arg_t;
+
+static uint64_t pool_round(pool_t *p, EVP_CIPHER_CTX *c, size_t lo, size_t hi) {
+    uint64_t bad = 0;
+    uint8_t nonce[12], st = 0;
+    int outl = 0;
+    for (size_t i = lo; i < hi; i++) { /* seal: desc.len = P */
+        const rg_oracle_desc *d = &p->desc[i];
+        uint8_t *frame = p->buf + d->offset;
+        if (p->impl == 0) {
+            rg_oracle_seal_one(p->keys, p->receivers, d, p->counters[i], p->buf, &st);
+            bad += st != RG_ORACLE_OK;
+        } else {
+            int ok = 1;
+            rg_oracle_wg_nonce(p->counters[i], nonce);
+            ok &= ssl.cipher_init(c, NULL, NULL, p->keys + 32 * (size_t)d->key_idx, nonce, 1);
+            ok &= ssl.cipher_update(c, frame + 16, &outl, frame + 16, (int)d->len);
+            ok &= ssl.cipher_final(c, frame + 16 + d->len, &outl);
+            ok &= ssl.ctrl(c, CTRL_AEAD_GET_TAG, 16, frame + 16 + d->len);
+            put32(frame, 4u);
+            put32(frame + 4, p->receivers ? p->receivers[d->key_idx] : 0u);
+            put64(frame + 8, p->counters[i]);
+            bad += !ok;
+        }
+    }
+    for (size_t i = lo; i < hi; i++) { /* open the frames just sealed: W = P + 32 */
+        rg_oracle_desc d = p->desc[i];
+        d.len += 32;
+        uint8_t *frame = p->buf + d.offset;
+        if (p->impl == 0) {
+            rg_oracle_open_one(p->keys, &d, p->buf, &st, NULL);
+            bad += st != RG_ORACLE_OK;
+        } else {
+            int ok = 1;
+            const uint32_t P = d.len - 32;
+            rg_oracle_wg_nonce(get64(frame + 8), nonce);
+            ok &= ssl.cipher_init(c, NULL, NULL, p->keys + 32 * (size_t)d.key_idx, nonce, 0);
+            ok &= ssl.ctrl(c, CTRL_AEAD_SET_TAG, 16, frame + 16 + P);
+            ok &= ssl.cipher_update(c, frame + 16, &outl, frame + 16, (int)P);
+            ok &= ssl.cipher_final(c, frame + 16 + P, &outl) > 0;
+            bad += !ok;
+        }
+    }
+    return bad;
+}
+
+static void *pool_worker(void *arg) {
+    pool_arg_t *a = (pool_arg_t *)arg;
+    pool_t *p = a->p;
+    const size_t lo = p->n * (size_t)a->t / (size_t)p->nthreads, hi = p->n * (size_t)(a->t + 1) / (size_t)p->nthreads;
+    EVP_CIPHER_CTX *c = NULL;
+    if (p->impl == 1) { /* one context for the worker's lifetime, the cipher bound once */
+        c = ssl.ctx_new();
+        ssl.cipher_init(c, ssl.chacha(), NULL, NULL, NULL, 1);
+    }
+    uint64_t bad = 0;
+    for (;;) {
+        pthread_barrier_wait(&p->start);
+        if (p->stop) break;
+        bad += pool_round(p, c, lo, hi);
+        pthread_barrier_wait(&p->done);
+    }
+    if (c) ssl.ctx_free(c);
+    pthread_mutex_lock(&p->mu);
+    p->bad += bad;
+    pthread_mutex_unlock(&p->mu);
+    return NULL;
+}
+
+int rg_cpu_bench(int impl, int nthreads, const uint8_t *keys, const uint32_t *receivers, const rg_oracle_desc *desc,
+                 const uint64_t *counters, size_t n, uint8_t *buf, double seconds, double out[3]) {
+    if (impl == 1 && !rg_openssl_available()) return -1;
+    if (nthreads < 1 || nthreads > 256 || n == 0) return -2;
+    pool_t p;
+    memset(&p, 0, sizeof p);
+    p.impl = impl;
+    p.keys = keys;
+    p.receivers = receivers;
+    p.desc = desc;
+    p.counters = counters;
+    p.buf = buf;
+    p.n = n;
+    p.nthreads = nthreads;
+    pthread_barrier_init(&p.start, NULL, (unsigned)nthreads + 1);
+    pthread_barrier_init(&p.done, NULL, (unsigned)nthreads + 1);
+    pthread_mutex_init(&p.mu, NULL);
+    pthread_t th[256];
+    pool_arg_t args[256];
+    int started = 0;
+    for (; started < nthreads; started++) {
+        args[started].p = &p;
+        args[started].t = started;
+        if (pthread_create(&th[started], NULL, pool_worker, &args[started]) != 0) break;
+    }
+    if (started < nthreads) { /* cannot run the measurement as asked: release the ones that started */
+        /* the barriers count nthreads + 1: a short pool would block forever, so nothing ran yet */
+        for (int t = 0; t < started; t++) pthread_cancel(th[t]);
+        for (int t = 0; t < started; t++) pthread_join(th[t], NULL);
+        return -3;
+    }
+    /* one untimed round (first-touch, caches, frequency ramp) */
+    pthread_barrier_wait(&p.start);
+    pthread_barrier_wait(&p.done);
+    uint64_t rounds = 0;
+    const double t0 = now_ns();
+    double el = 0;
+    do {
+        pthread_barrier_wait(&p.start);
+        pthread_barrier_wait(&p.done);
+        rounds++;
+        el = (now_ns() - t0) * 1e-9;
+    } while (el < seconds);
+    p.stop = 1;
+    pthread_barrier_wait(&p.start);
+    for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+    pthread_barrier_destroy(&p.start);
+    pthread_barrier_destroy(&p.done);
+    pthread_mutex_destroy(&p.mu);
+    out[0] = el;
+    out[1] = (double)rounds;
+    out[2] = (double)p.bad;
+    return 0;
+}

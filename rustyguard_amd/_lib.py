@@ -88,12 +88,18 @@ SIGNATURES = {
     "rg_open_batch_dev_multi": (c_int, [c_vp, c_vp]),
     "rg_sessions_create_group": (c_int, [c_vp, c_u32, ctypes.POINTER(c_vp)]),
     "rg_set_host_slice": (c_int, [c_vp, c_size]),
+    "rg_set_wait_timeout": (c_int, [c_vp, c_u32]),
 }
 
 # include/rg_aead_test.h: exported by the test library (librg_aead_test.so) only
 TEST_SIGNATURES = {
     "rg_debug_read_arena": (c_int, [c_vp, c_int, c_vp, c_size]),
     "rg_debug_fail_reserve": (None, [c_int]),
+    "rg_debug_plan_handoff": (None, [c_int]),
+    "rg_debug_lose_completions": (None, [c_int]),
+    "rg_debug_wait_selftest": (c_int, [c_u32, c_u32, c_vp, c_vp]),
+    "rg_debug_last_wipe": (ctypes.c_int64, [c_vp, c_size, c_vp]),
+    "rg_debug_secret_state": (c_int, [c_vp, c_int, c_vp, c_vp]),
 }
 
 

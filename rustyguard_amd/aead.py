@@ -26,7 +26,7 @@ from . import _lib
 from ._lib import check, lib
 from .workloads import DESC_DTYPE
 
-PKT_OK, PKT_DECRYPT_ERR, PKT_INVALID, PKT_REJECTED, PKT_UNALIGNED, PKT_NOT_DATA = range(6)
+PKT_OK, PKT_DECRYPT_ERR, PKT_INVALID, PKT_REJECTED, PKT_UNALIGNED, PKT_NOT_DATA, PKT_PENDING = range(7)
 RECV_AUTHENTICATED, RECV_KEEPALIVE = 1, 2
 KEY_SCAN = 0xFFFFFFFE  # rg_mac_verify_batch_dev: try every key
 KEY_SKIP = 0xFFFFFFFF
@@ -155,6 +155,10 @@ class Engine:
         """Byte span of one host-pipeline slice (rg_set_host_slice; default 8 MiB)."""
         self._check(self._L.rg_set_host_slice(self._h, nbytes), "rg_set_host_slice")
 
+    def set_wait_timeout(self, ms: int):
+        """Limit of every host wait of the library, in ms (rg_set_wait_timeout; default 10 000)."""
+        self._check(self._L.rg_set_wait_timeout(self._h, ms), "rg_set_wait_timeout")
+
     def set_wg_per_cu(self, wg: int):
         self._check(self._L.rg_set_wg_per_cu(self._h, wg), "rg_set_wg_per_cu")
 
@@ -162,8 +166,9 @@ class Engine:
         return self._check(self._L.rg_get_lanes_per_packet(self._h, n), "rg_get_lanes_per_packet")
 
     # ---------------------------------------------------- device-resident
-    def seal_dev(self, keys, receivers, desc, counters, buf, status=None, stream=None):
-        """Enqueue a batched seal on `stream`; all tensors on this device."""
+    def seal_dev(self, keys, receivers, desc, counters, buf, status, stream=None):
+        """Enqueue a batched seal on `stream`; all tensors on this device.  status (uint8, one per packet) is
+        required: RG_PKT_OK there is the proof that the packet was sealed (ABI 6)."""
         n = _ndesc(desc)
         nkeys = _nbytes(keys) // 32
         self._check(self._L.rg_seal_batch_dev(self._h, _vp(keys), _vp(receivers), nkeys, _vp(desc), _vp(counters), n,
@@ -535,7 +540,7 @@ class Sessions:
                                      _vp(slots), _vp(fl)), "rg_recv_batch_ex")
         return (status[:n], slots[:n], fl[:n]) if flags else (status[:n], slots[:n])
 
-    def send_batch_dev(self, slots, desc, buf, status=None, stream=None):
+    def send_batch_dev(self, slots, desc, buf, status, stream=None):
         """rg_send_batch_dev: device frames / descriptors (torch tensors), host slots; enqueued on
         `stream`, returns the rekey flags (host) without waiting for the GPU."""
         slots = np.ascontiguousarray(slots, np.uint32)

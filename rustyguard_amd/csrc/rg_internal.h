@@ -261,4 +261,21 @@ hipError_t launch_undo_gather(const rg_pkt_desc *rd, const uint64_t *ctr, const 
 hipError_t launch_synth_fill(const rg_pkt_desc *desc, const uint32_t *inner_len, uint32_t n, uint8_t *buf,
                              uint64_t buf_len, uint64_t seed, hipStream_t s);
 
+// Control words of one planner (rg_api.cpp PlanBuf): the planner's class counts and finished-workgroup
+// count, the pipelined kernel's schedule and the tile kernel's work pool, in one block that the preset
+// pass clears before every launch that hands work from one workgroup to another.
+constexpr uint32_t kCtlCounts = 0;   // [kClasses] class counts, [kClasses] finished planner / tile workgroups
+constexpr uint32_t kCtlSched = 64;   // [kSchedWords] pipelined kernel's schedule
+constexpr uint32_t kCtlPool = 192;   // [0] next pool item, [32] workgroups done (tile kernel)
+constexpr uint32_t kCtlWords = 256;
+static_assert(kCtlCounts + kClasses + 1 <= kCtlSched && kCtlSched + kSchedWords <= kCtlPool &&
+                  kCtlPool + 33 <= kCtlWords, "control block layout");
+// Preset pass (rg_kernels.hip), ahead of every launch whose packets are handed between workgroups (the
+// planned pipelined kernel, the tile kernels): status[0, n) = RG_PKT_PENDING, so a packet the transport
+// kernel never reaches cannot read as RG_PKT_OK, and ctl[0, kCtlWords) = 0 except ctl[kCtlCounts +
+// kClasses] = done_init and ctl[kCtlPool] = pool_init (both 0; the test library's hand-off hooks start
+// them stale).  status may be nullptr.
+hipError_t launch_preset(uint8_t *status, uint32_t n, uint32_t *ctl, uint32_t done_init, uint32_t pool_init,
+                         hipStream_t s);
+
 } // namespace rg

@@ -212,7 +212,28 @@ __global__ __launch_bounds__(256) void synth_fill_kernel(const rg_pkt_desc *desc
     }
 }
 
+// ---------------------------------------------------------------- preset
+// Fail-closed statuses (rg_internal.h): every status of the batch reads RG_PKT_PENDING until the transport
+// kernel writes the packet's verdict, and the planner's control block starts from zero.  Byte stores,
+// coalesced 64 per wave instruction; workgroup 0 also clears the control words.
+__global__ __launch_bounds__(256) void preset_kernel(uint8_t *status, uint32_t n, uint32_t *ctl, uint32_t done_init,
+                                                     uint32_t pool_init) {
+    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+    if (ctl && blockIdx.x == 0)
+        for (uint32_t w = threadIdx.x; w < kCtlWords; w += 256)
+            ctl[w] = w == kCtlCounts + kClasses ? done_init : w == kCtlPool ? pool_init : 0u;
+    if (!status) return;
+    for (uint32_t i = t; i < n; i += gridDim.x * 256) status[i] = RG_PKT_PENDING;
+}
+
 // ---------------------------------------------------------------- launch
+hipError_t launch_preset(uint8_t *status, uint32_t n, uint32_t *ctl, uint32_t done_init, uint32_t pool_init,
+                         hipStream_t s) {
+    const uint32_t blocks = status ? max(1u, min(1024u, (n + 1023) / 1024)) : 1u;
+    hipLaunchKernelGGL(preset_kernel, dim3(blocks), dim3(256), 0, s, status, n, ctl, done_init, pool_init);
+    return hipGetLastError();
+}
+
 hipError_t launch_general(GeneralJob *jobs, uint32_t njobs, uint8_t *arena, hipStream_t s) {
     if (njobs == 0) return hipSuccess;
     hipLaunchKernelGGL(general_kernel, dim3(njobs), dim3(64), 0, s, jobs, njobs, arena);

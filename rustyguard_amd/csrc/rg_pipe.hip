@@ -164,9 +164,19 @@ __device__ __forceinline__ Ring pin_window(const Ring &R) {
     return o;
 }
 
+// Cache policy of a line-store wave's last stores -- the lines stored after its final keystream step
+// (the ring's last half-lines, the partial last chunk, the tag): 0 write-back (default), 16 write-through
+// (sc1), 2 non-temporal.  A store-heavy launch ends with the dirty lines of the XCDs' L2s written back
+// after its last wave (MI355X_MICROARCH.md, the "boundary" row); write-through final stores leave fewer of
+// them (tools/l2tail.hip, round 6).  Diagnostic builds set it with -DRG_TAIL_CP.
+#ifndef RG_TAIL_CP
+#define RG_TAIL_CP 0
+#endif
+constexpr int kTailCp = RG_TAIL_CP;
+
 // a 16-byte piece of this lane's frame at byte `off` of the frame (line-store waves)
-__device__ __forceinline__ void frame_store(const Ring &R, uint32_t off, const uint4 &x) {
-    __builtin_amdgcn_raw_buffer_store_b128(to_v4(x), R.rs, (int)(R.self + off), 0, 0);
+template <int CP = 0> __device__ __forceinline__ void frame_store(const Ring &R, uint32_t off, const uint4 &x) {
+    __builtin_amdgcn_raw_buffer_store_b128(to_v4(x), R.rs, (int)(R.self + off), 0, CP);
 }
 
 // block t (4 pieces) of this lane's frame into set t & 3
@@ -194,7 +204,7 @@ __device__ __forceinline__ Ring4 ring_get(const Ring &R, uint32_t k, uint32_t h)
 }
 
 // store it (MASK: pieces of block 2k+1 only when that block is in the ring, i.e. 2k+1 < nblk)
-template <bool MASK = false>
+template <bool MASK = false, int CP = 0>
 __device__ __forceinline__ void ring_store(const Ring &R, const Ring4 &x, uint32_t k, uint32_t h, uint32_t nblk = 0) {
     if constexpr (MASK) {
         const uint32_t lane = threadIdx.x & 63;
@@ -202,7 +212,7 @@ __device__ __forceinline__ void ring_store(const Ring &R, const Ring4 &x, uint32
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-        __builtin_amdgcn_raw_buffer_store_b128(x.v[q], R.rs, (int)((h ? R.fo[1][q] : R.fo[0][q]) + 128 * k), 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(x.v[q], R.rs, (int)((h ? R.fo[1][q] : R.fo[0][q]) + 128 * k), 0, CP);
 }
 
 // One step: keystream block t+1 -- with the previous chunk's four Poly1305
@@ -274,10 +284,10 @@ __device__ __forceinline__ void pipe_step(uint4 *pl, const Stream &st, const Mul
         const uint32_t cnt = nb & 3u;
         if constexpr (LINES) { // one lane per packet: pl = frame + 16, dst = frame byte 16 + 64 t
             const uint32_t o = 16 + 64 * t;
-            if (have_prev) frame_store(R, o - 16, prev);
-            frame_store(R, o, x.q0); // cnt >= 1
-            if (cnt > 1) frame_store(R, o + 16, x.q1);
-            if (cnt > 2) frame_store(R, o + 32, x.q2);
+            if (have_prev) frame_store<kTailCp>(R, o - 16, prev);
+            frame_store<kTailCp>(R, o, x.q0); // cnt >= 1
+            if (cnt > 1) frame_store<kTailCp>(R, o + 16, x.q1);
+            if (cnt > 2) frame_store<kTailCp>(R, o + 32, x.q2);
         } else {
             if (have_prev) st16<NT>(dst - 1, prev);
             st16<NT>(dst + 0, x.q0); // cnt >= 1
@@ -338,7 +348,8 @@ __device__ __forceinline__ Acc pipe_pass(uint4 *pl, const Stream &st, const Mul 
             // last line of one block stores its first four pieces only
             wave_sync();
             for (uint32_t m = F >= 2 ? F - 2 : 0; m < 2 * ((F + 1) >> 1); ++m)
-                ring_store<true>(R, ring_get(R, m >> 1, m & 1u), MODE == 8 ? (m >> 1) & 1u : m >> 1, m & 1u, F);
+                ring_store<true, kTailCp>(R, ring_get(R, m >> 1, m & 1u), MODE == 8 ? (m >> 1) & 1u : m >> 1, m & 1u,
+                                          F);
         } else {
             for (; t + 2 < F; t += 3) {
                 pipe_step<OPEN, true, false, MODE, false>(pl, st, r, h, pi, b1, prev, have_prev, t, nb, c0, R);
@@ -361,7 +372,7 @@ __device__ __forceinline__ Acc pipe_pass(uint4 *pl, const Stream &st, const Mul 
         pending = bl;
     }
     if constexpr (LINES) {
-        if (have_prev) frame_store(R, 64 * F, prev); // pl + 4 F - 1
+        if (have_prev) frame_store<kTailCp>(R, 64 * F, prev); // pl + 4 F - 1
     } else if (have_prev && MODE != 1) st16<mode_nt<MODE>()>(pl + 4 * F - 1, prev);
     if constexpr (!OPEN) absorb_chunk(h, pi, r, pending); // the last chunk's blocks
     return h;
@@ -495,7 +506,7 @@ __device__ __forceinline__ void pipe_seal_packet(const SealArgs &a, uint32_t i, 
     uint32_t tag[4];
     pipe_tag(h, r, P, ks + 4, tag);
     const uint4 tagv = make_uint4(tag[0], tag[1], tag[2], tag[3]);
-    if (lines) frame_store(pin_window(R), 16 + P, tagv);
+    if (lines) frame_store<kTailCp>(pin_window(R), 16 + P, tagv);
     else *reinterpret_cast<uint4 *>(frame + 16 + P) = tagv;
     if (a.status) a.status[i] = RG_PKT_OK;
 }

@@ -262,7 +262,9 @@ __global__ __launch_bounds__(512) void tile_kernel(SealArgs sa, OpenArgs oa, Til
     const uint32_t S = halves * gridDim.x;
     const uint32_t my_slot = half == 0 ? blockIdx.x : S - 1 - blockIdx.x;
     const uint32_t rounds = (sc.total_groups + S - 1) / S;
-    const bool dyn = halves == 2 && __ballot(sc.K > 1) == 0; // same in every wave
+    // (empty buckets carry a K of their own class size: only the buckets holding packets count -- round 5
+    // asked every lane, so a planned batch never took the dynamic deal)
+    const bool dyn = halves == 2 && __ballot(sc.cnt > 0 && sc.K > 1) == 0; // same in every wave
     // From eight deal rounds on, the last eighth of them goes to a pool shared by the whole
     // grid: the XCDs do not run at one rate (per-CU finish times at config 4 spread by 8 %, by XCD), so
     // the workgroups that run out of their own tiles first take these, one tile per device-scope atomic

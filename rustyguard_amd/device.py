@@ -31,14 +31,13 @@ class DeviceBatch:
         """Synthetic plaintext (see workloads.py) written on the device."""
         self.engine.synth_fill_dev(self.desc_seal, self.inner_len, self.buf, self.w.data_seed, stream=stream)
 
-    def seal(self, stream=None, with_header: bool = True, status: bool = True, part=None, engine=None):
+    def seal(self, stream=None, with_header: bool = True, part=None, engine=None):
         """Seal packets [a, b) when `part` = (a, b) (all of them by default), on `engine` (default: the
         batch's).  Concurrent calls on different streams need different engines: an engine's planner
-        scratch is stream-ordered."""
+        scratch is stream-ordered (a second stream while the first one's batch is in flight is refused)."""
         a, b = part if part is not None else (0, self.w.n)
         (engine or self.engine).seal_dev(self.keys, self.receivers if with_header else None, self.desc_seal[a:b],
-                                         self.counters[a:b], self.buf, self.status[a:b] if status else None,
-                                         stream=stream)
+                                         self.counters[a:b], self.buf, self.status[a:b], stream=stream)
 
     def open(self, stream=None, counters_out: bool = True, part=None, engine=None):
         a, b = part if part is not None else (0, self.w.n)

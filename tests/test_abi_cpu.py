@@ -79,7 +79,8 @@ def test_product_library_has_no_diagnostics_or_test_hooks():
     test = subprocess.run(["nm", "-D", "--defined-only", b.TEST_LIB], capture_output=True, text=True,
                           check=True).stdout
     hooks = header_functions(TEST_HEADER)
-    assert hooks == ["rg_debug_fail_reserve", "rg_debug_read_arena"]
+    assert hooks == ["rg_debug_fail_reserve", "rg_debug_last_wipe", "rg_debug_lose_completions",
+                     "rg_debug_plan_handoff", "rg_debug_read_arena", "rg_debug_secret_state", "rg_debug_wait_selftest"]
     for h in hooks:
         assert f" T {h}\n" not in prod and f" T {h}\n" in test, h
     assert set(hooks) == set(_lib.TEST_SIGNATURES)
@@ -99,7 +100,7 @@ def test_product_library_refuses_debug_modes(tmp_path):
 
 
 def test_abi_version():
-    assert _lib.lib().rg_abi_version() == 5
+    assert _lib.lib().rg_abi_version() == 6
 
 
 def test_struct_layout_with_gcc(tmp_path):
@@ -176,3 +177,33 @@ def test_product_package_does_not_import_oracle():
             if f.endswith((".py", ".cpp", ".hip", ".h")):
                 text = open(os.path.join(root, f)).read()
                 assert "from oracle" not in text and "import oracle" not in text and "rg_oracle" not in text, f
+
+
+def test_bounded_wait_loop_times_out_without_gpu():
+    """every host wait of the library is the bounded polling loop (wait_bounded); the test
+    library runs that loop against a fake completion (no HIP call).  A completion that never comes ends in
+    RG_EDEVICE after the limit, not a hang; one that comes after k polls returns RG_OK after k + 1 polls."""
+    L = _lib.lib_test()
+    polls, ms = ctypes.c_uint32(), ctypes.c_uint32()
+    rc = L.rg_debug_wait_selftest(60, 0xFFFFFFFF, ctypes.byref(polls), ctypes.byref(ms))
+    assert rc == -2 and b"timed out" in L.rg_last_error()
+    assert 60 <= ms.value < 2000 and polls.value > 10
+    rc = L.rg_debug_wait_selftest(5000, 25, ctypes.byref(polls), ctypes.byref(ms))
+    assert rc == 0 and polls.value == 26 and ms.value < 1000
+
+
+def test_create_refuses_agent_scope_signals():
+    """rg_create refuses ROC_SYSTEM_SCOPE_SIGNAL=0 (round 5: the host pipeline hung under it) before it
+    touches the device, so the refusal shows without a GPU too."""
+    code = textwrap.dedent(f"""
+        import ctypes, sys
+        sys.path.insert(0, {REPO!r})
+        from rustyguard_amd import _lib
+        h = ctypes.c_void_p()
+        rc = _lib.lib().rg_create(0, ctypes.byref(h))
+        print(rc, _lib.lib().rg_last_error().decode())
+    """)
+    env = dict(os.environ, ROC_SYSTEM_SCOPE_SIGNAL="0")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.split()[0] == "-1" and "ROC_SYSTEM_SCOPE_SIGNAL" in r.stdout

@@ -106,3 +106,42 @@ def test_roofline_reports_the_valu_bound():
     # no recorded clock for a workload: no kernel-clock fraction, and nothing claims one
     _, v2 = bench.rooflines("open", 1.0, 1, None, 1.0, ceil, None)
     assert "frac_at_kernel_clock" not in v2 and "clock_assumed" not in v2
+
+
+def test_cpu_baseline_harness_reports_scaling_and_limits():
+    """the CPU baselines run on a persistent pool (threads and OpenSSL contexts kept
+    across rounds) over a >= 64 Ki-packet sample of the workload; each line names its thread count, the
+    limits it came from (affinity, cgroup cpu.max, OMP_NUM_THREADS) and its scaling efficiency
+    (N-thread / (N x 1-thread)).  Run here on a small workload with a short budget."""
+    from rustyguard_amd import workloads
+
+    bench = _bench_module()
+    assert bench.CPU_SAMPLE >= 65536
+    threads, limits = bench.all_core_threads(0)
+    assert threads >= 1 and "affinity" in limits
+    assert bench.all_core_threads(3)[0] == 3
+    w = workloads.uniform(1024, 1500, name="t")
+    port, ossl = bench.cpu_baselines(w, 1.2, (2, {"requested": 2}))
+    for d in (port, ossl):
+        if d is None:
+            continue
+        assert d["cores"] == 2 and d["n_sample"] == 1024 and d["value"] > 0 and d["one_thread"]["value"] > 0
+        sc = d["scaling"]
+        assert sc["threads"] == 2 and 0 < sc["efficiency"] and sc["thread_limits"] == {"requested": 2}
+        assert abs(sc["speedup"] - d["value"] / d["one_thread"]["value"]) < 0.02
+        assert "persistent pool" in d["sample"]
+
+
+def test_cgroup_quota_parser(monkeypatch, tmp_path):
+    bench = _bench_module()
+    real_open = open
+
+    def fake_open(path, *a, **k):
+        if path == "/sys/fs/cgroup/cpu.max":
+            p = tmp_path / "cpu.max"
+            p.write_text("1600000 100000\n")
+            return real_open(p, *a, **k)
+        return real_open(path, *a, **k)
+
+    monkeypatch.setattr("builtins.open", fake_open)
+    assert bench.cgroup_cpu_quota() == 16.0

@@ -6,6 +6,7 @@
   readers only, never for the whole device (round 4 called hipDeviceSynchronize before every wipe, so a
   regrow stalled every stream, the caller's unrelated torch work included).  The reference zeroizes keys on
   drop (rustyguard-crypto/src/prim.rs:227-231)."""
+import ctypes
 import time
 
 import numpy as np
@@ -71,7 +72,7 @@ def test_key_table_regrow_waits_for_no_other_stream():
     s = torch.cuda.Stream()
     dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
     small = _mac_batch(rng, 4)
-    big = _mac_batch(rng, 96)
+    big = _mac_batch(rng, 200)  # 200 x 32 B > the 4 KiB first block: a real regrow
     args = []
     for keys, desc, buf, _, _ in (small, big):
         args.append((dev(keys), dev(desc.view(np.uint8).reshape(-1, 16)), dev(buf),
@@ -86,7 +87,7 @@ def test_key_table_regrow_waits_for_no_other_stream():
     done = torch.cuda.Event()
     done.record(busy)
     t0 = time.perf_counter()
-    eng.mac_verify_dev(args[1][0], 1, args[1][1], args[1][2], args[1][3], args[1][4], stream=s)  # regrow: 4 -> 96 key states
+    eng.mac_verify_dev(args[1][0], 1, args[1][1], args[1][2], args[1][3], args[1][4], stream=s)  # regrow: 4 -> 200 key states
     call_s = time.perf_counter() - t0
     s.synchronize()
     own_s = time.perf_counter() - t0
@@ -119,3 +120,106 @@ def test_host_path_key_table_regrow_matches_oracle(engine):
         oracle.seal_batch(kt, rec, desc, ctr, want)
         st = engine.seal_host(kt, rec, desc, ctr, buf)
         assert (st == 0).all() and np.array_equal(buf, want), nk
+
+
+def _mac_args(eng, batch):
+    keys, desc, buf, want, wkey = batch
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    return (dev(keys), dev(desc.view(np.uint8).reshape(-1, 16)), dev(buf),
+            torch.zeros(len(desc), dtype=torch.uint8, device="cuda"),
+            torch.zeros(len(desc), dtype=torch.int32, device="cuda"))
+
+
+def _mac_ok(args, batch):
+    _, _, _, want, wkey = batch
+    return (list(args[3].cpu().numpy()) == list(want)
+            and list(args[4].cpu().numpy().view(np.uint32)) == list(wkey))
+
+
+def _state(L, eng, which=2):
+    retired, users = ctypes.c_uint32(), ctypes.c_uint32()
+    cap = L.rg_debug_secret_state(eng.handle, which, ctypes.byref(retired), ctypes.byref(users))
+    return cap, retired.value, users.value
+
+
+def _last_wipe(L, nbytes=4096):
+    buf = np.full(nbytes, 0xCC, np.uint8)
+    wipes = ctypes.c_uint64()
+    m = L.rg_debug_last_wipe(buf.ctypes.data_as(ctypes.c_void_p), nbytes, ctypes.byref(wipes))
+    return buf[:m], wipes.value
+
+
+def test_regrow_and_destroy_leave_no_key_bytes():
+    """the old MAC key-state block is zeroed before it is freed -- read back from the device
+    between its wipe and its free (test hook) -- on a regrow and again on rg_destroy."""
+    L = _lib.lib_test()
+    eng = aead.Engine(0, library=L)
+    rng = np.random.default_rng(73)
+    small, big = _mac_batch(rng, 4), _mac_batch(rng, 200)  # 200 x 32 B > the 4 KiB first block: a regrow
+    a = _mac_args(eng, small)
+    eng.mac_verify_dev(*a[:1], 1, *a[1:])
+    torch.cuda.synchronize()
+    _, w0 = _last_wipe(L)
+    b = _mac_args(eng, big)
+    eng.mac_verify_dev(*b[:1], 1, *b[1:])
+    torch.cuda.synchronize()
+    blk, w1 = _last_wipe(L)
+    assert w1 == w0 + 1 and len(blk) == 4096 and not blk.any(), (w0, w1, blk[:16])
+    assert _mac_ok(a, small) and _mac_ok(b, big)
+    eng.close()
+    blk, w2 = _last_wipe(L)
+    assert w2 >= w1 + 1 and len(blk) > 0 and not blk.any()
+
+
+def test_captured_key_states_are_not_freed_under_the_graph():
+    """a MAC verify captured into a graph reads the context's key-state block; a later
+    regrow outside the capture must not free that block under the graph.  The block is retired (kept until
+    rg_destroy), and replaying the graph after the regrow still gives the oracle's verdicts."""
+    L = _lib.lib_test()
+    eng = aead.Engine(0, library=L)
+    rng = np.random.default_rng(74)
+    small, big = _mac_batch(rng, 4), _mac_batch(rng, 200)
+    a = _mac_args(eng, small)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        eng.mac_verify_dev(*a[:1], 1, *a[1:], stream=s)  # warm: the 4 KiB block exists before the capture
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        eng.mac_verify_dev(*a[:1], 1, *a[1:])
+    torch.cuda.synchronize()
+    assert _state(L, eng)[0] == 1  # captured
+    b = _mac_args(eng, big)
+    eng.mac_verify_dev(*b[:1], 1, *b[1:])  # regrow outside the capture
+    torch.cuda.synchronize()
+    cap, retired, _ = _state(L, eng)
+    assert cap == 0 and retired == 1
+    a[3].zero_()
+    a[4].zero_()
+    torch.cuda.synchronize()
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    assert _mac_ok(a, small) and _mac_ok(b, big)
+    _, w0 = _last_wipe(L)
+    del g
+    eng.close()  # the retired block and the current one: both wiped, then freed
+    blk, w1 = _last_wipe(L)
+    assert w1 >= w0 + 2 and not blk.any()
+
+
+def test_key_state_events_do_not_grow_with_streams():
+    """a caller making a fresh stream per call no longer grows the list of stream events that
+    guard the key-state block (completed ones are dropped)."""
+    L = _lib.lib_test()
+    eng = aead.Engine(0, library=L)
+    rng = np.random.default_rng(75)
+    small = _mac_batch(rng, 4, n=64)
+    a = _mac_args(eng, small)
+    for _ in range(24):
+        s = torch.cuda.Stream()
+        eng.mac_verify_dev(*a[:1], 1, *a[1:], stream=s)
+        s.synchronize()
+    assert _state(L, eng)[2] <= 2
+    assert _mac_ok(a, small)
+    eng.close()

@@ -87,7 +87,7 @@ def test_send_batch_dev_two_in_flight_and_reject_after_time(engine):
     # three back-to-back sends on one stream (the third reuses the first's staging)
     for _ in range(3):
         ah.send_batch(half, desc, hb)
-        ad.send_batch_dev(half, dd, db, None, stream=s)
+        ad.send_batch_dev(half, dd, db, torch.zeros(300, dtype=torch.uint8, device="cuda"), stream=s)
     torch.cuda.synchronize()
     assert np.array_equal(db.cpu().numpy(), hb)
     assert ad.send_counter(sa) == ah.send_counter(sa) == 450
