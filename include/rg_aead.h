@@ -259,6 +259,19 @@ int rg_open_batch_host(rg_ctx *ctx, const uint8_t *keys, uint32_t nkeys, const r
 void *rg_host_alloc(size_t bytes);
 void rg_host_free(void *p);
 
+/* NUMA placement (a two-socket host: half the GPUs hang off each socket).  rg_numa_node: the host NUMA
+ * node closest to the context's GPU (-1 unknown).  A group's worker thread for a context runs on the CPUs
+ * of that node this process may use and prefers its memory for the slice buffers it allocates.  Frames
+ * are the caller's: for the full link rate a caller that owns a batch's buffer (a UDP ring, say) places
+ * each context's part -- rg_split_batch's bounds -- on that context's node, by first touch from a thread
+ * there or with rg_numa_bind (mbind MPOL_BIND + MPOL_MF_MOVE over the pages covering [p, p + bytes)), then
+ * pins it with rg_host_register (hipHostRegister; rg_host_unregister before freeing).  Pinned pages do not
+ * move: bind first. */
+int rg_numa_node(rg_ctx *ctx);
+int rg_numa_bind(void *p, size_t bytes, int node);
+int rg_host_register(void *p, size_t bytes);
+int rg_host_unregister(void *p);
+
 /* ------------------------- per-message drop-in for CryptoPrimatives */
 /* Exactly Core::chacha20poly1305_enc / _dec (prim.rs:179-201): any nonce,
  * any AAD, any length, host pointers, blocking.  dec returns RG_OK, or

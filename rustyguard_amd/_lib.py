@@ -89,6 +89,10 @@ SIGNATURES = {
     "rg_sessions_create_group": (c_int, [c_vp, c_u32, ctypes.POINTER(c_vp)]),
     "rg_set_host_slice": (c_int, [c_vp, c_size]),
     "rg_set_wait_timeout": (c_int, [c_vp, c_u32]),
+    "rg_numa_node": (c_int, [c_vp]),
+    "rg_numa_bind": (c_int, [c_vp, c_size, c_int]),
+    "rg_host_register": (c_int, [c_vp, c_size]),
+    "rg_host_unregister": (c_int, [c_vp]),
 }
 
 # include/rg_aead_test.h: exported by the test library (librg_aead_test.so) only

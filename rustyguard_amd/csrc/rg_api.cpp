@@ -4,11 +4,15 @@
 // AntiReplay, rustyguard-crypto/src/prim.rs:376-437,
 // rustyguard-utils/src/anti_replay.rs:1-64, rustyguard-core/src/lib.rs:249-681).
 #include <hip/hip_runtime.h>
+#include <sched.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
+#include <cerrno>
 #include <cstdlib>
 #include <cstring>
 #include <exception>
@@ -420,6 +424,7 @@ struct rg_ctx {
     int last_kernel = -1; // kernel family of the latest batched launch (-1: none yet)
     size_t host_slice = 8ull << 20; // byte span of one host-pipeline slice (rg_set_host_slice; 8 MiB default)
     uint32_t wait_ms = kDefaultWaitMs; // limit of every host wait (rg_set_wait_timeout)
+    int numa_node = -1; // host NUMA node closest to the GPU (hipDeviceAttributeHostNumaId; -1 unknown)
     PlanBuf plan_dev; // planner lists of the device API (calls on one ctx are stream-ordered)
     // the device API's last batch: its stream and an event behind it (not recorded for captured launches);
     // a call on another stream while that event is pending is refused (claim_stream)
@@ -486,9 +491,17 @@ int claim_stream(rg_ctx *ctx, hipStream_t st) {
     return set_err(RG_EDEVICE, "context stream check", q);
 }
 
+// The event is only queried, never used to read what the batch wrote: no system-scope fence (a plain
+// event's release writes back the L2s after the kernel -- +7 us on a config-2 seal timed eagerly,
+// round 6).
 int mark_stream(rg_ctx *ctx, hipStream_t st) {
+#if RG_NO_STREAM_MARK // diagnostic builds only (the A/B of the mark's cost)
+    return RG_OK;
+#endif
     if (capturing(st)) return RG_OK; // a graph is its owner's to order (include/rg_aead.h)
-    if (!ctx->dev_ev) RG_HIP(hipEventCreateWithFlags(&ctx->dev_ev, hipEventDisableTiming), "stream event");
+    if (!ctx->dev_ev)
+        RG_HIP(hipEventCreateWithFlags(&ctx->dev_ev, hipEventDisableTiming | hipEventDisableSystemFence),
+               "stream event");
     RG_HIP(hipEventRecord(ctx->dev_ev, st), "stream event");
     ctx->dev_stream = st;
     ctx->dev_busy = true;
@@ -528,6 +541,8 @@ int rg_create(int device, rg_ctx **out) {
     c->h_general.secret = true;
     {
         hipError_t e = hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device);
+        if (e == hipSuccess && hipDeviceGetAttribute(&c->numa_node, hipDeviceAttributeHostNumaId, device) != hipSuccess)
+            c->numa_node = -1;
         if (e == hipSuccess) e = rg::prepare_tile_kernels();
         if (e == hipSuccess) e = rg::prepare_pipe_kernels(c->pipe_max_wg);
         if (e == hipSuccess) e = rg::prepare_flat_kernels();
@@ -1003,6 +1018,42 @@ void rg_host_free(void *p) {
     if (p) (void)hipHostFree(p);
 }
 
+int rg_numa_node(rg_ctx *ctx) {
+    if (!ctx) return set_err(RG_EINVAL, "null context");
+    return ctx->numa_node;
+}
+
+int rg_numa_bind(void *p, size_t bytes, int node) {
+    if (!p || !bytes || node < 0 || node >= 1024) return set_err(RG_EINVAL, "numa_bind: bad args");
+#ifdef SYS_mbind
+    const uintptr_t pg = (uintptr_t)sysconf(_SC_PAGESIZE);
+    const uintptr_t a = (uintptr_t)p & ~(pg - 1), b = ((uintptr_t)p + bytes + pg - 1) & ~(pg - 1);
+    unsigned long mask[16] = {0};
+    mask[node / 64] = 1ul << (node % 64);
+    // MPOL_BIND, MPOL_MF_MOVE: pages already touched move to the node (pinned pages cannot: bind first)
+    if (syscall(SYS_mbind, a, b - a, 2 /* MPOL_BIND */, mask, 1024ul, 2u /* MPOL_MF_MOVE */) != 0) {
+        char what[96];
+        snprintf(what, sizeof what, "numa_bind: mbind to node %d failed (errno %d)", node, errno);
+        return set_err(RG_EINVAL, what);
+    }
+    return RG_OK;
+#else
+    return set_err(RG_EINVAL, "numa_bind: no mbind on this platform");
+#endif
+}
+
+int rg_host_register(void *p, size_t bytes) {
+    if (!p || !bytes) return set_err(RG_EINVAL, "host_register: bad args");
+    RG_HIP(hipHostRegister(p, bytes, hipHostRegisterDefault), "hipHostRegister");
+    return RG_OK;
+}
+
+int rg_host_unregister(void *p) {
+    if (!p) return set_err(RG_EINVAL, "host_unregister: null");
+    RG_HIP(hipHostUnregister(p), "hipHostUnregister");
+    return RG_OK;
+}
+
 } // extern "C"
 
 // ------------------------------------------------------------ host pipeline
@@ -1230,6 +1281,54 @@ int run_host(HostRun *runs, size_t nruns) {
 // own device. The caller's thread starts the workers and joins them. If a thread cannot be started, the
 // caller's thread runs the remaining runs itself. The first failing run's error becomes the call's
 // (rg_last_error is per thread).
+// NUMA placement of a group's worker thread: on a two-socket host half the GPUs hang
+// off the other socket, and a worker that drives a GPU from there crosses the socket link for every API
+// call and for the slot buffers it touches.  The worker is pinned to the CPUs of its GPU's node that this
+// process may use (none allowed there: left as it is), and its memory policy prefers that node, so the
+// slice buffers it allocates and first-touches land there.  The caller's frames are the caller's: see
+// rg_numa_bind / rg_host_register (include/rg_aead.h).
+bool node_cpus(int node, cpu_set_t *out) {
+    char path[96];
+    snprintf(path, sizeof path, "/sys/devices/system/node/node%d/cpulist", node);
+    FILE *f = fopen(path, "r");
+    if (!f) return false;
+    char line[4096];
+    const bool got = fgets(line, sizeof line, f) != nullptr;
+    fclose(f);
+    if (!got) return false;
+    CPU_ZERO(out);
+    for (char *p = line; *p && *p != '\n';) { // "0-15,128-143"
+        char *end = nullptr;
+        const long a = strtol(p, &end, 10);
+        if (end == p) break;
+        long b = a;
+        if (*end == '-') {
+            p = end + 1;
+            b = strtol(p, &end, 10);
+        }
+        for (long c = a; c <= b && c < CPU_SETSIZE; ++c) CPU_SET((int)c, out);
+        p = *end == ',' ? end + 1 : end;
+    }
+    return true;
+}
+
+int place_thread(int node) {
+    if (node < 0) return -1;
+    cpu_set_t want, allowed;
+    if (!node_cpus(node, &want) || sched_getaffinity(0, sizeof allowed, &allowed) != 0) return -1;
+    CPU_AND(&want, &want, &allowed);
+    if (CPU_COUNT(&want) == 0) return -1; // none of the node's CPUs is ours
+    if (sched_setaffinity(0, sizeof want, &want) != 0) return -1;
+#ifdef SYS_set_mempolicy
+    unsigned long mask[16] = {0};
+    if (node < 1024) {
+        mask[node / 64] = 1ul << (node % 64);
+        (void)syscall(SYS_set_mempolicy, 1 /* MPOL_PREFERRED */, mask, 1024ul);
+    }
+#endif
+    return CPU_COUNT(&want);
+}
+
 #ifndef RG_GROUP_THREADS
 #define RG_GROUP_THREADS 1
 #endif
@@ -1262,6 +1361,7 @@ int run_host_group(std::vector<HostRun> &runs) {
     try {
         for (; started < n; ++started)
             workers.emplace_back([&runs, &rcs, &errs, started]() {
+                place_thread(runs[started].ctx->numa_node); // the CPUs (and memory) next to this GPU
                 rcs[started] = run_host(&runs[started], 1);
                 if (rcs[started] != RG_OK) errs[started].swap(g_err); // the worker's own message, moved out
             });

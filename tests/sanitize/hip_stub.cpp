@@ -1,0 +1,334 @@
+// hip_stub.cpp -- TEST INFRASTRUCTURE ONLY (tests/test_sanitize_cpu.py): a CPU stand-in for the parts of
+// the HIP runtime and of the kernel launchers that rg_api.cpp calls, so that the library's host logic --
+// the slice pipeline and its ordering, the group's worker threads, the splitter, the session layer's
+// anti-replay pass and side effects, the key-table wiping, the bounded waits -- can run under
+// AddressSanitizer / UndefinedBehaviorSanitizer and ThreadSanitizer on a machine without a GPU
+// (VERDICT r5 item 8).  Never linked into a shipped library.
+//
+// "Device" memory is host memory, streams run every operation at once on the calling thread, events
+// are always complete.  The kernels are emulated with the real kernels' descriptor checks and status
+// rules (rg_pipe.hip pipe_seal_packet / pipe_open_packet) around a FAKE cipher: a keystream and a
+// 16-byte tag from a 64-bit mixer over (key, counter, position).  It is not ChaCha20-Poly1305 and proves
+// nothing about the arithmetic -- the GPU parity tests do that against the oracle -- but a seal followed
+// by an open restores the plaintext, a changed byte fails the tag, and every status path is the
+// product's.
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+
+#include "../../rustyguard_amd/csrc/rg_internal.h"
+
+struct ihipStream_t {
+    int dummy;
+};
+struct ihipEvent_t {
+    int dummy;
+};
+
+namespace {
+thread_local int g_dev = 0;
+int ndev() {
+    const char *v = getenv("RG_STUB_DEVICES");
+    return v ? atoi(v) : 2;
+}
+} // namespace
+
+extern "C" {
+hipError_t hipGetDeviceCount(int *n) {
+    *n = ndev();
+    return hipSuccess;
+}
+hipError_t hipSetDevice(int d) {
+    if (d < 0 || d >= ndev()) return hipErrorInvalidDevice;
+    g_dev = d;
+    return hipSuccess;
+}
+hipError_t hipGetDevice(int *d) {
+    *d = g_dev;
+    return hipSuccess;
+}
+hipError_t hipDeviceGetAttribute(int *pi, hipDeviceAttribute_t attr, int) {
+    *pi = attr == hipDeviceAttributeMultiprocessorCount ? 4 : 0;
+    return hipSuccess;
+}
+const char *hipGetErrorString(hipError_t e) { return e == hipSuccess ? "hipSuccess" : "stub error"; }
+hipError_t hipDeviceSynchronize(void) { return hipSuccess; }
+hipError_t hipMalloc(void **p, size_t n) {
+    *p = malloc(n ? n : 1);
+    return *p ? hipSuccess : hipErrorOutOfMemory;
+}
+hipError_t hipMallocAsync(void **p, size_t n, hipStream_t) { return hipMalloc(p, n); }
+hipError_t hipFree(void *p) {
+    free(p);
+    return hipSuccess;
+}
+hipError_t hipFreeAsync(void *p, hipStream_t) { return hipFree(p); }
+hipError_t hipHostMalloc(void **p, size_t n, unsigned int) { return hipMalloc(p, n); }
+hipError_t hipHostFree(void *p) { return hipFree(p); }
+hipError_t hipHostRegister(void *, size_t, unsigned int) { return hipSuccess; }
+hipError_t hipHostUnregister(void *) { return hipSuccess; }
+hipError_t hipHostGetDevicePointer(void **d, void *h, unsigned int) {
+    *d = h;
+    return hipSuccess;
+}
+hipError_t hipMemcpy(void *d, const void *s, size_t n, hipMemcpyKind) {
+    memmove(d, s, n);
+    return hipSuccess;
+}
+hipError_t hipMemcpyAsync(void *d, const void *s, size_t n, hipMemcpyKind k, hipStream_t) {
+    return hipMemcpy(d, s, n, k);
+}
+hipError_t hipMemset(void *d, int v, size_t n) {
+    memset(d, v, n);
+    return hipSuccess;
+}
+hipError_t hipMemsetAsync(void *d, int v, size_t n, hipStream_t) { return hipMemset(d, v, n); }
+hipError_t hipStreamCreateWithFlags(hipStream_t *s, unsigned int) {
+    *s = new ihipStream_t{0};
+    return hipSuccess;
+}
+hipError_t hipStreamDestroy(hipStream_t s) {
+    delete s;
+    return hipSuccess;
+}
+hipError_t hipStreamSynchronize(hipStream_t) { return hipSuccess; }
+hipError_t hipStreamWaitEvent(hipStream_t, hipEvent_t, unsigned int) { return hipSuccess; }
+hipError_t hipStreamIsCapturing(hipStream_t, hipStreamCaptureStatus *c) {
+    *c = hipStreamCaptureStatusNone;
+    return hipSuccess;
+}
+hipError_t hipEventCreateWithFlags(hipEvent_t *e, unsigned) {
+    *e = new ihipEvent_t{0};
+    return hipSuccess;
+}
+hipError_t hipEventDestroy(hipEvent_t e) {
+    delete e;
+    return hipSuccess;
+}
+hipError_t hipEventRecord(hipEvent_t, hipStream_t) { return hipSuccess; }
+hipError_t hipEventQuery(hipEvent_t) { return hipSuccess; }
+} // extern "C"
+
+// ------------------------------------------------------------------ fake cipher and kernels
+namespace {
+uint64_t mix(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+uint64_t key_word(const uint32_t *keys, uint32_t k) {
+    uint64_t h = 0;
+    for (int w = 0; w < 8; ++w) h = mix(h ^ keys[8 * (size_t)k + w]);
+    return h;
+}
+void xor_stream(uint8_t *p, uint32_t P, uint64_t kw, uint64_t ctr) {
+    for (uint32_t j = 0; j < P; ++j) p[j] ^= (uint8_t)(mix(kw ^ mix(ctr) ^ (j >> 3)) >> (8 * (j & 7)));
+}
+void fake_tag(const uint8_t *ct, uint32_t P, uint64_t kw, uint64_t ctr, uint8_t tag[16]) {
+    uint64_t a = mix(kw ^ ctr), b = mix(a ^ P);
+    for (uint32_t j = 0; j < P; ++j) {
+        a = mix(a ^ ct[j]);
+        b = mix(b + a);
+    }
+    memcpy(tag, &a, 8);
+    memcpy(tag + 8, &b, 8);
+}
+uint64_t get64(const uint8_t *p) {
+    uint64_t v;
+    memcpy(&v, p, 8);
+    return v;
+}
+
+void seal_all(const rg::SealArgs &a) {
+    for (uint32_t i = 0; i < a.n; ++i) {
+        const rg_pkt_desc d = a.desc[i];
+        const uint32_t P = d.len;
+        const bool valid = d.key_idx < a.nkeys && (P & 15u) == 0 && (d.offset & 15u) == 0 && P <= rg::kMaxPayload &&
+                           d.offset <= a.buf_len && P + 32 <= a.buf_len - d.offset;
+        if (!valid) {
+            a.status[i] = d.key_idx == RG_KEY_SKIP ? RG_PKT_REJECTED : RG_PKT_INVALID;
+            continue;
+        }
+        uint8_t *f = a.buf + d.offset;
+        const uint64_t ctr = a.counters[i], kw = key_word(a.keys, d.key_idx);
+        xor_stream(f + 16, P, kw, ctr);
+        fake_tag(f + 16, P, kw, ctr, f + 16 + P);
+        if (a.receivers) {
+            const uint32_t h[2] = {4u, a.receivers[d.key_idx]};
+            memcpy(f, h, 8);
+            memcpy(f + 8, &ctr, 8);
+        }
+        a.status[i] = RG_PKT_OK;
+    }
+}
+
+void open_all(const rg::OpenArgs &a) {
+    for (uint32_t i = 0; i < a.n; ++i) {
+        const rg_pkt_desc d = a.desc[i];
+        const uint32_t W = d.len;
+        uint32_t st = 0xFF;
+        uint64_t ctr = 0;
+        if (d.key_idx == RG_KEY_SKIP) st = RG_PKT_REJECTED;
+        else if ((d.offset & 15u) != 0) st = RG_PKT_UNALIGNED;
+        else if (d.key_idx >= a.nkeys || W > rg::kMaxPayload + 32 || d.offset > a.buf_len || W > a.buf_len - d.offset ||
+                 W < 4)
+            st = RG_PKT_INVALID;
+        uint8_t *f = a.buf + d.offset;
+        if (st == 0xFF) {
+            uint32_t type;
+            memcpy(&type, f, 4);
+            if (type != 4u) st = type - 1u < 3u ? RG_PKT_NOT_DATA : RG_PKT_INVALID;
+            else if ((W & 15u) != 0 || W < 16) st = RG_PKT_INVALID;
+            else {
+                ctr = get64(f + 8);
+                if (W < 32) st = RG_PKT_DECRYPT_ERR;
+            }
+        }
+        if (st == 0xFF) {
+            const uint32_t P = W - 32;
+            const uint64_t kw = key_word(a.keys, d.key_idx);
+            uint8_t want[16];
+            fake_tag(f + 16, P, kw, ctr, want);
+            uint8_t diff = 0;
+            for (int b = 0; b < 16; ++b) diff |= want[b] ^ f[16 + P + b];
+            if (diff == 0) xor_stream(f + 16, P, kw, ctr);
+            st = diff == 0 ? RG_PKT_OK : RG_PKT_DECRYPT_ERR;
+        }
+        a.status[i] = (uint8_t)st;
+        if (a.counters_out) a.counters_out[i] = ctr;
+    }
+}
+
+// the launch path taken (a planned launch runs the preset first), for the driver's checks
+std::atomic<uint64_t> g_launches{0};
+} // namespace
+
+extern "C" uint64_t rg_stub_launches(void) { return g_launches.load(); }
+
+namespace rg {
+hipError_t prepare_tile_kernels() { return hipSuccess; }
+hipError_t prepare_flat_kernels() { return hipSuccess; }
+hipError_t prepare_pipe_kernels(int max_wg[2]) {
+    max_wg[0] = max_wg[1] = 1;
+    return hipSuccess;
+}
+uint32_t flat_junk_bytes(int cus) { return (uint32_t)(cus > 0 ? cus : 1) * 4096u; }
+
+hipError_t launch_preset(uint8_t *status, uint32_t n, uint32_t *ctl, uint32_t done_init, uint32_t pool_init,
+                         hipStream_t) {
+    if (ctl)
+        for (uint32_t w = 0; w < kCtlWords; ++w)
+            ctl[w] = w == kCtlCounts + kClasses ? done_init : w == kCtlPool ? pool_init : 0u;
+    if (status) memset(status, RG_PKT_PENDING, n);
+    return hipSuccess;
+}
+hipError_t launch_plan(const rg_pkt_desc *, uint32_t, bool, const TilePlan &tp, hipStream_t) {
+    // the emulated transport kernels take packets in array order; a planner whose hand-off is lost (the
+    // test library's hook starts the finished count stale) leaves the pipelined kernel nothing to do
+    if (tp.sched) tp.sched[2] = tp.counts[kClasses] == 0 ? 1u : 0u;
+    return hipSuccess;
+}
+static hipError_t run(const SealArgs *sa, const OpenArgs *oa) {
+    ++g_launches;
+    if (sa) seal_all(*sa);
+    else open_all(*oa);
+    return hipSuccess;
+}
+hipError_t launch_pipe(const SealArgs *sa, const OpenArgs *oa, const Launch &, const PipePlan *plan, hipStream_t) {
+    if (plan && plan->sched[2] == 0) return hipSuccess; // no schedule: nothing runs (statuses stay pending)
+    return run(sa, oa);
+}
+hipError_t launch_tiles(const SealArgs *sa, const OpenArgs *oa, int, const TilePlan &tp, const Launch &, hipStream_t) {
+    if (tp.gq && tp.gq[0] != 0) return hipSuccess; // stale pool (test hook): emulated as nothing taken
+    return run(sa, oa);
+}
+hipError_t launch_flat(const SealArgs *sa, const OpenArgs *oa, bool, uint4 *, int, hipStream_t) { return run(sa, oa); }
+
+hipError_t launch_general(GeneralJob *jobs, uint32_t njobs, uint8_t *arena, hipStream_t) {
+    for (uint32_t i = 0; i < njobs; ++i) {
+        GeneralJob &j = jobs[i];
+        uint64_t kw = 0;
+        for (int w = 0; w < 8; ++w) kw = mix(kw ^ j.key[w]);
+        kw = mix(kw ^ j.nonce[0] ^ ((uint64_t)j.nonce[1] << 32)) ^ j.nonce[2];
+        uint8_t *pl = arena + j.payload_off, *tg = arena + j.tag_off;
+        const uint32_t P = (uint32_t)j.payload_len;
+        uint64_t aad = 0;
+        for (uint64_t b = 0; b < j.aad_len; ++b) aad = mix(aad ^ arena[j.aad_off + b]);
+        if (!j.decrypt) {
+            xor_stream(pl, P, kw, aad);
+            fake_tag(pl, P, kw, aad, tg);
+            j.status = RG_PKT_OK;
+        } else {
+            uint8_t want[16], diff = 0;
+            fake_tag(pl, P, kw, aad, want);
+            for (int b = 0; b < 16; ++b) diff |= want[b] ^ tg[b];
+            if (!diff) xor_stream(pl, P, kw, aad);
+            j.status = diff ? RG_PKT_DECRYPT_ERR : RG_PKT_OK;
+        }
+    }
+    return hipSuccess;
+}
+
+hipError_t launch_rx_resolve(const rg_pkt_desc *desc, uint32_t n, const uint8_t *buf, uint64_t buf_len,
+                             const rg_rx_entry *table, uint32_t cap, rg_pkt_desc *out, uint32_t *key_out, hipStream_t) {
+    for (uint32_t i = 0; i < n; ++i) {
+        rg_pkt_desc d = desc[i];
+        const uint64_t W = d.len;
+        uint32_t k = 0, found = RG_KEY_SKIP;
+        if ((d.offset & 15u) == 0 && d.offset <= buf_len && W <= buf_len - d.offset && W >= 16 && (W & 15u) == 0) {
+            uint32_t hdr[2];
+            memcpy(hdr, buf + d.offset, 8);
+            if (hdr[0] == 4u) {
+                uint32_t s = rx_slot(hdr[1], cap);
+                for (uint32_t probe = 0; probe < cap; ++probe) {
+                    if (table[s].key_idx == RG_KEY_SKIP) break;
+                    if (table[s].receiver == hdr[1]) {
+                        found = table[s].key_idx;
+                        break;
+                    }
+                    s = (s + 1) & (cap - 1);
+                }
+                k = found;
+            }
+        }
+        d.key_idx = k;
+        out[i] = d;
+        if (key_out) key_out[i] = found;
+    }
+    return hipSuccess;
+}
+hipError_t launch_bind_keys(const rg_pkt_desc *in, const uint32_t *key_idx, uint32_t n, rg_pkt_desc *out, hipStream_t) {
+    for (uint32_t i = 0; i < n; ++i) {
+        out[i] = in[i];
+        out[i].key_idx = key_idx[i];
+    }
+    return hipSuccess;
+}
+hipError_t launch_undo_gather(const rg_pkt_desc *rd, const uint64_t *ctr, const uint32_t *idx, uint32_t m,
+                              rg_pkt_desc *out, uint64_t *ctr_out, hipStream_t) {
+    for (uint32_t j = 0; j < m; ++j) {
+        out[j] = rd[idx[j]];
+        out[j].len -= 32;
+        ctr_out[j] = ctr[idx[j]];
+    }
+    return hipSuccess;
+}
+hipError_t launch_synth_fill(const rg_pkt_desc *desc, const uint32_t *inner_len, uint32_t n, uint8_t *buf,
+                             uint64_t buf_len, uint64_t seed, hipStream_t) {
+    for (uint32_t i = 0; i < n; ++i) {
+        const rg_pkt_desc d = desc[i];
+        if (d.offset > buf_len || 16 + (uint64_t)d.len > buf_len - d.offset) continue;
+        for (uint32_t b = 0; b < d.len; ++b)
+            buf[d.offset + 16 + b] = b < inner_len[i] ? (uint8_t)mix(seed + ((uint64_t)i << 16) + b) : 0;
+    }
+    return hipSuccess;
+}
+hipError_t launch_mac_verify(const MacArgs &a, hipStream_t) {
+    for (uint32_t i = 0; i < a.n; ++i) a.status[i] = RG_PKT_REJECTED; // not exercised by the driver
+    return hipSuccess;
+}
+} // namespace rg
