@@ -657,24 +657,30 @@ def e2e_multi_run(devices, reps: int = 3, verify: bool = True):
     """Packets that start and end in pinned host memory (the reference's UDP buffers,
     rustyguard-tun/src/main.rs:41-57), driven over several GPUs from ONE calling thread (the reference's
     single event loop, rustyguard-core/src/lib.rs:349-352): rg_seal_batch_host_multi then
-    rg_open_batch_host_multi on config 5's whole batch (8 Mi x 1500 B, 12.9 GB of frames) in one
-    hipHostMalloc buffer, split by equal work over the group's contexts (one per entry of `devices`), each
+    rg_open_batch_host_multi on config 5's whole batch (8 Mi x 1500 B, 12.9 GB of frames) in one host
+    buffer whose parts sit on their contexts' NUMA nodes, pinned (aead.placed_host_buffer; the line's
+    `placement`), split by equal work over the group's contexts (one per entry of `devices`), each
     running its own three-stream H2D -> kernel -> D2H slice pipeline from a worker thread of the library
     (round 5; no context waits on another's GPU).  Beside it the same batch through one context (device
     devices[0]) -- the e2e speed-up of the group.  Median of `reps` timed passes after one warm pass;
     every open must verify, and sampled payloads must come back to what they were before the first seal."""
     from rustyguard_amd import workloads
-    from rustyguard_amd.aead import Group, host_alloc
+    from rustyguard_amd.aead import Group, placed_host_buffer
 
     w = workloads.build("cfg5", 0, 1)
-    buf = host_alloc(w.buf_bytes)
+    # the frames placed per part on each context's NUMA node and pinned (round 6, VERDICT r5 item 5)
+    g0 = Group(list(devices))
+    try:
+        buf, placement = placed_host_buffer(g0, w.desc, w.buf_bytes)
+    finally:
+        g0.close()
     od = w.open_desc()
     rng = np.random.default_rng(11)
     pick = np.unique(np.concatenate([[0, w.n - 1], rng.choice(w.n, 256, replace=False)]))
     before = {int(k): buf[int(w.desc["offset"][k]) + 16:int(w.desc["offset"][k]) + 16 + int(w.desc["len"][k])].copy()
               for k in pick}
     out = {"workload": f"cfg5 whole batch ({w.n} packets, {w.buf_bytes / 1e9:.1f} GB of frames) in pinned host memory",
-           "reps": reps}
+           "reps": reps, "placement": placement}
     runs = [("group", list(devices))] + ([("one_context", [devices[0]])] if len(devices) > 1 else [])
     for name, devs in runs:
         g = Group(devs)

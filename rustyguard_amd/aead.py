@@ -619,6 +619,48 @@ def rx_find(table: np.ndarray, receiver: int) -> int:
     return int(lib().rg_rx_table_find(_vp(table), table.shape[0], receiver))
 
 
+def numa_node(engine) -> int:
+    """rg_numa_node: the host NUMA node closest to the engine's (or group context's) GPU, -1 if unknown."""
+    return int(engine.library.rg_numa_node(engine.handle))
+
+
+def placed_host_buffer(group: "Group", desc: np.ndarray, nbytes: int, open_: bool = False):
+    """A frame buffer for a host batch over `group`, placed for it (include/rg_aead.h, NUMA placement): an
+    anonymous mapping whose part k -- the frames of rg_split_batch's part k -- is bound to context k's NUMA
+    node (rg_numa_bind) and first-touched there, then the whole buffer pinned (rg_host_register).  Returns
+    (uint8 array, placement list).  The pin is dropped when the array's buffer is collected."""
+    import mmap
+    import weakref
+
+    L = group.library
+    n = len(desc)
+    mm = mmap.mmap(-1, max(nbytes, 1), flags=mmap.MAP_PRIVATE | mmap.MAP_ANONYMOUS)
+    arr = np.frombuffer(mm, np.uint8)
+    p = arr.ctypes.data
+    bounds = split_batch(desc, len(group), open_) if n else np.zeros(len(group) + 1, np.int64)
+    placement = []
+    for k in range(len(group)):
+        lo, hi = int(bounds[k]), int(bounds[k + 1])
+        node = numa_node(group.engine(k))
+        part = {"context": k, "device": group.devices[k], "numa_node": node, "packets": hi - lo, "bound": False}
+        if hi > lo:
+            a = int(desc["offset"][lo])
+            last = int(np.argmax(desc["offset"][lo:hi])) + lo
+            b = min(nbytes, int(desc["offset"][last]) + int(desc["len"][last]) + (0 if open_ else 32))
+            part["bytes"] = b - a
+            if node >= 0 and b > a:
+                part["bound"] = L.rg_numa_bind(ctypes.c_void_p(p + a), b - a, node) == 0
+        placement.append(part)
+    arr[:] = 0  # first touch: each part's pages on its node
+    check(L.rg_host_register(ctypes.c_void_p(p), arr.nbytes), "rg_host_register", L)
+
+    def _release(lib=L, ptr=p, m=mm):
+        lib.rg_host_unregister(ctypes.c_void_p(ptr))
+
+    weakref.finalize(arr, _release)
+    return arr, placement
+
+
 def host_alloc(nbytes: int) -> np.ndarray:
     """Pinned host buffer (hipHostMalloc) viewed as uint8; freed with the array's owner."""
     p = lib().rg_host_alloc(nbytes)

@@ -491,21 +491,27 @@ int claim_stream(rg_ctx *ctx, hipStream_t st) {
     return set_err(RG_EDEVICE, "context stream check", q);
 }
 
-// The event is only queried, never used to read what the batch wrote: no system-scope fence (a plain
-// event's release writes back the L2s after the kernel -- +7 us on a config-2 seal timed eagerly,
-// round 6).
-int mark_stream(rg_ctx *ctx, hipStream_t st) {
+// The event that marks a device batch's end: recorded by the transport kernel's own dispatch (RG_LAUNCH,
+// no separate queue packet), or nullptr inside a stream capture (a graph is its owner's to order,
+// include/rg_aead.h).  It is only queried, never used to read what the batch wrote: no system-scope fence
+// (with one, the release wrote the L2s back after the kernel: +7 us on an eager config-2 seal; a separate
+// fence-free hipEventRecord still cost +3 us, round 6).
+hipEvent_t stream_event(rg_ctx *ctx, hipStream_t st) {
 #if RG_NO_STREAM_MARK // diagnostic builds only (the A/B of the mark's cost)
-    return RG_OK;
+    return nullptr;
 #endif
-    if (capturing(st)) return RG_OK; // a graph is its owner's to order (include/rg_aead.h)
-    if (!ctx->dev_ev)
-        RG_HIP(hipEventCreateWithFlags(&ctx->dev_ev, hipEventDisableTiming | hipEventDisableSystemFence),
-               "stream event");
-    RG_HIP(hipEventRecord(ctx->dev_ev, st), "stream event");
+    if (capturing(st)) return nullptr;
+    if (!ctx->dev_ev &&
+        hipEventCreateWithFlags(&ctx->dev_ev, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess)
+        ctx->dev_ev = nullptr;
+    return ctx->dev_ev;
+}
+
+// after a launch that recorded ev (stream_event)
+void mark_stream(rg_ctx *ctx, hipStream_t st, hipEvent_t ev) {
+    if (!ev) return;
     ctx->dev_stream = st;
     ctx->dev_busy = true;
-    return RG_OK;
 }
 
 } // namespace
@@ -719,6 +725,7 @@ int rg_last_kernel(rg_ctx *ctx) {
 
 static rg::Launch launch_cfg(rg_ctx *ctx, size_t n, bool open) {
     rg::Launch L;
+    L.done = nullptr;
     L.lanes = rg_get_lanes_per_packet(ctx, n);
     L.cus = ctx->cus;
     L.staged_g = rg_get_kernel(ctx, n);
@@ -819,10 +826,11 @@ static hipError_t launch_pipe_any(rg_ctx *ctx, const rg::SealArgs *sa, const rg:
 
 // Flattened chunk-stream kernel: units of equal work (planner on / auto) or of
 // equal packet counts (planner off); the balancing runs inside the kernel.
-static hipError_t launch_flat_any(rg_ctx *ctx, const rg::SealArgs *sa, const rg::OpenArgs *oa, hipStream_t st) {
+static hipError_t launch_flat_any(rg_ctx *ctx, const rg::SealArgs *sa, const rg::OpenArgs *oa, hipStream_t st,
+                                  hipEvent_t done) {
     hipError_t e = ctx->d_junk.reserve(rg::flat_junk_bytes(ctx->cus));
     if (e != hipSuccess) return e;
-    return rg::launch_flat(sa, oa, ctx->plan != 0, static_cast<uint4 *>(ctx->d_junk.p), ctx->cus, st);
+    return rg::launch_flat(sa, oa, ctx->plan != 0, static_cast<uint4 *>(ctx->d_junk.p), ctx->cus, st, done);
 }
 
 // Automatic choice between the two small-batch kernels: when the last planned batch of this planner
@@ -843,25 +851,30 @@ static int pick_family(rg_ctx *ctx, int g, PlanBuf &pb, hipStream_t st) {
     return g;
 }
 
-static hipError_t launch_seal_any(rg_ctx *ctx, const rg::SealArgs &a0, PlanBuf &pb, hipStream_t st) {
+// done: the event the transport kernel's dispatch records as it completes (nullptr: none)
+static hipError_t launch_seal_any(rg_ctx *ctx, const rg::SealArgs &a0, PlanBuf &pb, hipStream_t st,
+                                  hipEvent_t done = nullptr) {
     rg::SealArgs a = a0;
     rg::Launch L = launch_cfg(ctx, a.n, false);
+    L.done = done;
     L.staged_g = pick_family(ctx, L.staged_g, pb, st);
     ctx->last_kernel = L.staged_g;
     // stamps (diagnostic builds): debug mode 3, or any diagnostic mode of the pipelined kernel
     a.dbg = L.debug_mode == 3 || (L.staged_g == 0 && L.debug_mode != 0) ? ctx->dbg : nullptr;
-    if (L.staged_g == 3) return launch_flat_any(ctx, &a, nullptr, st);
+    if (L.staged_g == 3) return launch_flat_any(ctx, &a, nullptr, st, done);
     if (L.staged_g == 0) return launch_pipe_any(ctx, &a, nullptr, pb, L, st);
     return launch_tiles_any(ctx, &a, nullptr, pb, L, st);
 }
 
-static hipError_t launch_open_any(rg_ctx *ctx, const rg::OpenArgs &a0, PlanBuf &pb, hipStream_t st) {
+static hipError_t launch_open_any(rg_ctx *ctx, const rg::OpenArgs &a0, PlanBuf &pb, hipStream_t st,
+                                  hipEvent_t done = nullptr) {
     rg::OpenArgs a = a0;
     rg::Launch L = launch_cfg(ctx, a.n, true);
+    L.done = done;
     L.staged_g = pick_family(ctx, L.staged_g, pb, st);
     ctx->last_kernel = L.staged_g;
     a.dbg = L.debug_mode == 3 ? ctx->dbg : nullptr;
-    if (L.staged_g == 3) return launch_flat_any(ctx, nullptr, &a, st);
+    if (L.staged_g == 3) return launch_flat_any(ctx, nullptr, &a, st, done);
     if (L.staged_g == 0) return launch_pipe_any(ctx, nullptr, &a, pb, L, st);
     return launch_tiles_any(ctx, nullptr, &a, pb, L, st);
 }
@@ -889,8 +902,10 @@ int rg_seal_batch_dev(rg_ctx *ctx, const uint8_t *keys, const uint32_t *receiver
     a.status = status;
     a.nkeys = nkeys;
     a.n = (uint32_t)n;
-    RG_HIP(launch_seal_any(ctx, a, ctx->plan_dev, st), "seal launch");
-    return mark_stream(ctx, st);
+    hipEvent_t ev = stream_event(ctx, st);
+    RG_HIP(launch_seal_any(ctx, a, ctx->plan_dev, st, ev), "seal launch");
+    mark_stream(ctx, st, ev);
+    return RG_OK;
 }
 
 int rg_open_batch_dev(rg_ctx *ctx, const uint8_t *keys, uint32_t nkeys, const rg_pkt_desc *desc, size_t n,
@@ -913,8 +928,10 @@ int rg_open_batch_dev(rg_ctx *ctx, const uint8_t *keys, uint32_t nkeys, const rg
     a.counters_out = counters_out;
     a.nkeys = nkeys;
     a.n = (uint32_t)n;
-    RG_HIP(launch_open_any(ctx, a, ctx->plan_dev, st), "open launch");
-    return mark_stream(ctx, st);
+    hipEvent_t ev = stream_event(ctx, st);
+    RG_HIP(launch_open_any(ctx, a, ctx->plan_dev, st, ev), "open launch");
+    mark_stream(ctx, st, ev);
+    return RG_OK;
 }
 
 int rg_synth_fill_dev(rg_ctx *ctx, const rg_pkt_desc *desc, const uint32_t *inner_len, size_t n, uint8_t *buf,

@@ -1120,7 +1120,8 @@ static uint32_t flat_coop_ok(uint32_t n, uint32_t units, bool balance) {
     return kgc % 4 == 0 && kgc >= 4 ? (uint32_t)kgc : 0u;
 }
 
-hipError_t launch_flat(const SealArgs *sa, const OpenArgs *oa, bool balance, uint4 *junk, int cus, hipStream_t s) {
+hipError_t launch_flat(const SealArgs *sa, const OpenArgs *oa, bool balance, uint4 *junk, int cus, hipStream_t s,
+                       hipEvent_t done) {
     const uint32_t n = sa ? sa->n : oa->n;
     if (n == 0) return hipSuccess;
     FlatArgs A{};
@@ -1136,10 +1137,10 @@ hipError_t launch_flat(const SealArgs *sa, const OpenArgs *oa, bool balance, uin
     A.wchk = kCoopWChk;
     const uint32_t lds = kFlatLdsBytes;
     const bool win = (sa ? sa->buf_len : oa->buf_len) < 0x7FFFFFF0ull; // frame offsets below 2 GiB
-    if (sa && win) hipLaunchKernelGGL((flat_kernel<false, true>), dim3(blocks), dim3(64 * kFlatWaves), lds, s, A);
-    else if (sa) hipLaunchKernelGGL((flat_kernel<false, false>), dim3(blocks), dim3(64 * kFlatWaves), lds, s, A);
-    else if (win) hipLaunchKernelGGL((flat_kernel<true, true>), dim3(blocks), dim3(64 * kFlatWaves), lds, s, A);
-    else hipLaunchKernelGGL((flat_kernel<true, false>), dim3(blocks), dim3(64 * kFlatWaves), lds, s, A);
+    if (sa && win) RG_LAUNCH(done, (flat_kernel<false, true>), dim3(blocks), dim3(64 * kFlatWaves), lds, s, A);
+    else if (sa) RG_LAUNCH(done, (flat_kernel<false, false>), dim3(blocks), dim3(64 * kFlatWaves), lds, s, A);
+    else if (win) RG_LAUNCH(done, (flat_kernel<true, true>), dim3(blocks), dim3(64 * kFlatWaves), lds, s, A);
+    else RG_LAUNCH(done, (flat_kernel<true, false>), dim3(blocks), dim3(64 * kFlatWaves), lds, s, A);
     return hipGetLastError();
 }
 

@@ -1,5 +1,6 @@
 // rg_internal.h -- declarations shared by the kernel TU and the C-ABI TU.
 #pragma once
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -77,7 +78,18 @@ struct Launch {
     int debug_mode; // diagnostics: 0 normal, 1/2 seal compute/memory only, 3 staged stamps
     int staged_g;   // kernel family: 0 pipelined lanes (rg_pipe.hip), 1/2 LDS-staged tiles of that window (rg_tile.hip),
                     // 3 flattened chunk stream (rg_flat.hip)
+    hipEvent_t done; // recorded by the transport kernel's own dispatch (hipExtLaunchKernel's stop event: no
+                     // extra queue packet; the device API's stream check, rg_api.cpp), or nullptr
 };
+
+// A transport launch, with its stop event when one is asked for: recorded as the kernel completes, by
+// the dispatch itself (a separate hipEventRecord is one more queue packet between back-to-back launches:
+// +3 us on an eagerly launched config-2 seal, round 6).
+#define RG_LAUNCH(done, kernel, grid, block, lds, stream, ...)                                              \
+    do {                                                                                                   \
+        if (done) hipExtLaunchKernelGGL(kernel, grid, block, lds, stream, nullptr, done, 0u, __VA_ARGS__); \
+        else hipLaunchKernelGGL(kernel, grid, block, lds, stream, __VA_ARGS__);                            \
+    } while (0)
 constexpr uint32_t kLdsPerCu = 160u * 1024u;
 
 // Size-class work lists built by the planner (rg_tile.hip).  counts == nullptr:
@@ -238,7 +250,8 @@ hipError_t launch_pipe(const SealArgs *sa, const OpenArgs *oa, const Launch &L, 
 // work (balance) or equal packet counts; the chunks of a unit are dealt evenly
 // over the wave's 64 lanes.
 constexpr uint32_t kFlatGroup = 1024;
-hipError_t launch_flat(const SealArgs *sa, const OpenArgs *oa, bool balance, uint4 *junk, int cus, hipStream_t s);
+hipError_t launch_flat(const SealArgs *sa, const OpenArgs *oa, bool balance, uint4 *junk, int cus, hipStream_t s,
+                       hipEvent_t done = nullptr);
 uint32_t flat_junk_bytes(int cus);
 hipError_t prepare_flat_kernels();
 hipError_t prepare_pipe_kernels(int max_wg[2]); // [seal, open] resident 256-thread workgroups per CU

@@ -786,7 +786,7 @@ hipError_t launch_pipe(const SealArgs *sa, const OpenArgs *oa, const Launch &L, 
     }
     const uint32_t fl = lg | (lds >= 4 * kRingBytes ? kPipeLinesFlag : 0u);
     if (oa) {
-        hipLaunchKernelGGL(pipe_open_kernel, dim3(blocks), dim3(256), lds, s, *oa, fl, pp);
+        RG_LAUNCH(L.done, pipe_open_kernel, dim3(blocks), dim3(256), lds, s, *oa, fl, pp);
         return hipGetLastError();
     }
 #if RG_DIAG
@@ -801,7 +801,7 @@ hipError_t launch_pipe(const SealArgs *sa, const OpenArgs *oa, const Launch &L, 
     default: break;
     }
 #endif
-    hipLaunchKernelGGL(pipe_seal_kernel<0>, dim3(blocks), dim3(256), lds, s, *sa, fl, pp);
+    RG_LAUNCH(L.done, pipe_seal_kernel<0>, dim3(blocks), dim3(256), lds, s, *sa, fl, pp);
     return hipGetLastError();
 }
 

@@ -753,6 +753,7 @@ __global__ __launch_bounds__(512) void tile_kernel(SealArgs sa, OpenArgs oa, Til
         uint64_t *dbg = OPEN ? oa.dbg : sa.dbg;
         if (dbg && lane == 0) {
             uint64_t *o = dbg + 8 * (blockIdx.x * 8 + wave);
+            const uint64_t rt1 = realtime();
             o[0] = t_setup;
             o[1] = t_store;
             o[2] = t_issue;
@@ -760,7 +761,14 @@ __global__ __launch_bounds__(512) void tile_kernel(SealArgs sa, OpenArgs oa, Til
             o[4] = t_chunk;
             o[5] = t_tail;
             o[6] = 1;
-            o[7] = realtime() - rt0;
+            o[7] = rt1 - rt0;
+            // second block of rows (after gridDim.x x 8 waves): wall-clock start / end (100 MHz), the
+            // wave's items and XCC_ID << 32 | HW_ID (round 6: the shard-size attribution, tools/shard_attrib.py)
+            uint64_t *o2 = dbg + 8 * ((uint64_t)gridDim.x * 8 + blockIdx.x * 8 + wave);
+            o2[0] = rt0;
+            o2[1] = rt1;
+            o2[2] = gen;
+            o2[3] = ((uint64_t)(uint32_t)__builtin_amdgcn_s_getreg(0xF814) << 32) | (uint32_t)__builtin_amdgcn_s_getreg(0xF804);
         }
     }
     if (R) {
@@ -841,12 +849,12 @@ hipError_t launch_tiles(const SealArgs *sa, const OpenArgs *oa, int G, const Til
     if (L.debug_mode == 3) {                                                                                  \
         if (sa) hipLaunchKernelGGL((tile_kernel<GG, false, true>), dim3(blocks), dim3(threads), lds, s, a, b, tp); \
         else hipLaunchKernelGGL((tile_kernel<GG, true, true>), dim3(blocks), dim3(threads), lds, s, a, b, tp);     \
-    } else if (sa) hipLaunchKernelGGL((tile_kernel<GG, false>), dim3(blocks), dim3(threads), lds, s, a, b, tp);   \
-    else hipLaunchKernelGGL((tile_kernel<GG, true>), dim3(blocks), dim3(threads), lds, s, a, b, tp);
+    } else if (sa) RG_LAUNCH(L.done, (tile_kernel<GG, false>), dim3(blocks), dim3(threads), lds, s, a, b, tp);    \
+    else RG_LAUNCH(L.done, (tile_kernel<GG, true>), dim3(blocks), dim3(threads), lds, s, a, b, tp);
 #else
 #define RG_TILES(GG)                                                                                          \
-    if (sa) hipLaunchKernelGGL((tile_kernel<GG, false>), dim3(blocks), dim3(threads), lds, s, a, b, tp);      \
-    else hipLaunchKernelGGL((tile_kernel<GG, true>), dim3(blocks), dim3(threads), lds, s, a, b, tp);
+    if (sa) RG_LAUNCH(L.done, (tile_kernel<GG, false>), dim3(blocks), dim3(threads), lds, s, a, b, tp);       \
+    else RG_LAUNCH(L.done, (tile_kernel<GG, true>), dim3(blocks), dim3(threads), lds, s, a, b, tp);
 #endif
     if (G == 1) {
         RG_TILES(1)

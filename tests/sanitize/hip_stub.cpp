@@ -246,7 +246,9 @@ hipError_t launch_tiles(const SealArgs *sa, const OpenArgs *oa, int, const TileP
     if (tp.gq && tp.gq[0] != 0) return hipSuccess; // stale pool (test hook): emulated as nothing taken
     return run(sa, oa);
 }
-hipError_t launch_flat(const SealArgs *sa, const OpenArgs *oa, bool, uint4 *, int, hipStream_t) { return run(sa, oa); }
+hipError_t launch_flat(const SealArgs *sa, const OpenArgs *oa, bool, uint4 *, int, hipStream_t, hipEvent_t) {
+    return run(sa, oa);
+}
 
 hipError_t launch_general(GeneralJob *jobs, uint32_t njobs, uint8_t *arena, hipStream_t) {
     for (uint32_t i = 0; i < njobs; ++i) {

@@ -464,3 +464,33 @@ def _alternate(group, rng, kt, rec):
         for k in (0, n // 2, n - 1):
             o = int(desc["offset"][k]) + 16
             assert np.array_equal(got[o:o + 1504], buf[o:o + 1504]), f"open {i} packet {k}"
+
+
+def test_numa_placed_buffer_round_trip():
+    """Round 6: rg_numa_node names a node (or -1), and a frame buffer placed for a group
+    -- each context's part bound to its context's node (rg_numa_bind), first-touched, pinned
+    (rg_host_register) -- seals and opens bit-exactly against the oracle through the group."""
+    import numpy as np
+
+    from oracle import oracle
+    from rustyguard_amd import aead, workloads
+    from rustyguard_amd.aead import Group
+
+    g = Group([0, 0])
+    try:
+        for k in range(2):
+            assert aead.numa_node(g.engine(k)) >= -1
+        w = workloads.uniform(3000, 576, name="t")
+        buf, placement = aead.placed_host_buffer(g, w.desc, w.buf_bytes)
+        assert [p["context"] for p in placement] == [0, 1] and sum(p["packets"] for p in placement) == w.n
+        rng = np.random.default_rng(5)
+        buf[:] = rng.integers(0, 256, buf.nbytes, dtype=np.uint8)
+        plain = buf.copy()
+        want = plain.copy()
+        oracle.seal_batch(w.keys, w.receivers, w.desc, w.counters, want)
+        st = g.seal_host(w.keys, w.receivers, w.desc, w.counters, buf)
+        assert (st == 0).all() and np.array_equal(buf, want)
+        st2, _ = g.open_host(w.keys, w.open_desc(), buf)
+        assert (st2 == 0).all()
+    finally:
+        g.close()

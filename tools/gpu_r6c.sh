@@ -1,0 +1,9 @@
+set -u
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+tools/gpu_run.sh testall || exit $?
+echo "== ab cfg2 mark"; tools/ab.sh "base nomark" "cfg2" 3 || exit $?
+echo "== shard_attrib"; RG_AEAD_LIB=tools/build/librg_diag.so timeout -k 10 300 python tools/shard_attrib.py 1 2 4 8 > gpurun_out/shard_attrib.jsonl 2> gpurun_out/shard_attrib.err || exit $?
+cat gpurun_out/shard_attrib.jsonl
+echo "== numa_e2e"; timeout -k 10 300 python tools/numa_e2e.py > gpurun_out/numa_e2e.json 2> gpurun_out/numa_e2e.err || exit $?
+cat gpurun_out/numa_e2e.json; ls /sys/devices/system/node/; cat /sys/fs/cgroup/cpuset.mems.effective 2>/dev/null; cat /sys/fs/cgroup/cpu.max 2>/dev/null; nproc
