@@ -470,6 +470,28 @@ struct DeviceGuard {
     }
 };
 
+// The host NUMA node closest to a GPU, -1 if unknown.  HIP's attribute first; this runtime answers it with
+// hipErrorInvalidValue (round 6 box), and a failed query stays the thread's last error, which the next
+// launch's hipGetLastError (and PyTorch's checks) then report -- so it is cleared, and the node is read
+// from the device's PCI function in sysfs instead.
+int gpu_numa_node(int device) {
+    int node = -1;
+    if (hipDeviceGetAttribute(&node, hipDeviceAttributeHostNumaId, device) == hipSuccess && node >= 0) return node;
+    (void)hipGetLastError();
+    char bus[32] = {0};
+    if (hipDeviceGetPCIBusId(bus, (int)sizeof bus, device) != hipSuccess) {
+        (void)hipGetLastError();
+        return -1;
+    }
+    for (char *p = bus; *p; ++p) *p = (char)((*p >= 'A' && *p <= 'F') ? *p - 'A' + 'a' : *p); // sysfs: lower case
+    const std::string path = std::string("/sys/bus/pci/devices/") + bus + "/numa_node";
+    FILE *f = std::fopen(path.c_str(), "r");
+    if (!f) return -1;
+    if (std::fscanf(f, "%d", &node) != 1) node = -1;
+    std::fclose(f);
+    return node >= 0 ? node : -1;
+}
+
 int check_ctx(rg_ctx *ctx) {
     if (!ctx) return set_err(RG_EINVAL, "null context");
     hipError_t e = hipSetDevice(ctx->device);
@@ -547,8 +569,7 @@ int rg_create(int device, rg_ctx **out) {
     c->h_general.secret = true;
     {
         hipError_t e = hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device);
-        if (e == hipSuccess && hipDeviceGetAttribute(&c->numa_node, hipDeviceAttributeHostNumaId, device) != hipSuccess)
-            c->numa_node = -1;
+        if (e == hipSuccess) c->numa_node = gpu_numa_node(device);
         if (e == hipSuccess) e = rg::prepare_tile_kernels();
         if (e == hipSuccess) e = rg::prepare_pipe_kernels(c->pipe_max_wg);
         if (e == hipSuccess) e = rg::prepare_flat_kernels();

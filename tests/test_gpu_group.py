@@ -470,12 +470,6 @@ def test_numa_placed_buffer_round_trip():
     """Round 6: rg_numa_node names a node (or -1), and a frame buffer placed for a group
     -- each context's part bound to its context's node (rg_numa_bind), first-touched, pinned
     (rg_host_register) -- seals and opens bit-exactly against the oracle through the group."""
-    import numpy as np
-
-    from oracle import oracle
-    from rustyguard_amd import aead, workloads
-    from rustyguard_amd.aead import Group
-
     g = Group([0, 0])
     try:
         for k in range(2):
@@ -494,3 +488,17 @@ def test_numa_placed_buffer_round_trip():
         assert (st2 == 0).all()
     finally:
         g.close()
+
+
+def test_create_leaves_no_hip_error_pending():
+    """rg_create's NUMA query: this runtime answers hipDeviceAttributeHostNumaId with an error, and a failed
+    query stays the thread's last HIP error, which the next launch (ours, or PyTorch's checks) then reported
+    as its own failure.  rg_create clears it and reads the node from sysfs."""
+    eng = Engine(0)
+    try:
+        assert _hip().hipGetLastError() == 0
+        assert aead.numa_node(eng) >= -1
+        x = torch.arange(1024, device="cuda")
+        assert int((x + 1).sum().item()) == 1024 * 1025 // 2
+    finally:
+        eng.close()

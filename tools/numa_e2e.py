@@ -43,7 +43,7 @@ def main():
         rc = L.rg_numa_bind(p, buf.nbytes, node)
         if rc != 0:
             out["runs"].append({"node": node, "refused": L.rg_last_error().decode()})
-            del buf
+            del p, buf  # the exported pointers into the mapping go before it closes
             mm.close()
             continue
         buf[:] = plain  # first touch: the pages land on the bound node
@@ -69,7 +69,7 @@ def main():
         out["runs"].append({"node": node, "local": node == gpu_node, "seal_ms": round(sm * 1e3, 3),
                             "open_ms": round(om * 1e3, 3), "seal_gib_s": round(pay / sm / 2**30, 2),
                             "open_gib_s": round(pay / om / 2**30, 2), "round_trip_ok": ok})
-        del buf
+        del p, buf
         mm.close()
     print(json.dumps(out), flush=True)
     eng.close()
