@@ -117,6 +117,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="CPU baseline budget: port and OpenSSL, 1 thread and all cores, 5 runs each (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="all-core thread count (0 = this host's share)")
+    ap.add_argument("--cpu-study", action="store_true",
+                    help="only the CPU baselines' scaling study (free / pinned / pinned + private slices), no GPU")
     ap.add_argument("--e2e", action="store_true", help="also time the pinned host->GPU->host path")
     ap.add_argument("--single-process", action="store_true",
                     help="one process and one thread drive all --gpus N GPUs (rg_group: config 5's split, "
@@ -201,11 +203,72 @@ def all_core_threads(requested: int):
 CPU_SAMPLE = 65536  # packets: >= 64 Ki; config 2's whole batch
 
 
-def cpu_rate(w, impl: str, threads: int, rep_seconds: float, reps: int = 3):
+def cgroup_throttle():
+    """(periods throttled, µs throttled) of the job's cgroup (v2 cpu.stat), or None: the CPU quota at work."""
+    try:
+        d = {}
+        with open("/sys/fs/cgroup/cpu.stat") as f:
+            for line in f:
+                k, v = line.split()
+                d[k] = int(v)
+        return d.get("nr_throttled", 0), d.get("throttled_usec", 0)
+    except (OSError, ValueError):
+        return None
+
+
+def _cpulist(text: str):
+    out = []
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        a, _, b = part.partition("-")
+        out.extend(range(int(a), int(b or a) + 1))
+    return out
+
+
+def pick_cpus(n: int, node=None):
+    """n CPUs of this process's affinity mask for pinned baseline workers: one hardware thread per core
+    (the first sibling), on one NUMA node -- `node` if it has n, else the node with the most -- so that
+    the workers neither migrate nor share a core; None if the mask cannot give n."""
+    aff = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else []
+    allowed = set(aff)
+
+    def first_siblings(cpus):
+        seen, out = set(), []
+        for c in cpus:
+            try:
+                with open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list") as f:
+                    sib = tuple(_cpulist(f.read()))
+            except OSError:
+                sib = (c,)
+            if sib not in seen:
+                seen.add(sib)
+                out.append(c)
+        return out
+
+    nodes = {}
+    try:
+        for d in os.listdir("/sys/devices/system/node"):
+            if d.startswith("node") and d[4:].isdigit():
+                with open(f"/sys/devices/system/node/{d}/cpulist") as f:
+                    nodes[int(d[4:])] = first_siblings([c for c in _cpulist(f.read()) if c in allowed])
+    except OSError:
+        nodes = {}
+    if not nodes:
+        nodes = {0: first_siblings(aff)}
+    order = sorted(nodes, key=lambda k: (k != node, -len(nodes[k])))
+    for k in order:
+        if len(nodes[k]) >= n:
+            return nodes[k][:n]
+    return None
+
+
+def cpu_rate(w, impl: str, threads: int, rep_seconds: float, reps: int = 3, cpus=None, local: bool = False):
     """Median of `reps` timed runs of seal+open over a sample of the workload (its first CPU_SAMPLE
     packets) by a persistent pool of `threads` workers (oracle/rg_openssl_batch.c rg_cpu_bench: threads
     and OpenSSL cipher contexts live for the whole run, one untimed round first): GiB/s of payload and
-    Mpkt/s."""
+    Mpkt/s.  cpus pins worker t to cpus[t]; local gives each worker a first-touched private copy of its
+    slice.  throttled_ms: the cgroup's CPU-quota throttling during the runs."""
     from oracle import oracle  # checker / baseline only
 
     n = min(w.n, CPU_SAMPLE)
@@ -219,18 +282,24 @@ def cpu_rate(w, impl: str, threads: int, rep_seconds: float, reps: int = 3):
     ctr = w.counters[:n]
     payload = int(desc["len"].astype(np.int64).sum())
     runs = []
+    th0 = cgroup_throttle()
     for _ in range(reps):
-        el, rounds = oracle.cpu_bench(impl, threads, w.keys, w.receivers, desc, ctr, buf, rep_seconds)
+        el, rounds = oracle.cpu_bench(impl, threads, w.keys, w.receivers, desc, ctr, buf, rep_seconds,
+                                      cpus=cpus, local=local)
         runs.append((2 * payload * rounds / el / 2**30, 2 * n * rounds / el / 1e6))
+    th1 = cgroup_throttle()
     pay = np.zeros(span, bool)  # payload bytes (headers and tags are rewritten by every seal)
     for o, ln in zip(desc["offset"].astype(np.int64), desc["len"].astype(np.int64)):
         pay[o + 16:o + 16 + ln] = True
     assert np.array_equal(buf[pay], plain[pay]), "a seal+open round did not give the plaintext back"
     gib = sorted(r[0] for r in runs)[reps // 2]
     mpkt = sorted(r[1] for r in runs)[reps // 2]
-    return {"value": round(gib, 4), "unit": "GiB/s", "cores": threads, "mpkt_s": round(mpkt, 4),
-            "runs_gib_s": [round(r[0], 4) for r in runs], "median_of": reps, "n_sample": n,
-            "mean_payload": round(payload / n, 1)}
+    out = {"value": round(gib, 4), "unit": "GiB/s", "cores": threads, "mpkt_s": round(mpkt, 4),
+           "runs_gib_s": [round(r[0], 4) for r in runs], "median_of": reps, "n_sample": n,
+           "mean_payload": round(payload / n, 1)}
+    if th0 is not None and th1 is not None:
+        out["throttled_ms"] = round((th1[1] - th0[1]) / 1000.0, 1)
+    return out
 
 
 def cpu_baselines(w, seconds: float, threads_how):
@@ -265,6 +334,39 @@ def cpu_baselines(w, seconds: float, threads_how):
         d.update(info)
         out[impl] = d
     return out.get("port"), out.get("openssl")
+
+
+def cpu_study(args):
+    """The all-core CPU baseline's scaling, without the GPU (bench.py --cpu-study): each
+    implementation on 1 thread and on the host's share, with the workers free to migrate (the default
+    line's pool), pinned one per core on one NUMA node, and pinned with a private first-touched copy of
+    their slice; plus the pinned, private run on one thread fewer than the quota.  The cgroup's CPU-quota
+    throttling is read beside each run."""
+    from oracle import oracle
+    from rustyguard_amd import workloads
+
+    w = workloads.build("cfg2")
+    threads, limits = all_core_threads(args.cpu_threads)
+    cpus = pick_cpus(threads)
+    rep = max(0.3, args.cpu_seconds / 24)
+    res = {"threads": threads, "thread_limits": limits, "cpus": cpus, **host_cpu_info(), "rep_seconds": rep,
+           "runs": []}
+    impls = ["port"] + (["openssl"] if oracle.openssl_available() else [])
+    modes = [("free", None, False), ("pinned", cpus, False), ("pinned+local", cpus, True)]
+    for impl in impls:
+        for name, cp, loc in modes:
+            if name != "free" and cp is None:
+                continue
+            one = cpu_rate(w, impl, 1, rep, cpus=cp[:1] if cp else None, local=loc)
+            for t in ([threads] + ([threads - 1] if name == "pinned+local" and threads > 2 else [])):
+                many = cpu_rate(w, impl, t, rep, cpus=cp[:t] if cp else None, local=loc)
+                res["runs"].append({"impl": impl, "mode": name, "threads": t, "gib_s": many["value"],
+                                    "runs_gib_s": many["runs_gib_s"], "one_thread_gib_s": one["value"],
+                                    "speedup": round(many["value"] / one["value"], 2),
+                                    "efficiency": round(many["value"] / (t * one["value"]), 3),
+                                    "throttled_ms": many.get("throttled_ms")})
+                print(json.dumps(res["runs"][-1]), file=sys.stderr, flush=True)
+    print(json.dumps(res), flush=True)
 
 
 def bench_cfg1(args):
@@ -746,6 +848,9 @@ def main():
         sys.exit(2)
     if args.workload == "cfg1":
         bench_cfg1(args)
+        return
+    if args.cpu_study:
+        cpu_study(args)
         return
     workload = args.workload or ("cfg2" if world == 1 else "cfg5")
     if args.dry_run:

@@ -63,7 +63,7 @@ def lib():
         L.rg_openssl_open_batch.argtypes = [u8p, u8p, ctypes.c_size_t, u8p, u8p, ctypes.c_int]
         L.rg_openssl_open_batch.restype = ctypes.c_int
         L.rg_cpu_bench.argtypes = [ctypes.c_int, ctypes.c_int, u8p, u8p, u8p, u8p, ctypes.c_size_t, u8p,
-                                   ctypes.c_double, u8p]
+                                   ctypes.c_double, u8p, ctypes.c_int, u8p]
         L.rg_cpu_bench.restype = ctypes.c_int
         L.rg_cpu_time_one.argtypes = [ctypes.c_int, u8p, ctypes.c_uint32, ctypes.c_uint64, u8p]
         L.rg_cpu_time_one.restype = ctypes.c_int
@@ -240,16 +240,22 @@ def openssl_open_batch(keys, desc, buf, nthreads=1):
     return status[: len(desc)]
 
 
-def cpu_bench(impl: str, nthreads: int, keys, receivers, desc, counters, buf, seconds: float):
+def cpu_bench(impl: str, nthreads: int, keys, receivers, desc, counters, buf, seconds: float, cpus=None,
+              local: bool = False):
     """CPU baseline harness (rg_openssl_batch.c rg_cpu_bench): a persistent pool of `nthreads` workers
     seals then opens its slice of the sample in rounds for `seconds`; impl "port" (the C restatement) or
-    "openssl" (EVP, one cipher context per worker, re-keyed per packet).  Returns (elapsed_s, rounds)."""
+    "openssl" (EVP, one cipher context per worker, re-keyed per packet).  cpus: one CPU per worker to pin
+    it to; local: each worker works on its own first-touched copy of its slice (written back at the end).
+    Returns (elapsed_s, rounds)."""
     keys = np.ascontiguousarray(keys, dtype=np.uint8)
     counters = np.ascontiguousarray(counters, dtype=np.uint64)
     rec = None if receivers is None else np.ascontiguousarray(receivers, dtype=np.uint32)
     out = np.zeros(3, np.float64)
+    cp = None if cpus is None else np.ascontiguousarray(list(cpus)[:nthreads], dtype=np.int32)
+    if cp is not None and len(cp) < nthreads:
+        raise ValueError("cpu_bench: fewer CPUs than threads")
     rc = lib().rg_cpu_bench(1 if impl == "openssl" else 0, nthreads, _ptr(keys), _ptr(rec), _ptr(desc),
-                            _ptr(counters), len(desc), _ptr(buf), seconds, _ptr(out))
+                            _ptr(counters), len(desc), _ptr(buf), seconds, _ptr(cp), 1 if local else 0, _ptr(out))
     if rc != 0:
         raise RuntimeError(f"rg_cpu_bench({impl}, {nthreads}) failed: {rc}")
     if out[2] != 0:

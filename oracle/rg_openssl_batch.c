@@ -231,6 +231,9 @@ int rg_cpu_time_one(int impl, const uint8_t key[32], uint32_t P, uint64_t iters,
  * round seals the slice then opens it again (the frames return to plaintext, so every round does the same
  * work).  One untimed round first; then rounds until `seconds` have passed.
  * impl 0: the C restatement (rg_oracle_seal_one / _open_one); 1: OpenSSL EVP, re-keyed per packet.
+ * cpus (optional, nthreads entries): worker t runs on CPU cpus[t] only.  local != 0: each worker works on a
+ * private copy of its slice's frames, allocated and first-touched by itself (its NUMA node, its caches),
+ * copied back into buf at the end.
  * out[0] = elapsed seconds of the timed rounds, out[1] = timed rounds, out[2] = packets whose seal or open
  * failed (0 expected). */
 #include <sched.h>
@@ -244,6 +247,8 @@ typedef struct {
     uint8_t *buf;
     size_t n;
     int nthreads;
+    const int *cpus;
+    int local;
     pthread_barrier_t start, done;
     volatile int stop;
     volatile uint64_t bad;
@@ -255,15 +260,15 @@ typedef struct {
     int t;
 } pool_arg_t;
 
-static uint64_t pool_round(pool_t *p, EVP_CIPHER_CTX *c, size_t lo, size_t hi) {
+static uint64_t pool_round(pool_t *p, uint8_t *bufp, EVP_CIPHER_CTX *c, size_t lo, size_t hi) {
     uint64_t bad = 0;
     uint8_t nonce[12], st = 0;
     int outl = 0;
     for (size_t i = lo; i < hi; i++) { /* seal: desc.len = P */
         const rg_oracle_desc *d = &p->desc[i];
-        uint8_t *frame = p->buf + d->offset;
+        uint8_t *frame = bufp + d->offset;
         if (p->impl == 0) {
-            rg_oracle_seal_one(p->keys, p->receivers, d, p->counters[i], p->buf, &st);
+            rg_oracle_seal_one(p->keys, p->receivers, d, p->counters[i], bufp, &st);
             bad += st != RG_ORACLE_OK;
         } else {
             int ok = 1;
@@ -281,9 +286,9 @@ static uint64_t pool_round(pool_t *p, EVP_CIPHER_CTX *c, size_t lo, size_t hi) {
     for (size_t i = lo; i < hi; i++) { /* open the frames just sealed: W = P + 32 */
         rg_oracle_desc d = p->desc[i];
         d.len += 32;
-        uint8_t *frame = p->buf + d.offset;
+        uint8_t *frame = bufp + d.offset;
         if (p->impl == 0) {
-            rg_oracle_open_one(p->keys, &d, p->buf, &st, NULL);
+            rg_oracle_open_one(p->keys, &d, bufp, &st, NULL);
             bad += st != RG_ORACLE_OK;
         } else {
             int ok = 1;
@@ -303,6 +308,31 @@ static void *pool_worker(void *arg) {
     pool_arg_t *a = (pool_arg_t *)arg;
     pool_t *p = a->p;
     const size_t lo = p->n * (size_t)a->t / (size_t)p->nthreads, hi = p->n * (size_t)(a->t + 1) / (size_t)p->nthreads;
+    if (p->cpus) {
+        cpu_set_t set;
+        CPU_ZERO(&set);
+        CPU_SET(p->cpus[a->t], &set);
+        (void)pthread_setaffinity_np(pthread_self(), sizeof set, &set);
+    }
+    /* the frames this worker touches: [desc[lo].offset, end of desc[hi - 1]'s frame) when the slice is in
+     * offset order (the workloads' layout); a private copy rebases the same offsets onto it */
+    uint8_t *bufp = p->buf, *priv = NULL;
+    size_t base = 0, span = 0;
+    if (p->local && hi > lo) {
+        base = (size_t)p->desc[lo].offset;
+        size_t end = base;
+        for (size_t i = lo; i < hi; i++) {
+            const size_t e = (size_t)p->desc[i].offset + p->desc[i].len + 32;
+            if ((size_t)p->desc[i].offset < base) base = (size_t)p->desc[i].offset;
+            if (e > end) end = e;
+        }
+        span = end - base;
+        priv = (uint8_t *)malloc(span);
+        if (priv) {
+            memcpy(priv, p->buf + base, span); /* first touch by this worker */
+            bufp = priv - base;
+        }
+    }
     EVP_CIPHER_CTX *c = NULL;
     if (p->impl == 1) { /* one context for the worker's lifetime, the cipher bound once */
         c = ssl.ctx_new();
@@ -312,10 +342,14 @@ static void *pool_worker(void *arg) {
     for (;;) {
         pthread_barrier_wait(&p->start);
         if (p->stop) break;
-        bad += pool_round(p, c, lo, hi);
+        bad += pool_round(p, bufp, c, lo, hi);
         pthread_barrier_wait(&p->done);
     }
     if (c) ssl.ctx_free(c);
+    if (priv) { /* the slices do not overlap: each worker writes back its own frames */
+        memcpy(p->buf + base, priv, span);
+        free(priv);
+    }
     pthread_mutex_lock(&p->mu);
     p->bad += bad;
     pthread_mutex_unlock(&p->mu);
@@ -323,7 +357,8 @@ static void *pool_worker(void *arg) {
 }
 
 int rg_cpu_bench(int impl, int nthreads, const uint8_t *keys, const uint32_t *receivers, const rg_oracle_desc *desc,
-                 const uint64_t *counters, size_t n, uint8_t *buf, double seconds, double out[3]) {
+                 const uint64_t *counters, size_t n, uint8_t *buf, double seconds, const int *cpus, int local,
+                 double out[3]) {
     if (impl == 1 && !rg_openssl_available()) return -1;
     if (nthreads < 1 || nthreads > 256 || n == 0) return -2;
     pool_t p;
@@ -336,6 +371,22 @@ int rg_cpu_bench(int impl, int nthreads, const uint8_t *keys, const uint32_t *re
     p.buf = buf;
     p.n = n;
     p.nthreads = nthreads;
+    p.cpus = cpus;
+    p.local = local;
+    if (local) { /* private copies are written back whole: the slices' frame spans must not overlap */
+        size_t prev_end = 0;
+        for (int t = 0; t < nthreads; t++) {
+            const size_t lo = n * (size_t)t / (size_t)nthreads, hi = n * (size_t)(t + 1) / (size_t)nthreads;
+            if (hi <= lo) continue;
+            size_t b = (size_t)desc[lo].offset, e = b;
+            for (size_t i = lo; i < hi; i++) {
+                if ((size_t)desc[i].offset < b) b = (size_t)desc[i].offset;
+                if ((size_t)desc[i].offset + desc[i].len + 32 > e) e = (size_t)desc[i].offset + desc[i].len + 32;
+            }
+            if (b < prev_end) return -4;
+            prev_end = e;
+        }
+    }
     pthread_barrier_init(&p.start, NULL, (unsigned)nthreads + 1);
     pthread_barrier_init(&p.done, NULL, (unsigned)nthreads + 1);
     pthread_mutex_init(&p.mu, NULL);

@@ -13,9 +13,8 @@ and the number of tiles it took.  Per shard size and op (seal, open), median ove
   tail_us      last wave end - mean wave end (the spread the launch waits for)
   wave_us      mean wave life; tiles per wave (min / mean / max); setup cycles per wave (mean)
   per_tile_us  mean wave life / mean tiles: the rate a wave works at once running
-  first_us     mean time of a wave's first item (start -> second item's start): the ramp's share
-  steady_us    mean time per item between the second item's start and the last item's start
-  last_us      mean time of the wave's last item (its start -> wave end); pool_items: mean pool items per wave
+  clock_ghz    the waves' cycles (the stamps' section sums) over their wall time: the clock they ran at
+  pool_items   mean grid-pool items per wave (an item is a tile or a segment of one, so items differ in size)
   usage: RG_AEAD_LIB=tools/build/librg_diag.so tools/shard_attrib.py [N ...]   (default 1 8)"""
 import json
 import os
@@ -84,12 +83,9 @@ def main():
                 a, t = a[ok], t[ok]
                 st, en = t[:, 0].astype(np.float64), t[:, 1].astype(np.float64)
                 span = (en.max() - st.min()) / 100.0
-                g = t[:, 2].astype(np.float64)
-                f, l_ = t[:, 4].astype(np.float64), t[:, 5].astype(np.float64)
-                many = (g > 2) & (f > 0)
-                rows.append({"first_us": float(((f - st)[f > 0]).mean()) / 100.0,
-                             "steady_us": float(((l_ - f)[many] / (g[many] - 2)).mean()) / 100.0,
-                             "last_us": float((en - l_).mean()) / 100.0, "pool_items": float(t[:, 6].mean())})
+                cyc = a[:, 0:6].sum(axis=1).astype(np.float64)          # the wave's cycles, section by section
+                wall = a[:, 7].astype(np.float64) * 10.0                  # ns (100 MHz ticks)
+                rows.append({"clock_ghz": float(np.median(cyc / wall)), "pool_items": float(t[:, 6].mean())})
                 rows[-1].update({"event_us": ev, "plain_us": plain, "span_us": span, "overhead_us": ev - span,
                                  "start_us": (st.max() - st.min()) / 100.0,
                              "tail_us": (en.max() - en.mean()) / 100.0,

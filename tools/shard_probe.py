@@ -5,7 +5,9 @@ Rank 0's shard of `workloads.build("cfg5", 0, N)` (8 Mi / N packets of 1500 B) s
 as bench.py's timed step does (a captured HIP graph, replayed; one event pair around `steps` replays).  On
 a node every rank has a GPU of its own and nothing is exchanged, so N x this rate is what the N-GPU line
 can reach; below it, the difference is the smaller batch per GPU (tile rounds, launch tail).
-  usage: tools/shard_probe.py [N ...]   (default 1 2 4 8)"""
+  usage: tools/shard_probe.py [N ...]   (default 1 2 4 8)
+  RG_PROBE_SEGMENTS=K / RG_PROBE_STAGED=G / RG_PROBE_PLAN=P set the tile kernel's segments per packet, its
+  window (family) and the planner before the probe (library defaults otherwise)."""
 import json
 import os
 import sys
@@ -52,6 +54,10 @@ def probe(eng, world: int, steps: int = 10) -> dict:
 def main():
     worlds = [int(x) for x in sys.argv[1:]] or [1, 2, 4, 8]
     eng = Engine(0)
+    for env, fn in (("RG_PROBE_SEGMENTS", eng.set_segments), ("RG_PROBE_STAGED", eng.set_staged),
+                    ("RG_PROBE_PLAN", eng.set_plan)):
+        if os.environ.get(env):
+            fn(int(os.environ[env]))
     for n in worlds:
         print(json.dumps(probe(eng, n)), flush=True)
 
