@@ -226,24 +226,39 @@ def _cpulist(text: str):
     return out
 
 
-def pick_cpus(n: int, node=None):
+def pick_cpus(n: int, node=None, spread_l3: bool = True):
     """n CPUs of this process's affinity mask for pinned baseline workers: one hardware thread per core
-    (the first sibling), on one NUMA node -- `node` if it has n, else the node with the most -- so that
-    the workers neither migrate nor share a core; None if the mask cannot give n."""
+    (the first sibling), on one NUMA node -- `node` if it has n, else the node with the most -- dealt
+    round-robin over the node's L3 domains (CCDs), so that the workers neither migrate nor share a core
+    and their slices spread over every L3 and CCD link; None if the mask cannot give n."""
     aff = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else []
     allowed = set(aff)
 
-    def first_siblings(cpus):
-        seen, out = set(), []
+    def read_list(path, default):
+        try:
+            with open(path) as f:
+                return tuple(_cpulist(f.read()))
+        except (OSError, ValueError):
+            return default
+
+    def spread(cpus):
+        seen, doms = set(), {}
         for c in cpus:
-            try:
-                with open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list") as f:
-                    sib = tuple(_cpulist(f.read()))
-            except OSError:
-                sib = (c,)
-            if sib not in seen:
-                seen.add(sib)
-                out.append(c)
+            sib = read_list(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list", (c,))
+            if sib in seen:
+                continue
+            seen.add(sib)
+            l3 = read_list(f"/sys/devices/system/cpu/cpu{c}/cache/index3/shared_cpu_list", ())
+            doms.setdefault(l3, []).append(c)
+        lists = [doms[k] for k in sorted(doms, key=lambda k: min(k) if k else -1)]
+        if not spread_l3:
+            return [c for lst in lists for c in lst]
+        out, i = [], 0
+        while any(lists):
+            lst = lists[i % len(lists)]
+            if lst:
+                out.append(lst.pop(0))
+            i += 1
         return out
 
     nodes = {}
@@ -251,11 +266,11 @@ def pick_cpus(n: int, node=None):
         for d in os.listdir("/sys/devices/system/node"):
             if d.startswith("node") and d[4:].isdigit():
                 with open(f"/sys/devices/system/node/{d}/cpulist") as f:
-                    nodes[int(d[4:])] = first_siblings([c for c in _cpulist(f.read()) if c in allowed])
+                    nodes[int(d[4:])] = spread([c for c in _cpulist(f.read()) if c in allowed])
     except OSError:
         nodes = {}
     if not nodes:
-        nodes = {0: first_siblings(aff)}
+        nodes = {0: spread(aff)}
     order = sorted(nodes, key=lambda k: (k != node, -len(nodes[k])))
     for k in order:
         if len(nodes[k]) >= n:
@@ -263,7 +278,52 @@ def pick_cpus(n: int, node=None):
     return None
 
 
-def cpu_rate(w, impl: str, threads: int, rep_seconds: float, reps: int = 3, cpus=None, local: bool = False):
+def cpu_mhz(cpus):
+    """Mean current clock (MHz, /proc/cpuinfo) of the given CPUs, or None where the kernel does not say."""
+    want, cur, out = set(cpus), None, []
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("processor"):
+                    cur = int(line.split(":")[1])
+                elif line.startswith("cpu MHz") and cur in want:
+                    out.append(float(line.split(":")[1]))
+    except (OSError, ValueError):
+        return None
+    return sum(out) / len(out) if out else None
+
+
+class _MhzSampler:
+    """Samples cpu_mhz(cpus) every 0.1 s on a thread while the C pool runs (ctypes drops the GIL)."""
+
+    def __init__(self, cpus):
+        import threading
+
+        self.cpus, self.samples, self.stop = cpus, [], threading.Event()
+        self.t = threading.Thread(target=self._run, daemon=True) if cpus else None
+
+    def _run(self):
+        while not self.stop.wait(0.1):
+            m = cpu_mhz(self.cpus)
+            if m is not None:
+                self.samples.append(m)
+
+    def __enter__(self):
+        if self.t:
+            self.t.start()
+        return self
+
+    def __exit__(self, *exc):
+        self.stop.set()
+        if self.t:
+            self.t.join()
+
+    def mean(self):
+        return round(sum(self.samples) / len(self.samples)) if self.samples else None
+
+
+def cpu_rate(w, impl: str, threads: int, rep_seconds: float, reps: int = 3, cpus=None, local: bool = False,
+             sample: int = CPU_SAMPLE):
     """Median of `reps` timed runs of seal+open over a sample of the workload (its first CPU_SAMPLE
     packets) by a persistent pool of `threads` workers (oracle/rg_openssl_batch.c rg_cpu_bench: threads
     and OpenSSL cipher contexts live for the whole run, one untimed round first): GiB/s of payload and
@@ -271,7 +331,7 @@ def cpu_rate(w, impl: str, threads: int, rep_seconds: float, reps: int = 3, cpus
     slice.  throttled_ms: the cgroup's CPU-quota throttling during the runs."""
     from oracle import oracle  # checker / baseline only
 
-    n = min(w.n, CPU_SAMPLE)
+    n = min(w.n, sample)
     desc = w.desc[:n].copy()
     base = int(desc["offset"][0])
     desc["offset"] -= np.uint64(base)
@@ -283,10 +343,11 @@ def cpu_rate(w, impl: str, threads: int, rep_seconds: float, reps: int = 3, cpus
     payload = int(desc["len"].astype(np.int64).sum())
     runs = []
     th0 = cgroup_throttle()
-    for _ in range(reps):
-        el, rounds = oracle.cpu_bench(impl, threads, w.keys, w.receivers, desc, ctr, buf, rep_seconds,
-                                      cpus=cpus, local=local)
-        runs.append((2 * payload * rounds / el / 2**30, 2 * n * rounds / el / 1e6))
+    with _MhzSampler(list(cpus) if cpus else None) as mhz:
+        for _ in range(reps):
+            el, rounds = oracle.cpu_bench(impl, threads, w.keys, w.receivers, desc, ctr, buf, rep_seconds,
+                                          cpus=cpus, local=local)
+            runs.append((2 * payload * rounds / el / 2**30, 2 * n * rounds / el / 1e6))
     th1 = cgroup_throttle()
     pay = np.zeros(span, bool)  # payload bytes (headers and tags are rewritten by every seal)
     for o, ln in zip(desc["offset"].astype(np.int64), desc["len"].astype(np.int64)):
@@ -299,6 +360,8 @@ def cpu_rate(w, impl: str, threads: int, rep_seconds: float, reps: int = 3, cpus
            "mean_payload": round(payload / n, 1)}
     if th0 is not None and th1 is not None:
         out["throttled_ms"] = round((th1[1] - th0[1]) / 1000.0, 1)
+    if mhz.mean() is not None:
+        out["cpu_mhz"] = mhz.mean()  # the workers' CPUs while they ran
     return out
 
 
@@ -307,30 +370,50 @@ def cpu_baselines(w, seconds: float, threads_how):
     (kind "port": the reference's Rust + graviola 0.2.0 path cannot be built here -- no cargo, crate
     not vendored) and OpenSSL EVP ChaCha20-Poly1305 (an assembly-optimised stand-in for graviola),
     each on 1 thread and on the host's share of cores, median of 3 runs over a 64 Ki-packet sample.
-    scaling = all-core rate / (threads x 1-thread rate)."""
+    Workers are pinned one per core on one NUMA node and work on private first-touched copies of their
+    slices (bench.py --cpu-study: on the GPU box this took OpenSSL from 7.0x to 9.4x on 16 threads and the
+    port from 12.5x to 15.7x).  scaling = all-core rate / (threads x 1-thread rate), with the workers'
+    clock on 1 and on N threads and the cgroup's quota throttling, which say what stops it."""
     from oracle import oracle
 
     threads, limits = threads_how
     info = host_cpu_info()
+    cpus = pick_cpus(threads)
+    local = cpus is not None
+    placement = (f"pinned one per core, spread over the L3 domains of one NUMA node (CPUs {sorted(cpus)[0]}.."
+                 f"{sorted(cpus)[-1]}), private first-touched slices"
+                 if cpus else "unpinned (the affinity mask cannot give one core per worker on one node)")
     impls = ["port"] + (["openssl"] if oracle.openssl_available() else [])
     rep = max(0.2, seconds / (len(impls) * 2 * 3))
     out = {}
     for impl in impls:
-        many = cpu_rate(w, impl, threads, rep)
-        one = cpu_rate(w, impl, 1, rep)
+        many = cpu_rate(w, impl, threads, rep, cpus=cpus, local=local)
+        one = cpu_rate(w, impl, 1, rep, cpus=cpus[:1] if cpus else None, local=local)
         what = ("C RFC 8439 restatement (oracle/rg_oracle.c)" if impl == "port" else
                 f"{oracle.openssl_version()} EVP_chacha20_poly1305, re-keyed per packet (oracle/rg_openssl_batch.c)")
         d = dict(many)
         d["kind"] = "port" if impl == "port" else "openssl (stand-in for graviola)"
-        d["one_thread"] = {"value": one["value"], "unit": "GiB/s", "mpkt_s": one["mpkt_s"],
-                           "runs_gib_s": one["runs_gib_s"]}
+        d["one_thread"] = {k: one[k] for k in ("value", "unit", "mpkt_s", "runs_gib_s", "cpu_mhz") if k in one}
         eff = many["value"] / (threads * one["value"]) if one["value"] > 0 else None
-        d["scaling"] = {"speedup": round(many["value"] / one["value"], 2) if one["value"] else None,
-                        "efficiency": round(eff, 3) if eff is not None else None, "threads": threads,
-                        "thread_limits": limits}
+        sc = {"speedup": round(many["value"] / one["value"], 2) if one["value"] else None,
+              "efficiency": round(eff, 3) if eff is not None else None, "threads": threads,
+              "thread_limits": limits, "placement": placement}
+        m1, mn = one.get("cpu_mhz"), many.get("cpu_mhz")
+        if m1 and mn:
+            sc["cpu_mhz"] = {"one_thread": m1, "all_threads": mn}
+        if "throttled_ms" in many:
+            sc["throttled_ms"] = many["throttled_ms"]
+        if eff is not None and eff < 0.9:
+            why = []
+            if m1 and mn and mn < 0.95 * m1:
+                why.append(f"the workers' clock: {m1} MHz on 1 thread, {mn} MHz on {threads}")
+            if many.get("throttled_ms"):
+                why.append(f"cgroup quota throttling {many['throttled_ms']} ms over the runs")
+            sc["limit"] = "; ".join(why) or "not identified (no clock drop or throttling seen)"
+        d["scaling"] = sc
         d["sample"] = (f"first {many['n_sample']} packets of {w.name} (mean P={many['mean_payload']}) sealed then "
-                       f"opened by a persistent pool (threads and cipher contexts kept across rounds), {rep:.2f} s "
-                       f"per run, median of 3 runs on {threads} threads and on 1 thread; {what}")
+                       f"opened by a persistent pool (threads and cipher contexts kept across rounds; {placement}), "
+                       f"{rep:.2f} s per run, median of 3 runs on {threads} threads and on 1 thread; {what}")
         d.update(info)
         out[impl] = d
     return out.get("port"), out.get("openssl")
@@ -338,10 +421,10 @@ def cpu_baselines(w, seconds: float, threads_how):
 
 def cpu_study(args):
     """The all-core CPU baseline's scaling, without the GPU (bench.py --cpu-study): each
-    implementation on 1 thread and on the host's share, with the workers free to migrate (the default
-    line's pool), pinned one per core on one NUMA node, and pinned with a private first-touched copy of
-    their slice; plus the pinned, private run on one thread fewer than the quota.  The cgroup's CPU-quota
-    throttling is read beside each run."""
+    implementation on 1 thread and on the host's share, with the workers free to migrate, pinned one per
+    core on the first cores of one NUMA node (compact), pinned spread over its L3 domains, spread with
+    private first-touched slices (the default line's placement), and that on a 16 Ki-packet sample (slices
+    that fit the L3s).  The workers' clock and the cgroup's quota throttling are read beside each run."""
     from oracle import oracle
     from rustyguard_amd import workloads
 
@@ -352,20 +435,26 @@ def cpu_study(args):
     res = {"threads": threads, "thread_limits": limits, "cpus": cpus, **host_cpu_info(), "rep_seconds": rep,
            "runs": []}
     impls = ["port"] + (["openssl"] if oracle.openssl_available() else [])
-    modes = [("free", None, False), ("pinned", cpus, False), ("pinned+local", cpus, True)]
+    compact = pick_cpus(threads, spread_l3=False)
+    res["cpus_compact"] = compact
+    # (name, cpus, private slices, sample packets)
+    modes = [("free", None, False, CPU_SAMPLE), ("compact", compact, False, CPU_SAMPLE),
+             ("spread", cpus, False, CPU_SAMPLE), ("spread+local", cpus, True, CPU_SAMPLE),
+             ("spread+local, 16 Ki sample", cpus, True, 16384)]
     for impl in impls:
-        for name, cp, loc in modes:
+        for name, cp, loc, smp in modes:
             if name != "free" and cp is None:
                 continue
-            one = cpu_rate(w, impl, 1, rep, cpus=cp[:1] if cp else None, local=loc)
-            for t in ([threads] + ([threads - 1] if name == "pinned+local" and threads > 2 else [])):
-                many = cpu_rate(w, impl, t, rep, cpus=cp[:t] if cp else None, local=loc)
-                res["runs"].append({"impl": impl, "mode": name, "threads": t, "gib_s": many["value"],
-                                    "runs_gib_s": many["runs_gib_s"], "one_thread_gib_s": one["value"],
-                                    "speedup": round(many["value"] / one["value"], 2),
-                                    "efficiency": round(many["value"] / (t * one["value"]), 3),
-                                    "throttled_ms": many.get("throttled_ms")})
-                print(json.dumps(res["runs"][-1]), file=sys.stderr, flush=True)
+            one = cpu_rate(w, impl, 1, rep, cpus=cp[:1] if cp else None, local=loc, sample=smp)
+            many = cpu_rate(w, impl, threads, rep, cpus=cp, local=loc, sample=smp)
+            res["runs"].append({"impl": impl, "mode": name, "threads": threads, "sample": smp,
+                                "gib_s": many["value"], "runs_gib_s": many["runs_gib_s"],
+                                "one_thread_gib_s": one["value"],
+                                "speedup": round(many["value"] / one["value"], 2),
+                                "efficiency": round(many["value"] / (threads * one["value"]), 3),
+                                "cpu_mhz": [one.get("cpu_mhz"), many.get("cpu_mhz")],
+                                "throttled_ms": many.get("throttled_ms")})
+            print(json.dumps(res["runs"][-1]), file=sys.stderr, flush=True)
     print(json.dumps(res), flush=True)
 
 

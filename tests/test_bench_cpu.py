@@ -9,6 +9,9 @@ import os
 import subprocess
 import sys
 
+import numpy as np
+import pytest
+
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -129,7 +132,35 @@ def test_cpu_baseline_harness_reports_scaling_and_limits():
         sc = d["scaling"]
         assert sc["threads"] == 2 and 0 < sc["efficiency"] and sc["thread_limits"] == {"requested": 2}
         assert abs(sc["speedup"] - d["value"] / d["one_thread"]["value"]) < 0.02
-        assert "persistent pool" in d["sample"]
+        assert "persistent pool" in d["sample"] and sc["placement"] in d["sample"]
+        if sc["efficiency"] < 0.9:
+            assert sc["limit"]  # the line says what stops the scaling
+
+
+def test_pick_cpus_one_per_core_on_one_node():
+    """The pinned baseline's CPUs: distinct, inside the affinity mask, at most one per physical core."""
+    bench = _bench_module()
+    aff = sorted(os.sched_getaffinity(0))
+    cpus = bench.pick_cpus(2)
+    if cpus is None:
+        pytest.skip("the affinity mask has fewer than two cores on one node")
+    assert len(cpus) == len(set(cpus)) == 2 and set(cpus) <= set(aff)
+    assert bench.pick_cpus(len(aff) + 1) is None
+    assert bench._cpulist("0-2,5,7-8") == [0, 1, 2, 5, 7, 8]
+
+
+def test_private_slices_must_not_overlap():
+    """rg_cpu_bench's private copies are written back whole, so slices whose frame spans overlap are
+    refused (-4) instead of being corrupted."""
+    from oracle import oracle
+    from rustyguard_amd import workloads
+
+    w = workloads.uniform(64, 64, name="t")
+    desc = w.desc.copy()
+    desc["offset"] = desc["offset"][::-1].copy()  # frames in reverse: the second worker's span lies below the first's
+    buf = np.zeros(int(w.buf_bytes), np.uint8)
+    with pytest.raises(RuntimeError, match="failed: -4"):
+        oracle.cpu_bench("port", 2, w.keys, w.receivers, desc, w.counters, buf, 0.05, local=True)
 
 
 def test_cgroup_quota_parser(monkeypatch, tmp_path):
