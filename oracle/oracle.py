@@ -244,7 +244,8 @@ def cpu_bench(impl: str, nthreads: int, keys, receivers, desc, counters, buf, se
               local: bool = False):
     """CPU baseline harness (rg_openssl_batch.c rg_cpu_bench): a persistent pool of `nthreads` workers
     seals then opens its slice of the sample in rounds for `seconds`; impl "port" (the C restatement) or
-    "openssl" (EVP, one cipher context per worker, re-keyed per packet).  cpus: one CPU per worker to pin
+    "openssl" (EVP, one cipher context per worker, re-keyed per packet) or "openssl-keyed-once" (the key
+    installed only when it changes: the study's measure of the re-key's cost).  cpus: one CPU per worker to pin
     it to; local: each worker works on its own first-touched copy of its slice (written back at the end).
     Returns (elapsed_s, rounds)."""
     keys = np.ascontiguousarray(keys, dtype=np.uint8)
@@ -254,7 +255,8 @@ def cpu_bench(impl: str, nthreads: int, keys, receivers, desc, counters, buf, se
     cp = None if cpus is None else np.ascontiguousarray(list(cpus)[:nthreads], dtype=np.int32)
     if cp is not None and len(cp) < nthreads:
         raise ValueError("cpu_bench: fewer CPUs than threads")
-    rc = lib().rg_cpu_bench(1 if impl == "openssl" else 0, nthreads, _ptr(keys), _ptr(rec), _ptr(desc),
+    code = {"port": 0, "openssl": 1, "openssl-keyed-once": 2}[impl]
+    rc = lib().rg_cpu_bench(code, nthreads, _ptr(keys), _ptr(rec), _ptr(desc),
                             _ptr(counters), len(desc), _ptr(buf), seconds, _ptr(cp), 1 if local else 0, _ptr(out))
     if rc != 0:
         raise RuntimeError(f"rg_cpu_bench({impl}, {nthreads}) failed: {rc}")

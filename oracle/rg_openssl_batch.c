@@ -230,7 +230,8 @@ int rg_cpu_time_one(int impl, const uint8_t key[32], uint32_t P, uint64_t iters,
  * the sample and (OpenSSL) one cipher context for its lifetime, run in rounds between two barriers; a
  * round seals the slice then opens it again (the frames return to plaintext, so every round does the same
  * work).  One untimed round first; then rounds until `seconds` have passed.
- * impl 0: the C restatement (rg_oracle_seal_one / _open_one); 1: OpenSSL EVP, re-keyed per packet.
+ * impl 0: the C restatement (rg_oracle_seal_one / _open_one); 1: OpenSSL EVP, re-keyed per packet; 2: OpenSSL
+ * EVP with the key installed only when it changes (bench.py --cpu-study only).
  * cpus (optional, nthreads entries): worker t runs on CPU cpus[t] only.  local != 0: each worker works on a
  * private copy of its slice's frames, allocated and first-touched by itself (its NUMA node, its caches),
  * copied back into buf at the end.
@@ -264,6 +265,10 @@ static uint64_t pool_round(pool_t *p, uint8_t *bufp, EVP_CIPHER_CTX *c, size_t l
     uint64_t bad = 0;
     uint8_t nonce[12], st = 0;
     int outl = 0;
+    /* impl 2 (study only): the key is installed only when it changes from the previous packet's, the nonce
+     * per packet -- what per-packet re-keying costs beyond the cipher itself */
+    const uint8_t *cur_key = NULL;
+    int cur_enc = -1;
     for (size_t i = lo; i < hi; i++) { /* seal: desc.len = P */
         const rg_oracle_desc *d = &p->desc[i];
         uint8_t *frame = bufp + d->offset;
@@ -272,8 +277,12 @@ static uint64_t pool_round(pool_t *p, uint8_t *bufp, EVP_CIPHER_CTX *c, size_t l
             bad += st != RG_ORACLE_OK;
         } else {
             int ok = 1;
+            const uint8_t *key = p->keys + 32 * (size_t)d->key_idx;
             rg_oracle_wg_nonce(p->counters[i], nonce);
-            ok &= ssl.cipher_init(c, NULL, NULL, p->keys + 32 * (size_t)d->key_idx, nonce, 1);
+            if (p->impl == 2 && key == cur_key && cur_enc == 1) ok &= ssl.cipher_init(c, NULL, NULL, NULL, nonce, 1);
+            else ok &= ssl.cipher_init(c, NULL, NULL, key, nonce, 1);
+            cur_key = key;
+            cur_enc = 1;
             ok &= ssl.cipher_update(c, frame + 16, &outl, frame + 16, (int)d->len);
             ok &= ssl.cipher_final(c, frame + 16 + d->len, &outl);
             ok &= ssl.ctrl(c, CTRL_AEAD_GET_TAG, 16, frame + 16 + d->len);
@@ -293,8 +302,12 @@ static uint64_t pool_round(pool_t *p, uint8_t *bufp, EVP_CIPHER_CTX *c, size_t l
         } else {
             int ok = 1;
             const uint32_t P = d.len - 32;
+            const uint8_t *key = p->keys + 32 * (size_t)d.key_idx;
             rg_oracle_wg_nonce(get64(frame + 8), nonce);
-            ok &= ssl.cipher_init(c, NULL, NULL, p->keys + 32 * (size_t)d.key_idx, nonce, 0);
+            if (p->impl == 2 && key == cur_key && cur_enc == 0) ok &= ssl.cipher_init(c, NULL, NULL, NULL, nonce, 0);
+            else ok &= ssl.cipher_init(c, NULL, NULL, key, nonce, 0);
+            cur_key = key;
+            cur_enc = 0;
             ok &= ssl.ctrl(c, CTRL_AEAD_SET_TAG, 16, frame + 16 + P);
             ok &= ssl.cipher_update(c, frame + 16, &outl, frame + 16, (int)P);
             ok &= ssl.cipher_final(c, frame + 16 + P, &outl) > 0;
@@ -334,7 +347,7 @@ static void *pool_worker(void *arg) {
         }
     }
     EVP_CIPHER_CTX *c = NULL;
-    if (p->impl == 1) { /* one context for the worker's lifetime, the cipher bound once */
+    if (p->impl >= 1) { /* one context for the worker's lifetime, the cipher bound once */
         c = ssl.ctx_new();
         ssl.cipher_init(c, ssl.chacha(), NULL, NULL, NULL, 1);
     }
@@ -359,7 +372,7 @@ static void *pool_worker(void *arg) {
 int rg_cpu_bench(int impl, int nthreads, const uint8_t *keys, const uint32_t *receivers, const rg_oracle_desc *desc,
                  const uint64_t *counters, size_t n, uint8_t *buf, double seconds, const int *cpus, int local,
                  double out[3]) {
-    if (impl == 1 && !rg_openssl_available()) return -1;
+    if (impl >= 1 && !rg_openssl_available()) return -1;
     if (nthreads < 1 || nthreads > 256 || n == 0) return -2;
     pool_t p;
     memset(&p, 0, sizeof p);

@@ -220,7 +220,7 @@ __global__ __launch_bounds__(512) void tile_kernel(SealArgs sa, OpenArgs oa, Til
     using Cfg = StagedCfg<G>;
     constexpr uint32_t PPW = Cfg::PPW;
     uint64_t t_setup = 0, t_store = 0, t_issue = 0, t_wait = 0, t_chunk = 0, t_tail = 0, t_mark = 0, rt0 = 0;
-    uint64_t rt_first = 0, rt_last = 0, n_pool = 0; // wall clock at the end of the first item, at the start of the last
+    uint64_t n_pool = 0; // items taken from the grid-wide pool
     if constexpr (STAMP) {
         rt0 = realtime();
         t_mark = stamp();
@@ -320,8 +320,6 @@ __global__ __launch_bounds__(512) void tile_kernel(SealArgs sa, OpenArgs oa, Til
             const uint64_t t = stamp();
             t_tail += t - t_mark;
             t_mark = t;
-            rt_last = realtime();
-            if (gen == 2) rt_first = rt_last;
             if (pooled) ++n_pool;
         }
         // ---- which bucket / tile / segment this wave works on (wave-uniform)
@@ -773,8 +771,6 @@ __global__ __launch_bounds__(512) void tile_kernel(SealArgs sa, OpenArgs oa, Til
             o2[1] = rt1;
             o2[2] = gen;
             o2[3] = ((uint64_t)(uint32_t)__builtin_amdgcn_s_getreg(0xF814) << 32) | (uint32_t)__builtin_amdgcn_s_getreg(0xF804);
-            o2[4] = rt_first; // 0: the wave took one item
-            o2[5] = rt_last;
             o2[6] = n_pool;
         }
     }
