@@ -113,8 +113,9 @@ int rg_abi_version(void);
  * have to regrow such a buffer while its stream is being captured into a graph fails with RG_EDEVICE.  A
  * block that a captured launch reads is never freed under the graph: a later regrow takes a new block and
  * keeps the captured one allocated until rg_destroy (rg_sessions_destroy for a session table's rows),
- * which zeroes and frees it; such a graph must not be replayed after that.  rg_create refuses (RG_EINVAL) to run under ROC_SYSTEM_SCOPE_SIGNAL=0: agent-scope completion
- * signals hung the host pipeline's waits in round 5 (profiles/r5_e2e_rtenv.txt). */
+ * which zeroes and frees it; such a graph must not be replayed after that.  rg_create refuses (RG_EINVAL)
+ * to run under ROC_SYSTEM_SCOPE_SIGNAL=0: agent-scope completion signals hung the host pipeline's waits in
+ * round 5 (profiles/r5_e2e_rtenv.txt). */
 int rg_create(int device, rg_ctx **out);
 void rg_destroy(rg_ctx *ctx);
 /* Text of the last error on this thread ("" if none). */
