@@ -249,7 +249,10 @@ int rg_set_debug_buffer(rg_ctx *ctx, void *dev_ptr);
  * report within rg_set_wait_timeout's limit (default 10 000 ms per wait; 1 ..
  * 3 600 000) ends the call with RG_EDEVICE ("... timed out") and every status
  * RG_PKT_PENDING, instead of blocking forever.  Waits poll (hipEventQuery),
- * yielding the CPU between polls and sleeping once a wait has run 2 ms. */
+ * yielding the CPU between polls and sleeping once a wait has run 2 ms.  The
+ * transfers of a timed-out call may still complete later: until the next host
+ * call on that context returns (it waits for them, bounded, and discards them),
+ * the frames of the failed call's buffer can still be written back. */
 int rg_set_host_slice(rg_ctx *ctx, size_t bytes);
 int rg_set_wait_timeout(rg_ctx *ctx, uint32_t ms);
 int rg_seal_batch_host(rg_ctx *ctx, const uint8_t *keys, const uint32_t *receivers, uint32_t nkeys,
