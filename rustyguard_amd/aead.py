@@ -624,6 +624,18 @@ def numa_node(engine) -> int:
     return int(engine.library.rg_numa_node(engine.handle))
 
 
+def _node_free_bytes(node: int):
+    """MemFree of a NUMA node (sysfs), or None when unreadable."""
+    try:
+        with open(f"/sys/devices/system/node/node{node}/meminfo") as f:
+            for line in f:
+                if "MemFree:" in line:
+                    return int(line.split()[-2]) * 1024
+    except (OSError, ValueError, IndexError):
+        return None
+    return None
+
+
 def placed_host_buffer(group: "Group", desc: np.ndarray, nbytes: int, open_: bool = False):
     """A frame buffer for a host batch over `group`, placed for it (include/rg_aead.h, NUMA placement): an
     anonymous mapping whose part k -- the frames of rg_split_batch's part k -- is bound to context k's NUMA
@@ -648,8 +660,13 @@ def placed_host_buffer(group: "Group", desc: np.ndarray, nbytes: int, open_: boo
             last = int(np.argmax(desc["offset"][lo:hi])) + lo
             b = min(nbytes, int(desc["offset"][last]) + int(desc["len"][last]) + (0 if open_ else 32))
             part["bytes"] = b - a
-            if node >= 0 and b > a:
+            free = _node_free_bytes(node) if node >= 0 else None
+            # a strict bind on a node without the room would leave the first touch to the OOM killer: bind
+            # only with twice the part free there (else the pages land where the kernel puts them)
+            if node >= 0 and b > a and (free is None or free >= 2 * (b - a)):
                 part["bound"] = L.rg_numa_bind(ctypes.c_void_p(p + a), b - a, node) == 0
+            elif free is not None:
+                part["unbound_reason"] = f"node {node} has {free >> 20} MiB free"
         placement.append(part)
     arr[:] = 0  # first touch: each part's pages on its node
     check(L.rg_host_register(ctypes.c_void_p(p), arr.nbytes), "rg_host_register", L)
