@@ -51,6 +51,8 @@ hipError_t hipGetDevice(int *d) {
     return hipSuccess;
 }
 hipError_t hipDeviceGetAttribute(int *pi, hipDeviceAttribute_t attr, int) {
+    // the runtime on the GPU boxes refuses the host NUMA attribute (rg_create then reads sysfs)
+    if (attr == hipDeviceAttributeHostNumaId) return hipErrorInvalidValue;
     *pi = attr == hipDeviceAttributeMultiprocessorCount ? 4 : 0;
     return hipSuccess;
 }
