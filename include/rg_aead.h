@@ -132,8 +132,9 @@ const char *rg_last_error(void);
  * kernel's work pool, see rg_set_plan); use a context per concurrent stream.  A
  * call on another stream while this context's last batch is still in flight on
  * its stream fails with RG_EINVAL and enqueues nothing (the check needs no
- * wait: an event query; launches captured into a graph are not tracked, so a
- * graph counts as work of the stream it was captured on). */
+ * wait: an event query).  Launches captured into a graph are not tracked: a
+ * caller that replays such a graph orders the replays against the context's
+ * other calls itself (same stream, or events). */
 int rg_seal_batch_dev(rg_ctx *ctx, const uint8_t *keys, const uint32_t *receivers, uint32_t nkeys,
                       const rg_pkt_desc *desc, const uint64_t *counters, size_t n, uint8_t *buf, size_t buf_len,
                       uint8_t *status, void *stream);
